@@ -1,0 +1,227 @@
+"""ctypes front end of the CPU oracle (gsr_oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module; the product never does.  It mirrors the two entry points
+of the reference extension (DGR/rasterize_points.cu:39-258):
+
+  forward(...)  -> dict(color, alpha, normal, mdepth, radii, num_rendered, state)
+  backward(...) -> dict(dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh,
+                        dsg_axis, dsg_sharpness, dsg_color, dscales, drotations)
+
+All arrays are float32/int32 numpy arrays (torch CPU tensors are accepted and
+converted).  Outputs are allocated zero-filled like torch::full / torch::zeros.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libgsr_oracle.so")
+_lib = None
+
+_f = ctypes.POINTER(ctypes.c_float)
+_i = ctypes.POINTER(ctypes.c_int)
+_u32 = ctypes.POINTER(ctypes.c_uint32)
+_u64 = ctypes.POINTER(ctypes.c_uint64)
+_u8 = ctypes.POINTER(ctypes.c_uint8)
+_d = ctypes.POINTER(ctypes.c_double)
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc) if needed."""
+    src = os.path.join(_HERE, "gsr_oracle.c")
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.gsro_forward.restype = ctypes.c_void_p
+        L.gsro_forward.argtypes = (
+            [ctypes.c_int] * 5 + [_f, ctypes.c_int, ctypes.c_int] + [_f] * 10 + [ctypes.c_float] + [_f] * 3
+            + [ctypes.c_float] * 3 + [ctypes.c_int] + [_f] * 4 + [_i, ctypes.c_int, _i])
+        L.gsro_backward.restype = ctypes.c_int
+        L.gsro_backward.argtypes = (
+            [ctypes.c_void_p] + [_f] * 11 + [ctypes.c_float] + [_f] * 3 + [ctypes.c_float] * 3 + [_i]
+            + [_f] * 7 + [_f] * 11)
+        L.gsro_free.argtypes = [ctypes.c_void_p]
+        L.gsro_set_threads.argtypes = [ctypes.c_int]
+        L.gsro_max_threads.restype = ctypes.c_int
+        L.gsro_higher_msb.argtypes = [ctypes.c_uint32]
+        L.gsro_higher_msb.restype = ctypes.c_uint32
+        L.gsro_mark_visible.argtypes = [ctypes.c_int, _f, _f, _u8]
+        L.gsro_num_rendered.argtypes = [ctypes.c_void_p]
+        L.gsro_num_rendered.restype = ctypes.c_int
+        L.gsro_get_geometry.argtypes = [ctypes.c_void_p, _f, _f, _f, _f, _f, _f, _u32, _u8]
+        L.gsro_get_binning.argtypes = [ctypes.c_void_p, _u64, _u32]
+        L.gsro_get_tiles.argtypes = [ctypes.c_void_p, _u32, _u32]
+        L.gsro_get_n_contrib.argtypes = [ctypes.c_void_p, _u32]
+        L.gsro_get_bwd_accum.argtypes = [ctypes.c_void_p, _d, _d, _d]
+        _lib = L
+    return _lib
+
+
+def set_threads(n: int) -> None:
+    lib().gsro_set_threads(int(n))
+
+
+def max_threads() -> int:
+    return lib().gsro_max_threads()
+
+
+def _np(x, dtype=np.float32):
+    if x is None:
+        return None
+    if hasattr(x, "detach"):
+        x = x.detach().cpu().numpy()
+    a = np.ascontiguousarray(np.asarray(x, dtype=dtype))
+    return None if a.size == 0 else a
+
+
+def _p(a, ty=_f):
+    return None if a is None else a.ctypes.data_as(ty)
+
+
+class State:
+    """Owns the oracle's forward state (geometry/binning/tile/image buffers)."""
+
+    def __init__(self, ptr, P, W, H, K):
+        self.ptr, self.P, self.W, self.H, self.K = ptr, P, W, H, K
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.gsro_free(self.ptr)
+            self.ptr = None
+
+    @property
+    def tiles(self):
+        return ((self.W + 15) // 16) * ((self.H + 15) // 16)
+
+    def geometry(self) -> dict:
+        P = self.P
+        out = dict(depths=np.zeros(P, np.float32), means2D=np.zeros((P, 2), np.float32),
+                   conic_opacity=np.zeros((P, 4), np.float32), rgb=np.zeros((P, 3), np.float32),
+                   ray_planes=np.zeros((P, 4), np.float32), normals=np.zeros((P, 3), np.float32),
+                   tiles_touched=np.zeros(P, np.uint32), clamped=np.zeros((P, 3), np.uint8))
+        lib().gsro_get_geometry(self.ptr, _p(out["depths"]), _p(out["means2D"]), _p(out["conic_opacity"]),
+                                _p(out["rgb"]), _p(out["ray_planes"]), _p(out["normals"]),
+                                _p(out["tiles_touched"], _u32), _p(out["clamped"], _u8))
+        return out
+
+    def binning(self) -> dict:
+        keys = np.zeros(self.K, np.uint64)
+        plist = np.zeros(self.K, np.uint32)
+        lib().gsro_get_binning(self.ptr, _p(keys, _u64), _p(plist, _u32))
+        return dict(keys=keys, point_list=plist)
+
+    def tile_state(self) -> dict:
+        ranges = np.zeros((self.tiles, 2), np.uint32)
+        mc = np.zeros(self.tiles, np.uint32)
+        lib().gsro_get_tiles(self.ptr, _p(ranges, _u32), _p(mc, _u32))
+        return dict(ranges=ranges, max_contributor=mc)
+
+    def n_contrib(self) -> np.ndarray:
+        n = np.zeros(self.W * self.H, np.uint32)
+        lib().gsro_get_n_contrib(self.ptr, _p(n, _u32))
+        return n.reshape(self.H, self.W)
+
+    def bwd_accum(self) -> dict:
+        P = self.P
+        out = dict(conic=np.zeros((P, 4)), ray_plane=np.zeros((P, 4)), normal=np.zeros((P, 3)))
+        lib().gsro_get_bwd_accum(self.ptr, _p(out["conic"], _d), _p(out["ray_plane"], _d), _p(out["normal"], _d))
+        return out
+
+
+def forward(bg, means3D, colors_precomp, opacities, scales, rotations, cov3D_precomp, sh, sg_axis, sg_sharpness,
+            sg_color, sh_degree, sg_degree, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy,
+            kernel_size, image_height, image_width, campos, prefiltered=False, require_depth=True) -> dict:
+    """Same argument list as _C.rasterize_gaussians (DGR/rasterize_points.h:18-43)."""
+    L = lib()
+    means3D = _np(means3D)
+    P = 0 if means3D is None else means3D.shape[0]
+    sh_a = _np(sh)
+    sgc = _np(sg_color)
+    SHM = 0 if sh_a is None else sh_a.shape[1]
+    SGM = 0 if sgc is None else sgc.shape[1]
+    H, W = int(image_height), int(image_width)
+    color = np.zeros((3, H, W), np.float32)
+    mdepth = np.zeros((1, H, W), np.float32)
+    alpha = np.zeros((1, H, W), np.float32)
+    normal = np.zeros((3, H, W), np.float32)
+    radii = np.zeros(P, np.int32)
+    K = ctypes.c_int(0)
+    keep = [_np(bg), means3D, _np(colors_precomp), _np(opacities), _np(scales), _np(rotations), _np(cov3D_precomp),
+            sh_a, _np(sg_axis), _np(sg_sharpness), sgc, _np(viewmatrix), _np(projmatrix), _np(campos)]
+    if P == 0:
+        return dict(num_rendered=0, color=color, alpha=alpha, normal=normal, mdepth=mdepth, radii=radii, state=None)
+    ptr = L.gsro_forward(P, int(sh_degree), SHM, int(sg_degree), SGM, _p(keep[0]), W, H, _p(keep[1]), _p(keep[2]),
+                         _p(keep[3]), _p(keep[4]), _p(keep[5]), _p(keep[6]), _p(keep[7]), _p(keep[8]), _p(keep[9]),
+                         _p(keep[10]), float(scale_modifier), _p(keep[11]), _p(keep[12]), _p(keep[13]),
+                         float(tan_fovx), float(tan_fovy), float(kernel_size), int(bool(prefiltered)), _p(color),
+                         _p(mdepth), _p(alpha), _p(normal), _p(radii, _i), int(bool(require_depth)),
+                         ctypes.byref(K))
+    st = State(ptr, P, W, H, K.value)
+    return dict(num_rendered=K.value, color=color, alpha=alpha, normal=normal, mdepth=mdepth, radii=radii,
+                state=st)
+
+
+def backward(state: State, bg, means3D, colors_precomp, opacities, scales, rotations, cov3D_precomp, sh, sg_axis,
+             sg_sharpness, sg_color, sh_degree, sg_degree, scale_modifier, viewmatrix, projmatrix, tan_fovx,
+             tan_fovy, kernel_size, dL_dcolor, dL_dmdepth, dL_dalpha, dL_dnormal, alpha, normal, mdepth, campos,
+             radii) -> dict:
+    """Same meaning as _C.rasterize_gaussians_backward (DGR/rasterize_points.h:45-80)."""
+    L = lib()
+    means3D = _np(means3D)
+    P = means3D.shape[0]
+    sh_a = _np(sh)
+    sgc = _np(sg_color)
+    SHM = 0 if sh_a is None else sh_a.shape[1]
+    SGM = 0 if sgc is None else sgc.shape[1]
+    out = dict(dmeans2D=np.zeros((P, 3), np.float32), dcolors=np.zeros((P, 3), np.float32),
+               dopacity=np.zeros((P, 1), np.float32), dmeans3D=np.zeros((P, 3), np.float32),
+               dcov3D=np.zeros((P, 6), np.float32), dsh=np.zeros((P, SHM, 3), np.float32),
+               dsg_axis=np.zeros((P, SGM, 3), np.float32), dsg_sharpness=np.zeros((P, SGM), np.float32),
+               dsg_color=np.zeros((P, SGM, 3), np.float32), dscales=np.zeros((P, 3), np.float32),
+               drotations=np.zeros((P, 4), np.float32))
+    if P == 0 or state is None:
+        return out
+    keep = [_np(bg), means3D, _np(colors_precomp), _np(opacities), _np(scales), _np(rotations), _np(cov3D_precomp),
+            sh_a, _np(sg_axis), _np(sg_sharpness), sgc, _np(viewmatrix), _np(projmatrix), _np(campos),
+            _np(radii, np.int32), _np(alpha), _np(normal), _np(mdepth), _np(dL_dcolor), _np(dL_dmdepth),
+            _np(dL_dalpha), _np(dL_dnormal)]
+    zeros_hw = np.zeros(state.W * state.H * 3, np.float32)
+    for k in (15, 16, 17, 18, 19, 20, 21):  # never pass NULL pixel planes
+        if keep[k] is None:
+            keep[k] = zeros_hw
+    rc = L.gsro_backward(state.ptr, _p(keep[0]), _p(keep[1]), _p(keep[2]), _p(keep[3]), _p(keep[4]), _p(keep[5]),
+                         _p(keep[6]), _p(keep[7]), _p(keep[8]), _p(keep[9]), _p(keep[10]), float(scale_modifier),
+                         _p(keep[11]), _p(keep[12]), _p(keep[13]), float(tan_fovx), float(tan_fovy),
+                         float(kernel_size), _p(keep[14], _i), _p(keep[15]), _p(keep[16]), _p(keep[17]),
+                         _p(keep[18]), _p(keep[19]), _p(keep[20]), _p(keep[21]), _p(out["dmeans3D"]),
+                         _p(out["dmeans2D"]), _p(out["dcolors"]), _p(out["dopacity"]), _p(out["dscales"]),
+                         _p(out["drotations"]), _p(out["dcov3D"]), _p(out["dsh"]), _p(out["dsg_axis"]),
+                         _p(out["dsg_sharpness"]), _p(out["dsg_color"]))
+    if rc != 0:
+        raise RuntimeError(f"oracle backward failed: {rc}")
+    return out
+
+
+def mark_visible(means3D, viewmatrix) -> np.ndarray:
+    m = _np(means3D)
+    P = 0 if m is None else m.shape[0]
+    out = np.zeros(P, np.uint8)
+    if P:
+        lib().gsro_mark_visible(P, _p(m), _p(_np(viewmatrix)), _p(out, _u8))
+    return out.astype(bool)
+
+
+def higher_msb(n: int) -> int:
+    return int(lib().gsro_higher_msb(int(n)))

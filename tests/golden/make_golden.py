@@ -1,0 +1,228 @@
+"""Generate golden fixtures by importing the reference's own Python code.
+
+Run in the build container (where /root/reference exists):
+    python tests/golden/make_golden.py
+The reference never travels: only the small .npz/.json DATA files written
+next to this script are committed (inputs and the reference's outputs).
+
+What is captured (all on CPU; `.cuda()` is monkey-patched to identity and
+the CUDA-only / unavailable imports are stubbed — nothing here runs the
+reference's CUDA rasterizer, which cannot build in this image):
+  sh_eval.npz      utils/sh_utils.py:57-112 eval_sh on random coefficients
+  cameras.npz      scene/cameras.py:20-73 Camera matrices built by
+                   utils/graphics_utils.py:44-92
+  getters.npz      scene/gaussian_model.py:146-262 activations + compute_3D_filter
+  boundary.json    DGR/diff_gaussian_rasterization/__init__.py:23-336 — the
+                   exact _C argument tuples (order, kinds, dtypes, shapes) and
+                   the 12-gradient routing, recorded with a stub `_C`.
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _stub(name, **attrs):
+    m = types.ModuleType(name)
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    sys.modules[name] = m
+    return m
+
+
+def _install_stubs():
+    _stub("cv2")
+    _stub("trimesh")
+    _stub("plyfile", PlyData=object, PlyElement=object)
+    _stub("simple_knn")
+    _stub("simple_knn._C", distCUDA2=lambda *a, **k: None)
+    _stub("open3d")
+    # import the reference's `scene` as a namespace so scene/__init__.py
+    # (dataset readers, open3d) is not executed
+    scene = types.ModuleType("scene")
+    scene.__path__ = [os.path.join(REF, "scene")]
+    sys.modules["scene"] = scene
+    sys.path.insert(0, REF)
+    torch.Tensor.cuda = lambda self, *a, **k: self  # CPU-only container
+
+
+def sh_fixture(rng):
+    sh_utils = importlib.import_module("utils.sh_utils")
+    out = {}
+    for deg in range(4):
+        n = 64
+        sh = rng.standard_normal((n, 3, 16)).astype(np.float32) * 0.5
+        d = rng.standard_normal((n, 3)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        res = sh_utils.eval_sh(deg, torch.tensor(sh), torch.tensor(d)).numpy()
+        out[f"sh_{deg}"] = sh
+        out[f"dirs_{deg}"] = d
+        out[f"out_{deg}"] = res
+    np.savez(os.path.join(OUT, "sh_eval.npz"), **out)
+
+
+def camera_fixture(rng):
+    cams = importlib.import_module("scene.cameras")
+    out = {}
+    cases = [(np.eye(3), np.zeros(3), 60.0, 64, 48), (None, None, 45.0, 96, 64), (None, None, 75.0, 40, 40)]
+    for i, (R, T, fovx_deg, W, H) in enumerate(cases):
+        if R is None:
+            a = rng.standard_normal(3)
+            a /= np.linalg.norm(a)
+            th = rng.uniform(-0.6, 0.6)
+            K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+            R = np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+            T = rng.standard_normal(3) * 0.5
+        fovx = math.radians(fovx_deg)
+        fovy = 2 * math.atan(math.tan(fovx / 2) * H / W)
+        img = torch.zeros(3, H, W)
+        cam = cams.Camera(colmap_id=0, R=R, T=T, FoVx=fovx, FoVy=fovy, image=img, gt_alpha_mask=None, gt_mask=None,
+                          image_name="x", uid=0, data_device="cpu")
+        out[f"R_{i}"] = R
+        out[f"T_{i}"] = T
+        out[f"fov_{i}"] = np.array([fovx, fovy])
+        out[f"wh_{i}"] = np.array([W, H])
+        out[f"world_view_{i}"] = cam.world_view_transform.numpy()
+        out[f"full_proj_{i}"] = cam.full_proj_transform.numpy()
+        out[f"center_{i}"] = cam.camera_center.numpy()
+    np.savez(os.path.join(OUT, "cameras.npz"), **out)
+
+
+def getters_fixture(rng):
+    gm = importlib.import_module("scene.gaussian_model")
+    P, sh_deg, sg_deg = 64, 3, 2
+    g = gm.GaussianModel(sh_deg, sg_deg)
+    xyz = rng.standard_normal((P, 3)).astype(np.float32)
+    xyz[:, 2] = rng.uniform(1.0, 6.0, P)
+    raw = dict(
+        xyz=xyz,
+        features_dc=rng.standard_normal((P, 1, 3)).astype(np.float32),
+        features_rest=rng.standard_normal((P, 15, 3)).astype(np.float32) * 0.1,
+        scaling=(rng.standard_normal((P, 3)) * 0.5 + math.log(0.02)).astype(np.float32),
+        rotation=rng.standard_normal((P, 4)).astype(np.float32),
+        opacity=rng.standard_normal((P, 1)).astype(np.float32),
+        sg_axis=rng.standard_normal((P, sg_deg, 3)).astype(np.float32),
+        sg_sharpness=rng.standard_normal((P, sg_deg)).astype(np.float32),
+        sg_color=rng.standard_normal((P, sg_deg, 3)).astype(np.float32) * 0.1,
+    )
+    for k, v in raw.items():
+        setattr(g, "_" + k, torch.tensor(v))
+
+    class _Cam:  # the attributes compute_3D_filter reads (gaussian_model.py:225-262)
+        def __init__(self, R, T, W, H, F):
+            self.R, self.T = torch.tensor(R, dtype=torch.float32), torch.tensor(T, dtype=torch.float32)
+            self.image_width, self.image_height, self.Fx, self.Fy = W, H, F, F
+
+    cams = [_Cam(np.eye(3), np.zeros(3), 64, 48, 55.0), _Cam(np.eye(3), np.array([0.1, 0.0, 0.5]), 64, 48, 70.0)]
+    g.compute_3D_filter(cams)
+    filt = g.filter_3D.numpy()
+    scales, opac = g.get_scaling_n_opacity_with_3D_filter
+    out = {f"raw_{k}": v for k, v in raw.items()}
+    out.update(filter_3D=filt, scales=scales.numpy(), opacity=opac.numpy(), rotation_out=g.get_rotation.numpy(),
+               features=g.get_features.numpy(), sg_axis_out=g.get_sg_axis.numpy(),
+               sg_sharpness_out=g.get_sg_sharpness.numpy(), sg_color_out=g.get_sg_color.numpy(),
+               cam_R=np.stack([c.R.numpy() for c in cams]), cam_T=np.stack([c.T.numpy() for c in cams]),
+               cam_WHF=np.array([[c.image_width, c.image_height, c.Fx] for c in cams], np.float32))
+    np.savez(os.path.join(OUT, "getters.npz"), **out)
+
+
+def boundary_fixture():
+    calls = {}
+
+    def describe(a):
+        if isinstance(a, torch.Tensor):
+            return {"kind": "tensor", "dtype": str(a.dtype).replace("torch.", ""), "shape": list(a.shape)}
+        return {"kind": type(a).__name__, "value": a if isinstance(a, (int, float, bool)) else None}
+
+    P, H, W, SHM, SGM = 5, 8, 12, 16, 2
+
+    def rasterize_gaussians(*args):
+        calls["forward"] = [describe(a) for a in args]
+        color = torch.full((3, H, W), 1.0)
+        alpha = torch.full((1, H, W), 2.0)
+        normal = torch.full((3, H, W), 3.0)
+        mdepth = torch.full((1, H, W), 4.0)
+        radii = torch.arange(P, dtype=torch.int32)
+        bufs = [torch.zeros(7, dtype=torch.uint8) for _ in range(4)]
+        return (17, color, alpha, normal, mdepth, radii, *bufs)
+
+    def rasterize_gaussians_backward(*args):
+        calls["backward"] = [describe(a) for a in args]
+        calls["backward_num_rendered"] = args[29]
+        # tag every returned grad with its C++ position so routing is visible
+        shapes = [(P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, SHM, 3), (P, SGM, 3), (P, SGM), (P, SGM, 3), (P, 3),
+                  (P, 4)]
+        return tuple(torch.full(s, float(i + 1)) for i, s in enumerate(shapes))
+
+    def mark_visible(*args):
+        calls["mark_visible"] = [describe(a) for a in args]
+        return torch.ones(P, dtype=torch.bool)
+
+    _stub("diff_gaussian_rasterization._C", rasterize_gaussians=rasterize_gaussians,
+          rasterize_gaussians_backward=rasterize_gaussians_backward, mark_visible=mark_visible)
+    pkg = types.ModuleType("diff_gaussian_rasterization")
+    pkg.__path__ = [os.path.join(REF, "submodules/diff-gaussian-rasterization/diff_gaussian_rasterization")]
+    sys.modules["diff_gaussian_rasterization"] = pkg
+    spec = importlib.util.spec_from_file_location(
+        "diff_gaussian_rasterization",
+        os.path.join(REF, "submodules/diff-gaussian-rasterization/diff_gaussian_rasterization/__init__.py"),
+        submodule_search_locations=pkg.__path__)
+    dgr = importlib.util.module_from_spec(spec)
+    sys.modules["diff_gaussian_rasterization"] = dgr
+    spec.loader.exec_module(dgr)
+    settings = dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=0.5, tanfovy=0.4, kernel_size=0.1, bg=torch.zeros(3),
+        scale_modifier=1.0, viewmatrix=torch.eye(4), projmatrix=torch.eye(4), sh_degree=3, sg_degree=1,
+        campos=torch.zeros(3), prefiltered=False, require_depth=True, debug=False)
+    rz = dgr.GaussianRasterizer(settings)
+    inputs = dict(means3D=torch.zeros(P, 3), means2D=torch.zeros(P, 3), opacities=torch.zeros(P, 1),
+                  shs=torch.zeros(P, SHM, 3), sg_axis=torch.zeros(P, SGM, 3), sg_sharpness=torch.zeros(P, SGM),
+                  sg_color=torch.zeros(P, SGM, 3), scales=torch.zeros(P, 3), rotations=torch.zeros(P, 4))
+    for v in inputs.values():
+        v.requires_grad_(True)
+    outs = rz(**inputs)
+    calls["forward_outputs"] = [describe(o) for o in outs]
+    calls["forward_output_values"] = [float(o.flatten()[0]) for o in outs]
+    loss = sum((o.float() * (i + 1)).sum() for i, o in enumerate(outs) if o.dtype.is_floating_point)
+    loss.backward()
+    calls["grad_routing"] = {k: (None if v.grad is None else float(v.grad.flatten()[0])) for k, v in inputs.items()}
+    rz.markVisible(torch.zeros(P, 3))
+    # argument-validation behaviour (DGR/__init__.py:302-308)
+    errs = {}
+    for name, kw in [("no_colors", dict(shs=None)), ("both_colors", dict(colors_precomp=torch.zeros(P, 3))),
+                     ("no_cov", dict(scales=None)), ("both_cov", dict(cov3D_precomp=torch.zeros(P, 6)))]:
+        args = dict(inputs)
+        args.update(kw)
+        try:
+            rz(**args)
+            errs[name] = None
+        except Exception as e:  # noqa: BLE001 - record the reference's behaviour
+            errs[name] = type(e).__name__ + ": " + str(e)
+    calls["errors"] = errs
+    calls["settings_fields"] = list(dgr.GaussianRasterizationSettings._fields)
+    with open(os.path.join(OUT, "boundary.json"), "w") as f:
+        json.dump(calls, f, indent=1)
+
+
+def main():
+    _install_stubs()
+    rng = np.random.default_rng(1234)
+    sh_fixture(rng)
+    camera_fixture(rng)
+    getters_fixture(rng)
+    boundary_fixture()
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,55 @@
+"""Shared test helpers: small seeded scenes and tolerance checks."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+import gsr_scene as S
+
+
+def small_case(P=40, W=40, H=24, seed=0, sh_degree=3, sg_degree=0, sgm=None, log_scale=math.log(0.12),
+               opacity_max_logit=2.0, z_range=(2.0, 4.0), kernel_size=0.0, require_depth=True, cam=None,
+               bg=(0.0, 0.0, 0.0)):
+    """A small random scene plus every argument of _C.rasterize_gaussians.
+
+    Opacity logits are capped (sigmoid(2) = 0.88) so o*G < 0.99 and the
+    reference's pass-through gradient of the 0.99 clamp never matters."""
+    cam = cam or S.make_camera(W, H)
+    raw = S.make_gaussians(P, sh_degree=sh_degree, sg_degree=sgm if sgm is not None else sg_degree, seed=seed,
+                           aspect=H / W, z_range=z_range, log_scale_mean=log_scale, log_scale_std=0.3,
+                           opacity_std=1.0)
+    raw.opacity.clamp_(max=opacity_max_logit)
+    inp = S.activated_inputs(raw)
+    inp = {k: v.detach().contiguous() for k, v in inp.items()}
+    return dict(
+        bg=torch.tensor(bg, dtype=torch.float32), inp=inp, cam=cam, W=W, H=H, sh_degree=sh_degree,
+        sg_degree=sg_degree, kernel_size=kernel_size, require_depth=require_depth,
+        tanx=math.tan(cam.FoVx * 0.5), tany=math.tan(cam.FoVy * 0.5), raw=raw)
+
+
+def oracle_args(c, colors_precomp=None):
+    inp = c["inp"]
+    return (c["bg"], inp["means3D"], colors_precomp, inp["opacities"], inp["scales"], inp["rotations"], None,
+            None if colors_precomp is not None else inp["shs"], inp["sg_axis"], inp["sg_sharpness"],
+            inp["sg_color"], c["sh_degree"], c["sg_degree"], 1.0, c["cam"].world_view_transform,
+            c["cam"].full_proj_transform, c["tanx"], c["tany"], c["kernel_size"], c["H"], c["W"],
+            c["cam"].camera_center, False, c["require_depth"])
+
+
+def rel_err(a, b) -> float:
+    """max|a-b| / max|b| (0 if both are zero)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    den = np.abs(b).max() if b.size else 0.0
+    num = np.abs(a - b).max() if a.size else 0.0
+    return 0.0 if den == 0 and num == 0 else float(num / max(den, 1e-30))
+
+
+def frac_bad(a, b, rtol, atol) -> float:
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    if a.size == 0:
+        return 0.0
+    return float(np.mean(np.abs(a - b) > atol + rtol * np.abs(b)))
