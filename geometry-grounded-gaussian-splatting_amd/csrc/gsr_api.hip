@@ -1,0 +1,323 @@
+// gsr_api.hip — the C ABI (include/gsr.h): host orchestration of the gfx950
+// kernels, replacing CudaRasterizer::Rasterizer::{forward, backward,
+// markVisible} (CR/rasterizer_impl.cu:186-592).
+//
+// Everything is enqueued on the caller's stream.  The forward synchronises
+// that stream exactly once, to read K (the number of Gaussian/tile instances)
+// and size the binning buffer, like the reference's cudaMemcpy at
+// rasterizer_impl.cu:384.  No other host<->device traffic, no device
+// allocation (all scratch comes from the caller's allocation callbacks).
+#include <stdio.h>
+
+#include <string>
+
+#include "../../include/gsr.h"
+#include "gsr_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* what, hipError_t e = hipSuccess) {
+    char buf[512];
+    if (e != hipSuccess)
+        snprintf(buf, sizeof(buf), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    else
+        snprintf(buf, sizeof(buf), "%s", what);
+    g_last_error = buf;
+    return code;
+}
+
+// getHigherMsb, CR/rasterizer_impl.cu:37-50
+uint32_t higher_msb(uint32_t n) {
+    uint32_t msb = sizeof(n) * 4;
+    uint32_t step = msb;
+    while (step > 1) {
+        step /= 2;
+        if (n >> msb) msb += step;
+        else msb -= step;
+    }
+    if (n >> msb) msb++;
+    return msb;
+}
+
+using namespace gsr;
+
+size_t carve_geom(void* base, int P, GeomState& g) {
+    Carver c(base);
+    g.splats = c.take<Splat>(P);
+    g.depths = c.take<float>(P);
+    g.tiles_touched = c.take<uint32_t>(P);
+    g.offsets = c.take<uint32_t>(P);
+    g.radii = c.take<int>(P);
+    g.clamped = c.take<uint8_t>(P);
+    g.scan_tmp_bytes = scan_temp_bytes(P);
+    g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
+    return c.off + 256;
+}
+
+size_t carve_binning(void* base, int K, int end_bit, BinningState& b) {
+    Carver c(base);
+    b.keys_unsorted = c.take<uint64_t>(K);
+    b.keys = c.take<uint64_t>(K);
+    b.values_unsorted = c.take<uint32_t>(K);
+    b.point_list = c.take<uint32_t>(K);
+    b.sort_tmp_bytes = sort_temp_bytes(K, end_bit);
+    b.sort_tmp = c.take<char>(b.sort_tmp_bytes);
+    return c.off + 256;
+}
+
+size_t carve_image(void* base, int HW, ImageState& s) {
+    Carver c(base);
+    s.n_contrib = c.take<uint32_t>(HW);
+    return c.off + 256;
+}
+
+size_t carve_tiles(void* base, int T, TileState& s) {
+    Carver c(base);
+    s.ranges = c.take<uint2>(T);
+    s.max_contrib = c.take<uint32_t>(T);
+    return c.off + 256;
+}
+
+size_t carve_bwd(void* base, int P, BwdState& s) {
+    Carver c(base);
+    s.acc = c.take<float>((size_t)P * kAccFields);
+    s.acc_abs = c.take<float>(P);
+    return c.off;
+}
+
+// 256-B alignment of the carve base (callbacks may return any alignment)
+void* aligned_base(void* p) {
+    return reinterpret_cast<void*>(align_up(reinterpret_cast<uintptr_t>(p), 256));
+}
+
+FwdParams make_params(int P, int D, int SHM, int SGD, int SGM, const float* background, int W, int H,
+                      const float* means3D, const float* colors_precomp, const float* opacities,
+                      const float* scales, const float* rotations, const float* cov3D_precomp, const float* shs,
+                      const float* sg_axis, const float* sg_sharpness, const float* sg_color, float scale_modifier,
+                      const float* view, const float* proj, const float* campos, float tan_fovx, float tan_fovy,
+                      float kernel_size, int require_depth) {
+    FwdParams p;
+    p.P = P;
+    p.D = D;
+    p.SHM = SHM;
+    p.SGD = SGD;
+    p.SGM = SGM;
+    p.W = W;
+    p.H = H;
+    p.background = background;
+    p.means3D = means3D;
+    p.colors_precomp = colors_precomp;
+    p.opacities = opacities;
+    p.scales = scales;
+    p.rotations = rotations;
+    p.cov3D_precomp = cov3D_precomp;
+    p.shs = shs;
+    p.sg_axis = sg_axis;
+    p.sg_sharpness = sg_sharpness;
+    p.sg_color = sg_color;
+    p.scale_modifier = scale_modifier;
+    p.view = view;
+    p.proj = proj;
+    p.campos = campos;
+    p.tan_fovx = tan_fovx;
+    p.tan_fovy = tan_fovy;
+    p.focal_y = H / (2.0f * tan_fovy);
+    p.focal_x = W / (2.0f * tan_fovx);
+    p.kernel_size = kernel_size;
+    p.grid_x = (W + kTile - 1) / kTile;
+    p.grid_y = (H + kTile - 1) / kTile;
+    p.require_depth = require_depth != 0;
+    return p;
+}
+
+const char* check_params(const FwdParams& p) {
+    if (p.P < 0 || p.W <= 0 || p.H <= 0) return "invalid P / image size";
+    if (p.P == 0) return nullptr;
+    if (!p.means3D || !p.opacities || !p.view || !p.proj || !p.background) return "missing required input";
+    if ((p.colors_precomp == nullptr) == (p.shs == nullptr))
+        return "Please provide excatly one of either SHs or precomputed colors!";
+    const bool have_sr = p.scales && p.rotations;
+    if (have_sr == (p.cov3D_precomp != nullptr))
+        return "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!";
+    if (p.shs && (p.D < 0 || p.D > 3 || p.SHM < (p.D + 1) * (p.D + 1))) return "sh_degree / SH size mismatch";
+    if (p.shs && !p.campos) return "campos required for SH colours";
+    if (p.SGD < 0 || p.SGD > p.SGM) return "sg_degree exceeds SG lobes";
+    if (p.SGD > 0 && (!p.sg_axis || !p.sg_sharpness || !p.sg_color)) return "missing SG tensors";
+    return nullptr;
+}
+
+#define GSR_TRY(expr, what)                                   \
+    do {                                                      \
+        hipError_t _e = (expr);                               \
+        if (_e != hipSuccess) return fail(GSR_ERR_HIP, what, _e); \
+        if (debug) {                                          \
+            _e = hipStreamSynchronize(stream);                \
+            if (_e != hipSuccess) return fail(GSR_ERR_HIP, what, _e); \
+        }                                                     \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int gsr_abi_version(void) { return 1; }
+
+const char* gsr_last_error(void) { return g_last_error.c_str(); }
+
+int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                          gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                          int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
+                          int height, const float* means3D, const float* colors_precomp, const float* opacities,
+                          const float* scales, const float* rotations, const float* cov3D_precomp,
+                          const float* shs, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                          float scale_modifier, const float* viewmatrix, const float* projmatrix,
+                          const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
+                          float* out_color, float* out_mdepth, float* out_alpha, float* out_normal, int* radii,
+                          int require_depth, int debug, void* stream_ptr, int* num_rendered) {
+    (void)prefiltered;
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    if (num_rendered) *num_rendered = 0;
+    FwdParams p = make_params(P, sh_degree, SHM, sg_degree, SGM, background, width, height, means3D, colors_precomp,
+                              opacities, scales, rotations, cov3D_precomp, shs, sg_axis, sg_sharpness, sg_color,
+                              scale_modifier, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, kernel_size,
+                              require_depth);
+    if (const char* msg = check_params(p)) return fail(GSR_ERR_ARGS, msg);
+    if (!out_color || !out_alpha || !out_mdepth || !out_normal) return fail(GSR_ERR_ARGS, "missing output buffer");
+    if (!geom_alloc || !binning_alloc || !image_alloc || !tile_alloc) return fail(GSR_ERR_ARGS, "missing allocator");
+    const int tiles = (int)(p.grid_x * p.grid_y);
+
+    GeomState gs;
+    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, gs));
+    if (!gbuf) return fail(GSR_ERR_ALLOC, "geometry buffer allocation failed");
+    carve_geom(aligned_base(gbuf), P, gs);
+    TileState ts;
+    void* tbuf = tile_alloc(tile_ctx, carve_tiles(nullptr, tiles, ts));
+    if (!tbuf) return fail(GSR_ERR_ALLOC, "tile buffer allocation failed");
+    carve_tiles(aligned_base(tbuf), tiles, ts);
+    ImageState is;
+    void* ibuf = image_alloc(image_ctx, carve_image(nullptr, width * height, is));
+    if (!ibuf) return fail(GSR_ERR_ALLOC, "image buffer allocation failed");
+    carve_image(aligned_base(ibuf), width * height, is);
+    if (radii == nullptr) radii = gs.radii;
+
+    if (P == 0) {
+        // empty scene: background image, zero geometry (rasterize_points.cu:95)
+        hipError_t e = hipMemsetAsync(ts.ranges, 0, sizeof(uint2) * tiles, stream);
+        if (e == hipSuccess) e = hipMemsetAsync(ts.max_contrib, 0, sizeof(uint32_t) * tiles, stream);
+        if (e != hipSuccess) return fail(GSR_ERR_HIP, "memset", e);
+        BinningState bs;
+        void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, 0, 32, bs));
+        if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
+        carve_binning(aligned_base(bbuf), 0, 32, bs);
+        GSR_TRY(launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
+        return GSR_OK;
+    }
+
+    GSR_TRY(launch_preprocess_fwd(p, gs, radii, stream), "preprocess");
+    GSR_TRY(launch_scan(gs, P, stream), "scan");
+    uint32_t K = 0;
+    GSR_TRY(hipMemcpyAsync(&K, gs.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
+    {
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
+    }
+    const int end_bit = 32 + (int)higher_msb((uint32_t)tiles);
+    BinningState bs;
+    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, end_bit, bs));
+    if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
+    carve_binning(aligned_base(bbuf), (int)K, end_bit, bs);
+    GSR_TRY(launch_emit_keys(p, gs, radii, bs, stream), "emit keys");
+    GSR_TRY(launch_sort(bs, (int)K, end_bit, stream), "sort");
+    GSR_TRY(launch_tile_ranges(bs, (int)K, ts, tiles, stream), "tile ranges");
+    GSR_TRY(launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
+    if (num_rendered) *num_rendered = (int)K;
+    return GSR_OK;
+}
+
+int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
+                           int sg_degree, int SGM, int R, const float* background, int width, int height,
+                           const float* means3D, const float* colors_precomp, const float* opacities,
+                           const float* scales, const float* rotations, const float* cov3D_precomp,
+                           const float* shs, const float* sg_axis, const float* sg_sharpness,
+                           const float* sg_color, float scale_modifier, const float* viewmatrix,
+                           const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                           float kernel_size, const int* radii, const float* alphas, const float* normalmap,
+                           const float* mdepth, const void* geom_buffer, const void* binning_buffer,
+                           const void* image_buffer, const void* tile_buffer, const float* dL_dpix,
+                           const float* dL_dpix_mdepth, const float* dL_dalphas, const float* dL_dpixel_normals,
+                           float* dL_dmean3D, float* dL_dmean2D, float* dL_dcolor, float* dL_dopacity,
+                           float* dL_dscale, float* dL_drot, float* dL_dcov3D, float* dL_dsh, float* dL_dsg_axis,
+                           float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
+                           void* stream_ptr) {
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    BwdParams b;
+    b.f = make_params(P, sh_degree, SHM, sg_degree, SGM, background, width, height, means3D, colors_precomp,
+                      opacities, scales, rotations, cov3D_precomp, shs, sg_axis, sg_sharpness, sg_color,
+                      scale_modifier, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, kernel_size, require_depth);
+    if (P == 0) return GSR_OK;
+    if (const char* msg = check_params(b.f)) return fail(GSR_ERR_ARGS, msg);
+    if (!geom_buffer || !binning_buffer || !image_buffer || !tile_buffer || !radii || !alphas || !dL_dpix ||
+        !dL_dalphas || !dL_dmean3D || !dL_dmean2D || !dL_dcolor || !dL_dopacity)
+        return fail(GSR_ERR_ARGS, "missing backward buffer");
+    if (b.f.require_depth && (!normalmap || !mdepth || !dL_dpix_mdepth || !dL_dpixel_normals))
+        return fail(GSR_ERR_ARGS, "missing geometry buffers for require_depth");
+    if (scales && (!dL_dscale || !dL_drot)) return fail(GSR_ERR_ARGS, "missing scale/rotation gradients");
+    if (cov3D_precomp && !dL_dcov3D) return fail(GSR_ERR_ARGS, "missing cov3D gradient");
+    if (shs && !dL_dsh) return fail(GSR_ERR_ARGS, "missing SH gradient");
+    if (SGM > 0 && shs && (!dL_dsg_axis || !dL_dsg_sharpness || !dL_dsg_color))
+        return fail(GSR_ERR_ARGS, "missing SG gradients");
+    b.R = R;
+    b.radii = radii;
+    b.alphas = alphas;
+    b.normalmap = normalmap;
+    b.mdepth = mdepth;
+    b.dL_dpix = dL_dpix;
+    b.dL_dmdepth = dL_dpix_mdepth;
+    b.dL_dalpha = dL_dalphas;
+    b.dL_dnormal = dL_dpixel_normals;
+    b.dL_dmean3D = dL_dmean3D;
+    b.dL_dmean2D = dL_dmean2D;
+    b.dL_dcolor = dL_dcolor;
+    b.dL_dopacity = dL_dopacity;
+    b.dL_dscale = dL_dscale;
+    b.dL_drot = dL_drot;
+    b.dL_dcov3D = dL_dcov3D;
+    b.dL_dsh = dL_dsh;
+    b.dL_dsg_axis = dL_dsg_axis;
+    b.dL_dsg_sharpness = dL_dsg_sharpness;
+    b.dL_dsg_color = dL_dsg_color;
+
+    const int tiles = (int)(b.f.grid_x * b.f.grid_y);
+    const int end_bit = 32 + (int)higher_msb((uint32_t)tiles);
+    GeomState gs;
+    carve_geom(aligned_base(const_cast<void*>(geom_buffer)), P, gs);
+    BinningState bs;
+    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, end_bit, bs);
+    ImageState is;
+    carve_image(aligned_base(const_cast<void*>(image_buffer)), width * height, is);
+    TileState ts;
+    carve_tiles(aligned_base(const_cast<void*>(tile_buffer)), tiles, ts);
+    BwdState ws;
+    const size_t wbytes = carve_bwd(nullptr, P, ws);
+    void* wbuf = geom_bwd_alloc(geom_bwd_ctx, wbytes + 256);
+    if (!wbuf) return fail(GSR_ERR_ALLOC, "backward buffer allocation failed");
+    void* wb = aligned_base(wbuf);
+    carve_bwd(wb, P, ws);
+    GSR_TRY(hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
+    GSR_TRY(launch_render_bwd(b, gs, bs, is, ts, ws, stream), "render backward");
+    GSR_TRY(launch_preprocess_bwd(b, gs, ws, stream), "preprocess backward");
+    return GSR_OK;
+}
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream_ptr) {
+    (void)projmatrix;
+    if (P < 0 || (P > 0 && (!means3D || !viewmatrix || !present))) return fail(GSR_ERR_ARGS, "invalid arguments");
+    hipError_t e = launch_mark_visible(P, means3D, viewmatrix, present, (hipStream_t)stream_ptr);
+    if (e != hipSuccess) return fail(GSR_ERR_HIP, "mark_visible", e);
+    return GSR_OK;
+}
+
+}  // extern "C"

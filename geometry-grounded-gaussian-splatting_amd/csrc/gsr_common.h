@@ -1,0 +1,167 @@
+// gsr_common.h — shared constants, HBM layouts and wave64 helpers for the
+// gfx950 rasterizer kernels.
+//
+// Semantics follow the reference's compile-time configuration
+// (DGR/cuda_rasterizer/config.h:21-40): 16x16 tiles are semantic (they decide
+// which Gaussians a pixel sees), SPLIT = 8 samples x 5 bisection iterations
+// over +-0.4 around the initial median depth, MIN_TRANSMITTANCE = 0.45.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsr {
+
+constexpr int kTile = 16;                 // BLOCK_X = BLOCK_Y
+constexpr int kTilePixels = kTile * kTile;  // one workgroup (4 wave64) per tile
+constexpr int kSplit = 8;
+constexpr int kSplitIterations = 5;
+constexpr float kSampleRange = 0.4f;
+constexpr float kMinTransmittance = 0.45f;
+constexpr float kNearPlane = 0.2f;
+
+// --------------------------------------------------------------------------
+// Per-Gaussian render record ("splat"), written by the preprocess and
+// gathered by both render kernels.  64 B = four 16-B words, one aligned
+// 64-B segment per Gaussian:
+//   w0 = (x_pix, y_pix, conic.x, conic.y)
+//   w1 = (conic.z, opacity*coef, plane.x, plane.y)
+//   w2 = (plane.z = |t|, plane.w = rsigma, r, g)
+//   w3 = (b, n.x, n.y, n.z)
+// The median-depth bisection needs only w0, w1, w2.xy (48 B).
+// --------------------------------------------------------------------------
+struct alignas(16) Splat {
+    float4 w0, w1, w2, w3;
+};
+
+// Per-Gaussian gradient accumulator written by the backward render with
+// wave-wide atomics: 16 fields in one 64-B record + the |dmean2D| channel in
+// a separate dense array.
+//   0..2  dL/dcolor          3..4  dL/dmean2D (x, y; NDC units)
+//   5..8  dL/dconic (x, y, z) and dL/d(opacity-weighted) w
+//   9..11 dL/dnormal         12..15 dL/dray_plane (x, y, tc, rsigma)
+enum AccField : int {
+    kAccColor = 0, kAccMean2D = 3, kAccConic = 5, kAccNormal = 9, kAccPlane = 12, kAccFields = 16
+};
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Carves a byte buffer into typed arrays, 256-B aligned.
+struct Carver {
+    char* base;
+    size_t off;
+    __host__ explicit Carver(void* b) : base(static_cast<char*>(b)), off(0) {}
+    template <class T>
+    __host__ T* take(size_t count) {
+        off = align_up(off, 256);
+        T* p = reinterpret_cast<T*>(base + off);
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+// ---- per-Gaussian forward state (replaces GeometryState, rasterizer_impl.h) ----
+struct GeomState {
+    Splat* splats;
+    float* depths;
+    uint32_t* tiles_touched;
+    uint32_t* offsets;  // inclusive scan of tiles_touched
+    int* radii;         // internal copy when the caller passes radii == NULL
+    uint8_t* clamped;   // bit c set: colour channel c was clamped at 0
+    void* scan_tmp;
+    size_t scan_tmp_bytes;
+};
+// ---- per-instance state (replaces BinningState) ----
+struct BinningState {
+    uint64_t* keys_unsorted;
+    uint64_t* keys;
+    uint32_t* values_unsorted;
+    uint32_t* point_list;
+    void* sort_tmp;
+    size_t sort_tmp_bytes;
+};
+// ---- per-pixel / per-tile state (ImageState, TileState<false>) ----
+struct ImageState {
+    uint32_t* n_contrib;
+};
+struct TileState {
+    uint2* ranges;
+    uint32_t* max_contrib;
+};
+// ---- backward scratch (replaces GeometryBwdState) ----
+struct BwdState {
+    float* acc;      // [P][16]
+    float* acc_abs;  // [P]
+};
+
+// --------------------------------------------------------------------------
+// wave64 helpers
+// --------------------------------------------------------------------------
+__device__ inline float wave_max_f(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ inline uint32_t wave_max_u(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint32_t w = __shfl_xor(v, o, 64);
+        v = v > w ? v : w;
+    }
+    return v;
+}
+__device__ inline float wave_sum_f(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Transposed butterfly reduction of 16 per-lane values over the 64 lanes of
+// a wave.  Stage 1/2 use gfx950's v_permlane32_swap / v_permlane16_swap (one
+// swap moves half of a pair across the 32- or 16-lane boundary, so each stage
+// halves the number of live values); stages 3/4 use xor shuffles with a
+// keep/send select; the last two stages are plain xor adds.  On return lane
+// l (l % 4 == 0) holds the full wave sum of field (l >> 2); 17 cross-lane ops
+// instead of 16 x 6 for independent reductions.
+__device__ inline float wave_transpose_reduce16(const float (&v)[16]) {
+    const int lane = threadIdx.x & 63;
+    float a[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
+        a[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    // lanes 0..31 hold fields 0..7, lanes 32..63 fields 8..15 (sums over l, l^32)
+    float b[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[i]), __float_as_uint(a[i + 4]), false, false);
+        b[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    // field bit 2 <- lane bit 4
+    const bool hi8 = (lane & 8) != 0;
+    float c[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        float keep = hi8 ? b[i + 2] : b[i];
+        float send = hi8 ? b[i] : b[i + 2];
+        c[i] = keep + __shfl_xor(send, 8, 64);
+    }
+    const bool hi4 = (lane & 4) != 0;
+    float keep = hi4 ? c[1] : c[0];
+    float send = hi4 ? c[0] : c[1];
+    float d = keep + __shfl_xor(send, 4, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 1, 64);
+    return d;
+}
+
+// XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so map
+// the blocks one XCD receives onto a contiguous run of tiles (rows of tiles
+// that share Gaussians then share that XCD's L2).  Bijective for any count.
+__device__ inline uint32_t xcd_remap(uint32_t b, uint32_t n) {
+    const uint32_t q = n / 8, r = n % 8, xcd = b % 8, local = b / 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
+}  // namespace gsr

@@ -1,0 +1,83 @@
+// gsr_kernels.h — internal launch interface between the C-ABI host code
+// (gsr_api.hip) and the kernels.  Not part of the public ABI (include/gsr.h).
+#pragma once
+
+#include "gsr_common.h"
+
+namespace gsr {
+
+struct FwdParams {
+    int P, D, SHM, SGD, SGM, W, H;
+    const float* background;
+    const float* means3D;
+    const float* colors_precomp;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+    const float* shs;
+    const float* sg_axis;
+    const float* sg_sharpness;
+    const float* sg_color;
+    float scale_modifier;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float tan_fovx, tan_fovy, focal_x, focal_y, kernel_size;
+    uint32_t grid_x, grid_y;
+    bool require_depth;
+};
+
+struct BwdParams {
+    FwdParams f;
+    int R;
+    const int* radii;
+    const float* alphas;
+    const float* normalmap;
+    const float* mdepth;
+    const float* dL_dpix;
+    const float* dL_dmdepth;
+    const float* dL_dalpha;
+    const float* dL_dnormal;
+    float* dL_dmean3D;
+    float* dL_dmean2D;
+    float* dL_dcolor;
+    float* dL_dopacity;
+    float* dL_dscale;
+    float* dL_drot;
+    float* dL_dcov3D;
+    float* dL_dsh;
+    float* dL_dsg_axis;
+    float* dL_dsg_sharpness;
+    float* dL_dsg_color;
+};
+
+// preprocess_fwd.hip
+hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* radii, hipStream_t stream);
+
+// binning.hip
+size_t scan_temp_bytes(int P);
+size_t sort_temp_bytes(int K, int end_bit);
+hipError_t launch_scan(const GeomState& gs, int P, hipStream_t stream);
+hipError_t launch_emit_keys(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
+                            hipStream_t stream);
+hipError_t launch_sort(const BinningState& bs, int K, int end_bit, hipStream_t stream);
+hipError_t launch_tile_ranges(const BinningState& bs, int K, const TileState& ts, int tiles, hipStream_t stream);
+
+// render_fwd.hip
+hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const ImageState& is,
+                             const TileState& ts, float* out_color, float* out_alpha, float* out_normal,
+                             float* out_mdepth, hipStream_t stream);
+
+// render_bwd.hip
+hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const BinningState& bs, const ImageState& is,
+                             const TileState& ts, const BwdState& ws, hipStream_t stream);
+
+// preprocess_bwd.hip
+hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const BwdState& ws, hipStream_t stream);
+
+// mark visible
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
+                               hipStream_t stream);
+
+}  // namespace gsr

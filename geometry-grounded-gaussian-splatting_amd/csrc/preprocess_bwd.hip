@@ -1,0 +1,567 @@
+// preprocess_bwd.hip — per-Gaussian backward on gfx950.
+//
+// One fused kernel replaces BACKWARD::preprocess (render_backward.cu:1071-1161):
+//   computeCov2DCUDA   (:249-656)  conic / Mip coef / ray-plane / normal -> cov3D -> scale, rot, mean
+//   computeCov3D bwd   (:193-244)
+//   preprocessCUDA bwd (:661-713)  screen-space mean -> mean3D, SH/SG colour backward (:56-191)
+// It also writes the dL/dmeans2D and dL/dcolors extension outputs from the
+// render-backward accumulator, so every gradient tensor is written exactly once
+// with plain stores (zeros for culled Gaussians) and the host never memsets
+// them (the reference zero-fills 11 tensors per backward,
+// rasterize_points.cu:190-200).
+//
+// Reproduced reference behaviour that differs from the exact derivative of
+// the forward (tests/torch_ref.py Q1, Q4): the normal backward scales by
+// 1/|normalize(n)| (== 1); d rsigma / d(u, v) through vb is not propagated.
+#include "gsr_kernels.h"
+#include "gsr_math.h"
+
+namespace gsr {
+
+struct PreprocessBwdArgs {
+    int P, D, SHM, SGD, SGM;
+    const float* means3D;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+    const float* shs;
+    const float* sg_axis;
+    const float* sg_sharpness;
+    const float* sg_color;
+    float scale_modifier;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float tan_fovx, tan_fovy, focal_x, focal_y, kernel_size;
+    const int* radii;
+    const uint8_t* clamped;
+    const float* acc;
+    const float* acc_abs;
+    float* dL_dmean3D;
+    float* dL_dmean2D;
+    float* dL_dcolor;
+    float* dL_dopacity;
+    float* dL_dscale;
+    float* dL_drot;
+    float* dL_dcov3D;
+    float* dL_dsh;
+    float* dL_dsg_axis;
+    float* dL_dsg_sharpness;
+    float* dL_dsg_color;
+};
+
+__device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
+    for (int k = 0; k < 3; k++) a.dL_dmean3D[3 * idx + k] = 0.f;
+    a.dL_dopacity[idx] = 0.f;
+    if (a.dL_dscale)
+        for (int k = 0; k < 3; k++) a.dL_dscale[3 * idx + k] = 0.f;
+    if (a.dL_drot)
+        for (int k = 0; k < 4; k++) a.dL_drot[4 * idx + k] = 0.f;
+    if (a.dL_dcov3D)
+        for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = 0.f;
+    if (a.dL_dsh)
+        for (int k = 0; k < 3 * a.SHM; k++) a.dL_dsh[(size_t)idx * 3 * a.SHM + k] = 0.f;
+    for (int k = 0; k < a.SGM; k++) {
+        const size_t o = (size_t)idx * a.SGM + k;
+        if (a.dL_dsg_sharpness) a.dL_dsg_sharpness[o] = 0.f;
+        for (int c = 0; c < 3; c++) {
+            if (a.dL_dsg_axis) a.dL_dsg_axis[3 * o + c] = 0.f;
+            if (a.dL_dsg_color) a.dL_dsg_color[3 * o + c] = 0.f;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    const float* acc = a.acc + (size_t)idx * kAccFields;
+    // extension outputs straight from the accumulator (zero for culled Gaussians)
+    a.dL_dmean2D[3 * idx + 0] = acc[kAccMean2D + 0];
+    a.dL_dmean2D[3 * idx + 1] = acc[kAccMean2D + 1];
+    a.dL_dmean2D[3 * idx + 2] = a.acc_abs[idx];
+    a.dL_dcolor[3 * idx + 0] = acc[kAccColor + 0];
+    a.dL_dcolor[3 * idx + 1] = acc[kAccColor + 1];
+    a.dL_dcolor[3 * idx + 2] = acc[kAccColor + 2];
+    if (!(a.radii[idx] > 0)) {
+        zero_outputs(a, idx);
+        return;
+    }
+    const float fx = a.focal_x, fy = a.focal_y;
+    const float* V = a.view;
+    const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
+    const float dconx = acc[kAccConic + 0], dcony = acc[kAccConic + 1], dconz = acc[kAccConic + 2],
+                dconw = acc[kAccConic + 3];
+    const float dnx = acc[kAccNormal + 0], dny = acc[kAccNormal + 1], dnz = acc[kAccNormal + 2];
+    const float drpx = acc[kAccPlane + 0] / fx, drpy = acc[kAccPlane + 1] / fy;
+    const float dL_dtc = acc[kAccPlane + 2], dL_drsig = acc[kAccPlane + 3];
+
+    // ---------------- computeCov2DCUDA ----------------
+    const ViewGeom g = view_geom(V, mx, my, mz, a.tan_fovx, a.tan_fovy);
+    const float rtc = 1.0f / sqrtf(g.t[0] * g.t[0] + g.t[1] * g.t[1] + g.t[2] * g.t[2]);
+    const float dtc_x = g.t[0] * rtc * dL_dtc, dtc_y = g.t[1] * rtc * dL_dtc, dtc_z = g.t[2] * rtc * dL_dtc;
+    const float xgm = g.clamp_x ? 0.f : 1.f, ygm = g.clamp_y ? 0.f : 1.f;
+    const float u = g.u, v = g.v, tz = g.tz, tx = g.tx, ty = g.ty;
+    const float j00 = fx / tz, j02 = -(fx * tx) / (tz * tz);
+    const float j11 = fy / tz, j12 = -(fy * ty) / (tz * tz);
+    float Wr[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) Wr[3 * i + j] = V[4 * j + i];
+    // Q = J W_r rows (glm T[0][k] = Q0[k], T[1][k] = Q1[k])
+    float Q0[3], Q1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        Q0[k] = j00 * Wr[k] + j02 * Wr[6 + k];
+        Q1[k] = j11 * Wr[3 + k] + j12 * Wr[6 + k];
+    }
+    float Vrk[9], Vinv[9], Rq[9], s[3] = {0.f, 0.f, 0.f};
+    float evl[3] = {0.f, 0.f, 0.f}, EV[9];
+    bool well_conditioned = true;
+    if (a.scales) {
+        s[0] = a.scale_modifier * a.scales[3 * idx];
+        s[1] = a.scale_modifier * a.scales[3 * idx + 1];
+        s[2] = a.scale_modifier * a.scales[3 * idx + 2];
+        const float* q = a.rotations + 4 * idx;
+        float A_unused[9];
+        rot_view(V, q[0], q[1], q[2], q[3], A_unused, Rq);
+        const float s2[3] = {s[0] * s[0], s[1] * s[1], s[2] * s[2]};
+        const float is2[3] = {1.0f / s2[0], 1.0f / s2[1], 1.0f / s2[2]};
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                Vrk[3 * i + j] = Rq[3 * i] * Rq[3 * j] * s2[0] + Rq[3 * i + 1] * Rq[3 * j + 1] * s2[1] +
+                                 Rq[3 * i + 2] * Rq[3 * j + 2] * s2[2];
+                Vinv[3 * i + j] = Rq[3 * i] * Rq[3 * j] * is2[0] + Rq[3 * i + 1] * Rq[3 * j + 1] * is2[1] +
+                                  Rq[3 * i + 2] * Rq[3 * j + 2] * is2[2];
+            }
+    } else {
+        const float* c = a.cov3D_precomp + 6 * idx;
+        const float Vk[9] = {c[0], c[1], c[2], c[1], c[3], c[4], c[2], c[4], c[5]};
+#pragma unroll
+        for (int k = 0; k < 9; k++) Vrk[k] = Vk[k];
+        sym3_eigen(Vk, evl, EV);
+        well_conditioned = evl[0] > 1e-8f;
+        if (well_conditioned) {
+            const float il[3] = {1.0f / evl[0], 1.0f / evl[1], 1.0f / evl[2]};
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++)
+                    Vinv[3 * i + j] = EV[i] * EV[j] * il[0] + EV[3 + i] * EV[3 + j] * il[1] + EV[6 + i] * EV[6 + j] * il[2];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++) Vinv[3 * i + j] = EV[i] * EV[j];
+        }
+    }
+    // cov2D = Q Vrk Q^T (no kernel), cov_cam_inv = W_r Vinv W_r^T
+    float VQ0[3], VQ1[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        VQ0[i] = Vrk[3 * i] * Q0[0] + Vrk[3 * i + 1] * Q0[1] + Vrk[3 * i + 2] * Q0[2];
+        VQ1[i] = Vrk[3 * i] * Q1[0] + Vrk[3 * i + 1] * Q1[1] + Vrk[3 * i + 2] * Q1[2];
+    }
+    const float c00 = Q0[0] * VQ0[0] + Q0[1] * VQ0[1] + Q0[2] * VQ0[2];
+    const float c01 = Q0[0] * VQ1[0] + Q0[1] * VQ1[1] + Q0[2] * VQ1[2];
+    const float c11 = Q1[0] * VQ1[0] + Q1[1] * VQ1[1] + Q1[2] * VQ1[2];
+    float WV[9], cinv[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            WV[3 * i + j] = Wr[3 * i] * Vinv[j] + Wr[3 * i + 1] * Vinv[3 + j] + Wr[3 * i + 2] * Vinv[6 + j];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            cinv[3 * i + j] = WV[3 * i] * Wr[3 * j] + WV[3 * i + 1] * Wr[3 * j + 1] + WV[3 * i + 2] * Wr[3 * j + 2];
+    const float ks = a.kernel_size;
+    const float det_0 = fmaxf(1e-6f, c00 * c11 - c01 * c01);
+    const float det_1 = fmaxf(1e-6f, (c00 + ks) * (c11 + ks) - c01 * c01);
+    const float coef = sqrtf(det_0 / det_1);
+
+    // ray-plane / normal backward (render_backward.cu:425-545)
+    const float m0 = cinv[0] * u + cinv[1] * v + cinv[2];
+    const float m1 = cinv[3] * u + cinv[4] * v + cinv[5];
+    const float m2 = cinv[6] * u + cinv[7] * v + cinv[8];
+    const float vb = m0 * u + m1 * v + m2;
+    const float u2 = u * u, v2 = v * v, uv = u * v;
+    const float l = sqrtf(tx * tx + ty * ty + tz * tz);
+    const float clamp_vb = fmaxf(vb, 1e-7f);
+    const float rl2 = u2 + v2 + 1.f;
+    const float rl_inv = __builtin_amdgcn_rsqf(rl2);
+    const float fn = l / rl2;
+    const float mv0 = m0 / clamp_vb, mv1 = m1 / clamp_vb, mv2 = m2 / clamp_vb;  // uvh_m / vb
+    const float plx = (v2 + 1.f) * mv0 - uv * mv1 - u * mv2;
+    const float ply = -uv * mv0 + (u2 + 1.f) * mv1 - v * mv2;
+    const float rn0 = -plx * fn, rn1 = -ply * fn, rn2 = -1.f;
+    const float itz = 1.f / tz, il = 1.f / l;
+    const float cn0 = rn0 * itz + tx * il * rn2;
+    const float cn1 = rn1 * itz + ty * il * rn2;
+    const float cn2 = -(tx * itz * itz) * rn0 - (ty * itz * itz) * rn1 + tz * il * rn2;
+    const float icn = 1.0f / sqrtf(cn0 * cn0 + cn1 * cn1 + cn2 * cn2);
+    const float nv0 = cn0 * icn, nv1 = cn1 * icn, nv2 = cn2 * icn;
+    const float rlv = 1.0f / sqrtf(nv0 * nv0 + nv1 * nv1 + nv2 * nv2);  // == 1 (reference quirk Q1)
+    const float ndot = nv0 * dnx + nv1 * dny + nv2 * dnz;
+    const float dc0 = (dnx - nv0 * ndot) * rlv, dc1 = (dny - nv1 * ndot) * rlv, dc2 = (dnz - nv2 * ndot) * rlv;
+    // dL/d rnv = nJ^T dL/dcam_n ; nJ rows (1/tz, 0, tx/l), (0, 1/tz, ty/l), (-tx/tz^2, -ty/tz^2, tz/l)
+    const float drn0 = dc0 * itz - dc2 * tx * itz * itz;
+    const float drn1 = dc1 * itz - dc2 * ty * itz * itz;
+    // dL_dnJ (glm [i][j] = dc[j] * rn[i])
+    const float aux_nJ = (-(dc0 * rn2) * u - (dc1 * rn2) * v - dc2 * rn2) / rl2 * rl_inv;
+    const float du_nJ = -(dc2 * rn0) / tz + (dc0 * rn2) * rl_inv + aux_nJ * u;
+    const float dv_nJ = -(dc2 * rn1) / tz + (dc1 * rn2) * rl_inv + aux_nJ * v;
+    const float dz_nJ = ((dc0 * rn0) + (dc1 * rn1) - (dc2 * rn0) * u - (dc2 * rn1) * v) / (-tz * tz);
+    const float e0 = -drn0 + drpx, e1 = -drn1 + drpy;
+    const float dL_dfn = plx * e0 + ply * e1;
+    const float dpx = e0 * fn, dpy = e1 * fn;
+    const float aux = dpx * plx + dpy * ply;
+    // nJ_inv^T dpa, nJ_inv rows (v2+1, -uv, -u), (-uv, u2+1, -v), 0
+    const float nt0 = (v2 + 1.f) * dpx - uv * dpy;
+    const float nt1 = -uv * dpx + (u2 + 1.f) * dpy;
+    const float nt2 = -u * dpx - v * dpy;
+    const float icvb = 1.0f / clamp_vb;
+    const float duvh0 = 2.f * (-aux) * mv0 + (cinv[0] * nt0 + cinv[1] * nt1 + cinv[2] * nt2) * icvb;
+    const float duvh1 = 2.f * (-aux) * mv1 + (cinv[3] * nt0 + cinv[4] * nt1 + cinv[5] * nt2) * icvb;
+    const float rsigmat = sqrtf(vb / rl2);
+    const float drl2_sig = -dL_drsig * rsigmat / rl2;
+    // dL_dnJ_inv glm [i][j] = dpa[j] * mv[i]
+    const float E01 = dpy * mv0, E10 = dpx * mv1, E11 = dpy * mv1, E20 = dpx * mv2, E00 = dpx * mv0, E21 = dpy * mv2;
+    const float du_plane = duvh0 + (E01 + E10) * (-v) + 2.f * E11 * u - E20;
+    const float dv_plane = duvh1 + (E01 + E10) * (-u) + 2.f * E00 * v - E21;
+    const float aux_f = dL_dfn * (-tz / rl2 * rl_inv);
+    const float dL_du = du_nJ + du_plane + aux_f * u + drl2_sig * u;
+    const float dL_dv = dv_nJ + dv_plane + aux_f * v + drl2_sig * v;
+    const float dL_dz = dz_nJ + dL_dfn * rl_inv;
+    const float dvbx = -aux + dL_drsig * 0.5f * rsigmat;
+    // W_uvh = W_r^T uvh ; W nJ_inv^T dpa = W_r^T nt
+    float Wu[3], Wn[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        Wu[k] = Wr[k] * u + Wr[3 + k] * v + Wr[6 + k];
+        Wn[k] = Wr[k] * nt0 + Wr[3 + k] * nt1 + Wr[6 + k] * nt2;
+    }
+    float dVrk[9];  // glm layout dVrk[3*i + j] = dL_dVrk[i][j]
+    float dLr[3] = {0.f, 0.f, 0.f};
+    if (well_conditioned) {
+        float av[3], bv[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            av[i] = Vinv[3 * i] * Wu[0] + Vinv[3 * i + 1] * Wu[1] + Vinv[3 * i + 2] * Wu[2];
+            const float r0 = Wn[0] + Wu[0] * dvbx, r1 = Wn[1] + Wu[1] * dvbx, r2 = Wn[2] + Wu[2] * dvbx;
+            bv[i] = Vinv[3 * i] * r0 + Vinv[3 * i + 1] * r1 + Vinv[3 * i + 2] * r2;
+        }
+        // -outerProduct(av, bv) / vb : glm [i][j] = -av[j] * bv[i] / vb
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) dVrk[3 * i + j] = -(av[j] * bv[i]) / vb;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; k++) dVrk[k] = 0.f;
+        float rv[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) rv[k] = Wu[k] * dvbx + Wn[k];
+        // S = dL_dVrk_inv + transpose (symmetric), dL_dv = S e_min
+        const float* em = EV;  // eigenvector of the smallest eigenvalue
+        float dLdv[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            float acc_i = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) acc_i += ((Wu[i] * rv[j] + Wu[j] * rv[i]) / vb) * em[j];
+            dLdv[i] = acc_i;
+        }
+        if (a.scales) {
+            // R[min_id] with well_conditioned always true on this path (kept for completeness)
+        } else {
+#pragma unroll
+            for (int kk = 1; kk < 3; kk++) {
+                const float* ek = EV + 3 * kk;
+                const float sc = (ek[0] * dLdv[0] + ek[1] * dLdv[1] + ek[2] * dLdv[2]) / fminf(evl[0] - evl[kk], -1e-7f);
+#pragma unroll
+                for (int i = 0; i < 3; i++)
+#pragma unroll
+                    for (int j = 0; j < 3; j++) dVrk[3 * i + j] += (ek[j] * sc) * em[i];
+            }
+        }
+    }
+    // conic / coefficient backward (render_backward.cu:547-579)
+    const float opacity = a.opacities[idx];
+    const float dL_dcoef = dconw * opacity;
+    const float dL_dsqrtcoef = dL_dcoef * 0.5f / (coef + 1e-6f);
+    const float dL_ddet0 = dL_dsqrtcoef / det_1;
+    const float dL_ddet1 = -dL_ddet0 * coef;
+    const float dcoef_da = dL_ddet0 * c11 + dL_ddet1 * (c11 + ks);
+    const float dcoef_db = (-2.f * c01) * (dL_ddet0 + dL_ddet1);
+    const float dcoef_dc = dL_ddet0 * c00 + dL_ddet1 * (c00 + ks);
+    const float ca = c00 + ks, cb = c01, cc = c11 + ks;
+    const float denom = ca * cc - cb * cb;
+    const float denom2inv = 1.0f / ((denom * denom) + 1e-7f);
+    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+    float dcl[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float dopa = 0.f;
+    if (denom2inv != 0.f) {
+        dL_da = denom2inv * (-cc * cc * dconx + 2 * cb * cc * dcony + (denom - ca * cc) * dconz);
+        dL_dc = denom2inv * (-ca * ca * dconz + 2 * ca * cb * dcony + (denom - ca * cc) * dconx);
+        dL_db = denom2inv * 2 * (cb * cc * dconx - (denom + 2 * cb * cb) * dcony + ca * cb * dconz);
+        dL_da += dcoef_da;
+        dL_dc += dcoef_dc;
+        dL_db += dcoef_db;
+        dopa = dconw * coef;
+        dcl[0] = Q0[0] * Q0[0] * dL_da + Q0[0] * Q1[0] * dL_db + Q1[0] * Q1[0] * dL_dc;
+        dcl[3] = Q0[1] * Q0[1] * dL_da + Q0[1] * Q1[1] * dL_db + Q1[1] * Q1[1] * dL_dc;
+        dcl[5] = Q0[2] * Q0[2] * dL_da + Q0[2] * Q1[2] * dL_db + Q1[2] * Q1[2] * dL_dc;
+        dcl[1] = 2 * Q0[0] * Q0[1] * dL_da + (Q0[0] * Q1[1] + Q0[1] * Q1[0]) * dL_db + 2 * Q1[0] * Q1[1] * dL_dc;
+        dcl[2] = 2 * Q0[0] * Q0[2] * dL_da + (Q0[0] * Q1[2] + Q0[2] * Q1[0]) * dL_db + 2 * Q1[0] * Q1[2] * dL_dc;
+        dcl[4] = 2 * Q0[2] * Q0[1] * dL_da + (Q0[1] * Q1[2] + Q0[2] * Q1[1]) * dL_db + 2 * Q1[1] * Q1[2] * dL_dc;
+    }
+    a.dL_dopacity[idx] = dopa;
+    dcl[0] += dVrk[0];
+    dcl[3] += dVrk[4];
+    dcl[5] += dVrk[8];
+    dcl[1] += dVrk[1] + dVrk[3];
+    dcl[2] += dVrk[2] + dVrk[6];
+    dcl[4] += dVrk[5] + dVrk[7];
+
+    if (a.scales) {
+        // computeCov3D backward (render_backward.cu:193-244), math layout:
+        // R_m = R_q^T, M = S R_m, dL/dM = 2 M G, d[i][j] = dL/dR_m[i][j]
+        const float G[9] = {dcl[0], 0.5f * dcl[1], 0.5f * dcl[2], 0.5f * dcl[1], dcl[3],
+                            0.5f * dcl[4], 0.5f * dcl[2], 0.5f * dcl[4], dcl[5]};
+        float Rm[9];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) Rm[3 * i + j] = Rq[3 * j + i];
+        float d[9], dsc[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            float dM[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                dM[j] = 2.0f * s[i] * (Rm[3 * i] * G[j] + Rm[3 * i + 1] * G[3 + j] + Rm[3 * i + 2] * G[6 + j]);
+            dsc[i] = Rm[3 * i] * dM[0] + Rm[3 * i + 1] * dM[1] + Rm[3 * i + 2] * dM[2];
+#pragma unroll
+            for (int j = 0; j < 3; j++) d[3 * i + j] = dM[j] * s[i];
+        }
+        (void)dLr;
+        a.dL_dscale[3 * idx] = dsc[0];
+        a.dL_dscale[3 * idx + 1] = dsc[1];
+        a.dL_dscale[3 * idx + 2] = dsc[2];
+        const float* q = a.rotations + 4 * idx;
+        const float r = q[0], x = q[1], y = q[2], z = q[3];
+#define D_(i, j) d[3 * (i) + (j)]
+        a.dL_drot[4 * idx + 0] = 2 * z * (D_(0, 1) - D_(1, 0)) + 2 * y * (D_(2, 0) - D_(0, 2)) + 2 * x * (D_(1, 2) - D_(2, 1));
+        a.dL_drot[4 * idx + 1] = 2 * y * (D_(1, 0) + D_(0, 1)) + 2 * z * (D_(2, 0) + D_(0, 2)) +
+                                 2 * r * (D_(1, 2) - D_(2, 1)) - 4 * x * (D_(2, 2) + D_(1, 1));
+        a.dL_drot[4 * idx + 2] = 2 * x * (D_(1, 0) + D_(0, 1)) + 2 * r * (D_(2, 0) - D_(0, 2)) +
+                                 2 * z * (D_(1, 2) + D_(2, 1)) - 4 * y * (D_(2, 2) + D_(0, 0));
+        a.dL_drot[4 * idx + 3] = 2 * r * (D_(0, 1) - D_(1, 0)) + 2 * x * (D_(2, 0) + D_(0, 2)) +
+                                 2 * y * (D_(1, 2) + D_(2, 1)) - 4 * z * (D_(1, 1) + D_(0, 0));
+#undef D_
+        if (a.dL_dcov3D)
+            for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = 0.f;
+    } else {
+        for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = dcl[k];
+        if (a.dL_dscale)
+            for (int k = 0; k < 3; k++) a.dL_dscale[3 * idx + k] = 0.f;
+        if (a.dL_drot)
+            for (int k = 0; k < 4; k++) a.dL_drot[4 * idx + k] = 0.f;
+    }
+
+    // dL/dT -> dL/dJ -> dL/dt (render_backward.cu:613-646)
+    float dQ0[3], dQ1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float vq0 = Vrk[3 * k] * Q0[0] + Vrk[3 * k + 1] * Q0[1] + Vrk[3 * k + 2] * Q0[2];
+        const float vq1 = Vrk[3 * k] * Q1[0] + Vrk[3 * k + 1] * Q1[1] + Vrk[3 * k + 2] * Q1[2];
+        dQ0[k] = 2 * vq0 * dL_da + vq1 * dL_db;
+        dQ1[k] = 2 * vq1 * dL_dc + vq0 * dL_db;
+    }
+    const float dJ00 = Wr[0] * dQ0[0] + Wr[1] * dQ0[1] + Wr[2] * dQ0[2];
+    const float dJ02 = Wr[6] * dQ0[0] + Wr[7] * dQ0[1] + Wr[8] * dQ0[2];
+    const float dJ11 = Wr[3] * dQ1[0] + Wr[4] * dQ1[1] + Wr[5] * dQ1[2];
+    const float dJ12 = Wr[6] * dQ1[0] + Wr[7] * dQ1[1] + Wr[8] * dQ1[2];
+    const float tz1 = 1.f / tz, tz2 = tz1 * tz1, tz3 = tz2 * tz1;
+    const float dtx = xgm * (-fx * tz2 * dJ02 + dL_du * tz1);
+    const float dty = ygm * (-fy * tz2 * dJ12 + dL_dv * tz1);
+    const float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + ((1 + xgm) * fx * tx) * tz3 * dJ02 +
+                      ((1 + ygm) * fy * ty) * tz3 * dJ12 - (xgm * dL_du * tx + ygm * dL_dv * ty) * tz2 + dL_dz;
+    const float gx_ = dtx + dtc_x, gy_ = dty + dtc_y, gz_ = dtz + dtc_z;
+    float dm0 = V[0] * gx_ + V[1] * gy_ + V[2] * gz_;
+    float dm1 = V[4] * gx_ + V[5] * gy_ + V[6] * gz_;
+    float dm2 = V[8] * gx_ + V[9] * gy_ + V[10] * gz_;
+
+    // ---------------- preprocessCUDA backward: screen-space mean ----------------
+    const float* Pm = a.proj;
+    const float hw = Pm[3] * mx + Pm[7] * my + Pm[11] * mz + Pm[15];
+    const float m_w = 1.0f / (hw + 0.0000001f);
+    const float mul1 = (Pm[0] * mx + Pm[4] * my + Pm[8] * mz + Pm[12]) * m_w * m_w;
+    const float mul2 = (Pm[1] * mx + Pm[5] * my + Pm[9] * mz + Pm[13]) * m_w * m_w;
+    const float g2x = acc[kAccMean2D + 0], g2y = acc[kAccMean2D + 1];
+    dm0 += (Pm[0] * m_w - Pm[3] * mul1) * g2x + (Pm[1] * m_w - Pm[3] * mul2) * g2y;
+    dm1 += (Pm[4] * m_w - Pm[7] * mul1) * g2x + (Pm[5] * m_w - Pm[7] * mul2) * g2y;
+    dm2 += (Pm[8] * m_w - Pm[11] * mul1) * g2x + (Pm[9] * m_w - Pm[11] * mul2) * g2y;
+
+    // ---------------- SH / SG colour backward ----------------
+    if (a.shs) {
+        const float dox = mx - a.campos[0], doy = my - a.campos[1], doz = mz - a.campos[2];
+        const float dlen = sqrtf(dox * dox + doy * doy + doz * doz);
+        const float x = dox / dlen, y = doy / dlen, z = doz / dlen;
+        const uint8_t cl = a.clamped[idx];
+        const float dR0 = (cl & 1) ? 0.f : acc[kAccColor + 0];
+        const float dR1 = (cl & 2) ? 0.f : acc[kAccColor + 1];
+        const float dR2 = (cl & 4) ? 0.f : acc[kAccColor + 2];
+        float Y[16];
+        sh_basis(a.D, x, y, z, Y);
+        const int n = sh_count(a.D);
+        const float* sh = a.shs + (size_t)idx * a.SHM * 3;
+        float* dsh = a.dL_dsh + (size_t)idx * a.SHM * 3;
+        for (int k = 0; k < n; k++) {
+            dsh[3 * k] = Y[k] * dR0;
+            dsh[3 * k + 1] = Y[k] * dR1;
+            dsh[3 * k + 2] = Y[k] * dR2;
+        }
+        for (int k = 3 * n; k < 3 * a.SHM; k++) dsh[k] = 0.f;
+        // d(colour)/d(dir) per channel: dx/dy/dz (render_backward.cu:94-153)
+        float gdx[3] = {0.f, 0.f, 0.f}, gdy[3] = {0.f, 0.f, 0.f}, gdz[3] = {0.f, 0.f, 0.f};
+        if (a.D > 0) {
+            for (int c = 0; c < 3; c++) {
+                const float s1 = sh[3 * 1 + c], s2 = sh[3 * 2 + c], s3 = sh[3 * 3 + c];
+                gdx[c] = -kSH_C1 * s3;
+                gdy[c] = -kSH_C1 * s1;
+                gdz[c] = kSH_C1 * s2;
+            }
+            if (a.D > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                for (int c = 0; c < 3; c++) {
+                    const float s4 = sh[12 + c], s5 = sh[15 + c], s6 = sh[18 + c], s7 = sh[21 + c], s8 = sh[24 + c];
+                    gdx[c] += kSH_C2[0] * y * s4 + kSH_C2[2] * 2.f * -x * s6 + kSH_C2[3] * z * s7 + kSH_C2[4] * 2.f * x * s8;
+                    gdy[c] += kSH_C2[0] * x * s4 + kSH_C2[1] * z * s5 + kSH_C2[2] * 2.f * -y * s6 + kSH_C2[4] * 2.f * -y * s8;
+                    gdz[c] += kSH_C2[1] * y * s5 + kSH_C2[2] * 2.f * 2.f * z * s6 + kSH_C2[3] * x * s7;
+                }
+                if (a.D > 2) {
+                    for (int c = 0; c < 3; c++) {
+                        const float s9 = sh[27 + c], s10 = sh[30 + c], s11 = sh[33 + c], s12 = sh[36 + c],
+                                    s13 = sh[39 + c], s14 = sh[42 + c], s15 = sh[45 + c];
+                        gdx[c] += kSH_C3[0] * s9 * 3.f * 2.f * xy + kSH_C3[1] * s10 * yz + kSH_C3[2] * s11 * -2.f * xy +
+                                  kSH_C3[3] * s12 * -3.f * 2.f * xz + kSH_C3[4] * s13 * (-3.f * xx + 4.f * zz - yy) +
+                                  kSH_C3[5] * s14 * 2.f * xz + kSH_C3[6] * s15 * 3.f * (xx - yy);
+                        gdy[c] += kSH_C3[0] * s9 * 3.f * (xx - yy) + kSH_C3[1] * s10 * xz +
+                                  kSH_C3[2] * s11 * (-3.f * yy + 4.f * zz - xx) + kSH_C3[3] * s12 * -3.f * 2.f * yz +
+                                  kSH_C3[4] * s13 * -2.f * xy + kSH_C3[5] * s14 * -2.f * yz +
+                                  kSH_C3[6] * s15 * -3.f * 2.f * xy;
+                        gdz[c] += kSH_C3[1] * s10 * xy + kSH_C3[2] * s11 * 4.f * 2.f * yz +
+                                  kSH_C3[3] * s12 * 3.f * (2.f * zz - xx - yy) + kSH_C3[4] * s13 * 4.f * 2.f * xz +
+                                  kSH_C3[5] * s14 * (xx - yy);
+                    }
+                }
+            }
+        }
+        float ddx = gdx[0] * dR0 + gdx[1] * dR1 + gdx[2] * dR2;
+        float ddy = gdy[0] * dR0 + gdy[1] * dR1 + gdy[2] * dR2;
+        float ddz = gdz[0] * dR0 + gdz[1] * dR1 + gdz[2] * dR2;
+        for (int sg = 0; sg < a.SGM; sg++) {
+            const size_t o = (size_t)idx * a.SGM + sg;
+            if (sg >= a.SGD) {
+                a.dL_dsg_sharpness[o] = 0.f;
+                for (int c = 0; c < 3; c++) {
+                    a.dL_dsg_axis[3 * o + c] = 0.f;
+                    a.dL_dsg_color[3 * o + c] = 0.f;
+                }
+                continue;
+            }
+            const float* ax = a.sg_axis + 3 * o;
+            const float* gc = a.sg_color + 3 * o;
+            const float sharp = a.sg_sharpness[o];
+            const float auxs = (ax[0] * x + ax[1] * y + ax[2] * z) - 1.0f;
+            const float gs = expf(sharp * auxs);
+            a.dL_dsg_color[3 * o + 0] = dR0 * gs;
+            a.dL_dsg_color[3 * o + 1] = dR1 * gs;
+            a.dL_dsg_color[3 * o + 2] = dR2 * gs;
+            const float dL_dgs = gc[0] * dR0 + gc[1] * dR1 + gc[2] * dR2;
+            const float dL_dexp = dL_dgs * gs;
+            a.dL_dsg_sharpness[o] = dL_dexp * auxs;
+            const float dL_daux = dL_dexp * sharp;
+            a.dL_dsg_axis[3 * o + 0] = dL_daux * x;
+            a.dL_dsg_axis[3 * o + 1] = dL_daux * y;
+            a.dL_dsg_axis[3 * o + 2] = dL_daux * z;
+            ddx += dL_daux * ax[0];
+            ddy += dL_daux * ax[1];
+            ddz += dL_daux * ax[2];
+        }
+        // dnormvdv (auxiliary.h:104-113)
+        const float inv = 1.0f / dlen;
+        const float vx = dox * inv, vy = doy * inv, vz = doz * inv;
+        dm0 += ((1.f - vx * vx) * ddx - vy * vx * ddy - vz * vx * ddz) * inv;
+        dm1 += (-vx * vy * ddx + (1.f - vy * vy) * ddy - vz * vy * ddz) * inv;
+        dm2 += (-vx * vz * ddx - vy * vz * ddy + (1.f - vz * vz) * ddz) * inv;
+    } else {
+        for (int sg = 0; sg < a.SGM; sg++) {
+            const size_t o = (size_t)idx * a.SGM + sg;
+            if (a.dL_dsg_sharpness) a.dL_dsg_sharpness[o] = 0.f;
+            for (int c = 0; c < 3; c++) {
+                if (a.dL_dsg_axis) a.dL_dsg_axis[3 * o + c] = 0.f;
+                if (a.dL_dsg_color) a.dL_dsg_color[3 * o + c] = 0.f;
+            }
+        }
+        if (a.dL_dsh)
+            for (int k = 0; k < 3 * a.SHM; k++) a.dL_dsh[(size_t)idx * 3 * a.SHM + k] = 0.f;
+    }
+    a.dL_dmean3D[3 * idx] = dm0;
+    a.dL_dmean3D[3 * idx + 1] = dm1;
+    a.dL_dmean3D[3 * idx + 2] = dm2;
+}
+
+hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const BwdState& ws, hipStream_t stream) {
+    const FwdParams& p = b.f;
+    if (p.P == 0) return hipSuccess;
+    PreprocessBwdArgs a;
+    a.P = p.P;
+    a.D = p.D;
+    a.SHM = p.SHM;
+    a.SGD = p.SGD;
+    a.SGM = p.SGM;
+    a.means3D = p.means3D;
+    a.opacities = p.opacities;
+    a.scales = p.scales;
+    a.rotations = p.rotations;
+    a.cov3D_precomp = p.cov3D_precomp;
+    a.shs = p.shs;
+    a.sg_axis = p.sg_axis;
+    a.sg_sharpness = p.sg_sharpness;
+    a.sg_color = p.sg_color;
+    a.scale_modifier = p.scale_modifier;
+    a.view = p.view;
+    a.proj = p.proj;
+    a.campos = p.campos;
+    a.tan_fovx = p.tan_fovx;
+    a.tan_fovy = p.tan_fovy;
+    a.focal_x = p.focal_x;
+    a.focal_y = p.focal_y;
+    a.kernel_size = p.kernel_size;
+    a.radii = b.radii;
+    a.clamped = gs.clamped;
+    a.acc = ws.acc;
+    a.acc_abs = ws.acc_abs;
+    a.dL_dmean3D = b.dL_dmean3D;
+    a.dL_dmean2D = b.dL_dmean2D;
+    a.dL_dcolor = b.dL_dcolor;
+    a.dL_dopacity = b.dL_dopacity;
+    a.dL_dscale = b.dL_dscale;
+    a.dL_drot = b.dL_drot;
+    a.dL_dcov3D = b.dL_dcov3D;
+    a.dL_dsh = b.dL_dsh;
+    a.dL_dsg_axis = b.dL_dsg_axis;
+    a.dL_dsg_sharpness = b.dL_dsg_sharpness;
+    a.dL_dsg_color = b.dL_dsg_color;
+    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -1,0 +1,274 @@
+// preprocess_fwd.hip — per-Gaussian forward preprocess on gfx950.
+//
+// Replaces FORWARD::preprocess / preprocessCUDA (render_forward.cu:283-386,
+// 710-774) together with computeCov2D (:81-243) and computeColorFromSHSG
+// (:22-78).  One lane per Gaussian; every output a later kernel gathers is
+// packed into one 64-B Splat record (gsr_common.h) so the render kernels
+// fetch a Gaussian with four 16-B loads.
+//
+// Outputs per Gaussian: radii (int32, the extension output), tiles_touched,
+// depth (= |p_view|, the sort key, render_forward.cu:380), clamped bits, and
+// the Splat record (only for Gaussians with radius > 0; the others are never
+// gathered).
+#include "gsr_kernels.h"
+#include "gsr_math.h"
+
+namespace gsr {
+
+struct PreprocessArgs {
+    int P, D, SHM, SGD, SGM, W, H;
+    const float* means3D;
+    const float* colors_precomp;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+    const float* shs;
+    const float* sg_axis;
+    const float* sg_sharpness;
+    const float* sg_color;
+    float scale_modifier;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float tan_fovx, tan_fovy, focal_x, focal_y, kernel_size;
+    uint32_t grid_x, grid_y;
+    int* radii;
+    uint8_t* clamped;
+    float* depths;
+    Splat* splats;
+    uint32_t* tiles_touched;
+};
+
+// ndc2Pix in double, as the reference (auxiliary.h:38-40)
+__device__ inline float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+__global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    a.radii[idx] = 0;
+    a.tiles_touched[idx] = 0;
+
+    const float px = a.means3D[3 * idx], py = a.means3D[3 * idx + 1], pz = a.means3D[3 * idx + 2];
+    const float* V = a.view;
+    const ViewGeom g = view_geom(V, px, py, pz, a.tan_fovx, a.tan_fovy);
+    if (g.t[2] <= kNearPlane) return;  // in_frustum (auxiliary.h:133-153)
+
+    const float* Pm = a.proj;
+    const float hx = Pm[0] * px + Pm[4] * py + Pm[8] * pz + Pm[12];
+    const float hy = Pm[1] * px + Pm[5] * py + Pm[9] * pz + Pm[13];
+    const float hw = Pm[3] * px + Pm[7] * py + Pm[11] * pz + Pm[15];
+    const float p_w = 1.0f / (hw + 0.0000001f);
+
+    const float fx = a.focal_x, fy = a.focal_y;
+    const float tz = g.tz, itz = 1.0f / tz;
+    float A[9], Rq[9], s[3];
+    float cinv[9];  // cov_cam_inv (row-major, symmetric)
+    float cov00, cov01, cov11;
+    bool well_conditioned = true;
+    if (a.scales) {
+        const float* q = a.rotations + 4 * idx;
+        rot_view(V, q[0], q[1], q[2], q[3], A, Rq);
+        s[0] = a.scale_modifier * a.scales[3 * idx];
+        s[1] = a.scale_modifier * a.scales[3 * idx + 1];
+        s[2] = a.scale_modifier * a.scales[3 * idx + 2];
+        // B = J A S (2x3): J rows (fx/tz, 0, -fx tx/tz^2), (0, fy/tz, -fy ty/tz^2)
+        const float j00 = fx * itz, j02 = -(fx * g.tx) / (tz * tz);
+        const float j11 = fy * itz, j12 = -(fy * g.ty) / (tz * tz);
+        float B0[3], B1[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            B0[k] = (j00 * A[k] + j02 * A[6 + k]) * s[k];
+            B1[k] = (j11 * A[3 + k] + j12 * A[6 + k]) * s[k];
+        }
+        cov00 = B0[0] * B0[0] + B0[1] * B0[1] + B0[2] * B0[2];
+        cov01 = B0[0] * B1[0] + B0[1] * B1[1] + B0[2] * B1[2];
+        cov11 = B1[0] * B1[0] + B1[1] * B1[1] + B1[2] * B1[2];
+        const float is2[3] = {1.0f / (s[0] * s[0]), 1.0f / (s[1] * s[1]), 1.0f / (s[2] * s[2])};
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                cinv[3 * i + j] = A[3 * i] * A[3 * j] * is2[0] + A[3 * i + 1] * A[3 * j + 1] * is2[1] +
+                                  A[3 * i + 2] * A[3 * j + 2] * is2[2];
+    } else {
+        // cov3D_precomp path (render_forward.cu:162-189): Vrk given; the
+        // camera-space inverse via the adjugate when Vrk is well conditioned,
+        // else the projector onto the eigenvector of the smallest eigenvalue.
+        const float* c = a.cov3D_precomp + 6 * idx;
+        const float Vk[9] = {c[0], c[1], c[2], c[1], c[3], c[4], c[2], c[4], c[5]};
+        float Vinv[9];
+        well_conditioned = sym3_inverse_or_null_projector(Vk, Vinv);
+        // cov2D = J W_r Vrk W_r^T J^T ; cov_cam_inv = W_r Vinv W_r^T
+        float Wr[9];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) Wr[3 * i + j] = V[4 * j + i];
+        const float j00 = fx * itz, j02 = -(fx * g.tx) / (tz * tz);
+        const float j11 = fy * itz, j12 = -(fy * g.ty) / (tz * tz);
+        float T0[3], T1[3];  // rows of J W_r
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            T0[k] = j00 * Wr[k] + j02 * Wr[6 + k];
+            T1[k] = j11 * Wr[3 + k] + j12 * Wr[6 + k];
+        }
+        float VT0[3], VT1[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            VT0[i] = Vk[3 * i] * T0[0] + Vk[3 * i + 1] * T0[1] + Vk[3 * i + 2] * T0[2];
+            VT1[i] = Vk[3 * i] * T1[0] + Vk[3 * i + 1] * T1[1] + Vk[3 * i + 2] * T1[2];
+        }
+        cov00 = T0[0] * VT0[0] + T0[1] * VT0[1] + T0[2] * VT0[2];
+        cov01 = T0[0] * VT1[0] + T0[1] * VT1[1] + T0[2] * VT1[2];
+        cov11 = T1[0] * VT1[0] + T1[1] * VT1[1] + T1[2] * VT1[2];
+        float WV[9];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                WV[3 * i + j] = Wr[3 * i] * Vinv[j] + Wr[3 * i + 1] * Vinv[3 + j] + Wr[3 * i + 2] * Vinv[6 + j];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                cinv[3 * i + j] = WV[3 * i] * Wr[3 * j] + WV[3 * i + 1] * Wr[3 * j + 1] + WV[3 * i + 2] * Wr[3 * j + 2];
+    }
+    const float k = a.kernel_size;
+    const float det_0 = fmaxf(1e-6f, cov00 * cov11 - cov01 * cov01);
+    const float det_1 = fmaxf(1e-6f, (cov00 + k) * (cov11 + k) - cov01 * cov01);
+    const float coef = sqrtf(det_0 / det_1);
+    const float ca = cov00 + k, cb = cov01, cc = cov11 + k;
+
+    // ray-plane and normal (render_forward.cu:207-241)
+    const float u = g.u, v = g.v;
+    const float m0 = cinv[0] * u + cinv[1] * v + cinv[2];
+    const float m1 = cinv[3] * u + cinv[4] * v + cinv[5];
+    const float m2 = cinv[6] * u + cinv[7] * v + cinv[8];
+    const float vb = m0 * u + m1 * v + m2;
+    const float u2 = u * u, v2 = v * v, uv = u * v;
+    const float l = sqrtf(g.tx * g.tx + g.ty * g.ty + tz * tz);
+    const float rl2 = u2 + v2 + 1.f;
+    const float fnorm = l / rl2;
+    const float ivb = 1.0f / vb;
+    const float plx = ((v2 + 1.f) * m0 - uv * m1 - u * m2) * ivb;
+    const float ply = (-uv * m0 + (u2 + 1.f) * m1 - v * m2) * ivb;
+    const float rsig = well_conditioned ? sqrtf(vb / rl2) : 0.f;
+    const float rnx = -plx * fnorm, rny = -ply * fnorm;
+    const float il = 1.0f / l;
+    const float cnx = rnx * itz - g.tx * il;
+    const float cny = rny * itz - g.ty * il;
+    const float cnz = -(g.tx * itz * itz) * rnx - (g.ty * itz * itz) * rny - tz * il;
+    const float inn = 1.0f / sqrtf(cnx * cnx + cny * cny + cnz * cnz);
+
+    // conic, radius, rect (render_forward.cu:347-368)
+    const float det = ca * cc - cb * cb;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float mid = 0.5f * (ca + cc);
+    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float radius = ceilf(3.f * sqrtf(lambda1));
+    const float xpix = ndc2pix(hx * p_w, a.W), ypix = ndc2pix(hy * p_w, a.H);
+    const int r = (int)radius;
+    const uint32_t rminx = min(a.grid_x, (uint32_t)max(0, (int)((xpix - r) / kTile)));
+    const uint32_t rminy = min(a.grid_y, (uint32_t)max(0, (int)((ypix - r) / kTile)));
+    const uint32_t rmaxx = min(a.grid_x, (uint32_t)max(0, (int)((xpix + r + kTile - 1) / kTile)));
+    const uint32_t rmaxy = min(a.grid_y, (uint32_t)max(0, (int)((ypix + r + kTile - 1) / kTile)));
+    const uint32_t area = (rmaxx - rminx) * (rmaxy - rminy);
+    if (area == 0) return;
+
+    // colour (render_forward.cu:22-78)
+    float col[3];
+    if (a.colors_precomp == nullptr) {
+        float dx = px - a.campos[0], dy = py - a.campos[1], dz = pz - a.campos[2];
+        const float dl = sqrtf(dx * dx + dy * dy + dz * dz);
+        dx /= dl;
+        dy /= dl;
+        dz /= dl;
+        float Y[16];
+        sh_basis(a.D, dx, dy, dz, Y);
+        const int n = sh_count(a.D);
+        const float* sh = a.shs + (size_t)idx * a.SHM * 3;
+        col[0] = Y[0] * sh[0];
+        col[1] = Y[0] * sh[1];
+        col[2] = Y[0] * sh[2];
+        for (int kk = 1; kk < n; kk++) {
+            col[0] += Y[kk] * sh[3 * kk];
+            col[1] += Y[kk] * sh[3 * kk + 1];
+            col[2] += Y[kk] * sh[3 * kk + 2];
+        }
+        for (int sg = 0; sg < a.SGD; sg++) {
+            const size_t o = (size_t)idx * a.SGM + sg;
+            const float* ax = a.sg_axis + 3 * o;
+            const float* sc = a.sg_color + 3 * o;
+            const float gs = expf(a.sg_sharpness[o] * ((ax[0] * dx + ax[1] * dy + ax[2] * dz) - 1.0f));
+            col[0] += sc[0] * gs;
+            col[1] += sc[1] * gs;
+            col[2] += sc[2] * gs;
+        }
+        col[0] += 0.5f;
+        col[1] += 0.5f;
+        col[2] += 0.5f;
+        a.clamped[idx] = (uint8_t)((col[0] < 0) | ((col[1] < 0) << 1) | ((col[2] < 0) << 2));
+        col[0] = fmaxf(col[0], 0.f);
+        col[1] = fmaxf(col[1], 0.f);
+        col[2] = fmaxf(col[2], 0.f);
+    } else {
+        col[0] = a.colors_precomp[3 * idx];
+        col[1] = a.colors_precomp[3 * idx + 1];
+        col[2] = a.colors_precomp[3 * idx + 2];
+        a.clamped[idx] = 0;
+    }
+
+    Splat sp;
+    sp.w0 = make_float4(xpix, ypix, cc * det_inv, -cb * det_inv);
+    sp.w1 = make_float4(ca * det_inv, a.opacities[idx] * coef, plx * fnorm / fx, ply * fnorm / fy);
+    sp.w2 = make_float4(g.tc, rsig, col[0], col[1]);
+    sp.w3 = make_float4(col[2], cnx * inn, cny * inn, cnz * inn);
+    a.splats[idx] = sp;
+    a.depths[idx] = g.tc;
+    a.radii[idx] = r;
+    a.tiles_touched[idx] = area;
+}
+
+hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* radii, hipStream_t stream) {
+    if (p.P == 0) return hipSuccess;
+    PreprocessArgs a;
+    a.P = p.P;
+    a.D = p.D;
+    a.SHM = p.SHM;
+    a.SGD = p.SGD;
+    a.SGM = p.SGM;
+    a.W = p.W;
+    a.H = p.H;
+    a.means3D = p.means3D;
+    a.colors_precomp = p.colors_precomp;
+    a.opacities = p.opacities;
+    a.scales = p.scales;
+    a.rotations = p.rotations;
+    a.cov3D_precomp = p.cov3D_precomp;
+    a.shs = p.shs;
+    a.sg_axis = p.sg_axis;
+    a.sg_sharpness = p.sg_sharpness;
+    a.sg_color = p.sg_color;
+    a.scale_modifier = p.scale_modifier;
+    a.view = p.view;
+    a.proj = p.proj;
+    a.campos = p.campos;
+    a.tan_fovx = p.tan_fovx;
+    a.tan_fovy = p.tan_fovy;
+    a.focal_x = p.focal_x;
+    a.focal_y = p.focal_y;
+    a.kernel_size = p.kernel_size;
+    a.grid_x = p.grid_x;
+    a.grid_y = p.grid_y;
+    a.radii = radii;
+    a.clamped = gs.clamped;
+    a.depths = gs.depths;
+    a.splats = gs.splats;
+    a.tiles_touched = gs.tiles_touched;
+    hipLaunchKernelGGL(preprocess_fwd_kernel, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

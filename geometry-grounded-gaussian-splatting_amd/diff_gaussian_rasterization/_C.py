@@ -1,0 +1,206 @@
+"""`_C` — the extension entry points of the reference, bound to libgsr.so.
+
+Mirrors the pybind module of the reference (DGR/ext.cpp:15-23) with the same
+names, argument order, return tuples and error behaviour:
+
+  rasterize_gaussians(25 args)           -> (num_rendered, color, alpha, normal, mdepth, radii,
+                                             geomBuffer, binningBuffer, imgBuffer, tileBuffer)
+                                             (DGR/rasterize_points.cu:39-139)
+  rasterize_gaussians_backward(35 args)  -> (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh,
+                                             dsg_axis, dsg_sharpness, dsg_color, dscales, drotations)
+                                             (DGR/rasterize_points.cu:141-258)
+  mark_visible(means3D, view, proj)      -> bool[P]  (DGR/rasterize_points.cu:260-277)
+
+The C ABI (include/gsr.h) takes raw device pointers and allocation callbacks;
+here torch provides the memory (caching allocator), the current HIP stream and
+the uint8 scratch tensors that autograd keeps alive between forward and
+backward.  There is no CPU fallback: inputs must be HIP (cuda) tensors and the
+shared library must load, otherwise these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgsr.so")
+
+_ALLOC = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libgsr.so not built ({LIB_PATH}); run `make -C geometry-grounded-gaussian-splatting_amd` "
+                           "or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    L.gsr_rasterize_forward.restype = i
+    L.gsr_rasterize_forward.argtypes = ([_ALLOC, vp] * 4 + [i] * 5 + [vp, i, i] + [vp] * 10 + [f] + [vp] * 3
+                                        + [f] * 3 + [i] + [vp] * 5 + [i, i, vp, ctypes.POINTER(i)])
+    L.gsr_rasterize_backward.restype = i
+    L.gsr_rasterize_backward.argtypes = ([_ALLOC, vp] + [i] * 6 + [vp, i, i] + [vp] * 10 + [f] + [vp] * 3
+                                         + [f] * 3 + [vp] * 4 + [vp] * 4 + [vp] * 4 + [vp] * 11 + [i, i, vp])
+    L.gsr_mark_visible.restype = i
+    L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
+    L.gsr_last_error.restype = ctypes.c_char_p
+    L.gsr_abi_version.restype = i
+    _lib = L
+    return L
+
+
+def loaded_library_path() -> str:
+    _load()
+    return LIB_PATH
+
+
+class _ByteBuffer:
+    """A resizable torch.uint8 device tensor handed to the C ABI as a callback
+    (replaces resizeFunctional, DGR/rasterize_points.cu:27-37)."""
+
+    def __init__(self, device, zero: bool = False):
+        self.device = device
+        self.zero = zero
+        self.tensor = torch.empty(0, dtype=torch.uint8, device=device)
+
+        def _cb(_ctx, n):
+            try:
+                self.tensor = (torch.zeros if self.zero else torch.empty)(int(n), dtype=torch.uint8,
+                                                                           device=self.device)
+                return self.tensor.data_ptr() if n else self.tensor.data_ptr() or 1
+            except Exception:  # noqa: BLE001 - allocation failure is reported as NULL
+                return None
+
+        self.cb = _ALLOC(_cb)
+
+
+def _ptr(t):
+    if t is None or t.numel() == 0:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _dev_contig(t, name):
+    if t is None:
+        return None
+    if t.numel() == 0:
+        return t
+    if not t.is_cuda:
+        raise RuntimeError(f"gsr: `{name}` must be a HIP device tensor (got {t.device})")
+    if t.dtype != torch.float32 and name not in ("radii",):
+        raise RuntimeError(f"gsr: `{name}` must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError("gsr: " + _lib.gsr_last_error().decode())
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, cov3D_precomp, sh, sg_axis,
+                        sg_sharpness, sg_color, sh_degree, sg_degree, scale_modifier, viewmatrix, projmatrix,
+                        tan_fovx, tan_fovy, kernel_size, image_height, image_width, campos, prefiltered,
+                        require_depth, debug):
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    L = _load()
+    P = means3D.size(0)
+    H, W = int(image_height), int(image_width)
+    dev = means3D.device
+    fopt = dict(dtype=torch.float32, device=dev)
+    if P == 0:  # rasterize_points.cu:77-95: zero outputs, nothing rendered
+        bufs = [torch.empty(0, dtype=torch.uint8, device=dev) for _ in range(4)]
+        return (0, torch.zeros(3, H, W, **fopt), torch.zeros(1, H, W, **fopt), torch.zeros(3, H, W, **fopt),
+                torch.zeros(1, H, W, **fopt), torch.zeros(0, dtype=torch.int32, device=dev), *bufs)
+    args = {k: _dev_contig(v, k) for k, v in dict(
+        background=background, means3D=means3D, colors=colors, opacity=opacity, scales=scales,
+        rotations=rotations, cov3D_precomp=cov3D_precomp, sh=sh, sg_axis=sg_axis, sg_sharpness=sg_sharpness,
+        sg_color=sg_color, viewmatrix=viewmatrix, projmatrix=projmatrix, campos=campos).items()}
+    SHM = sh.size(1) if sh is not None and sh.size(0) != 0 else 0
+    SGM = sg_color.size(1) if sg_color is not None and sg_color.size(0) != 0 else 0
+    color = torch.empty(3, H, W, **fopt)
+    mdepth = torch.empty(1, H, W, **fopt)
+    alpha = torch.empty(1, H, W, **fopt)
+    normal = torch.empty(3, H, W, **fopt)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)
+    bufs = [_ByteBuffer(dev) for _ in range(4)]
+    K = ctypes.c_int(0)
+    with torch.cuda.device(dev):
+        rc = L.gsr_rasterize_forward(
+            bufs[0].cb, None, bufs[1].cb, None, bufs[2].cb, None, bufs[3].cb, None,
+            P, int(sh_degree), SHM, int(sg_degree), SGM, _ptr(args["background"]), W, H, _ptr(args["means3D"]),
+            _ptr(args["colors"]), _ptr(args["opacity"]), _ptr(args["scales"]), _ptr(args["rotations"]),
+            _ptr(args["cov3D_precomp"]), _ptr(args["sh"]), _ptr(args["sg_axis"]), _ptr(args["sg_sharpness"]),
+            _ptr(args["sg_color"]), float(scale_modifier), _ptr(args["viewmatrix"]), _ptr(args["projmatrix"]),
+            _ptr(args["campos"]), float(tan_fovx), float(tan_fovy), float(kernel_size), int(bool(prefiltered)),
+            _ptr(color), _ptr(mdepth), _ptr(alpha), _ptr(normal), _ptr(radii), int(bool(require_depth)),
+            int(bool(debug)), _stream(dev), ctypes.byref(K))
+    _check(rc)
+    return (K.value, color, alpha, normal, mdepth, radii, bufs[0].tensor, bufs[1].tensor, bufs[2].tensor,
+            bufs[3].tensor)
+
+
+def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, rotations, cov3D_precomp, sh,
+                                 sg_axis, sg_sharpness, sg_color, sh_degree, sg_degree, scale_modifier, viewmatrix,
+                                 projmatrix, tan_fovx, tan_fovy, kernel_size, dL_dout_color, dL_dout_mdepth,
+                                 dL_dout_alpha, dL_dout_normal, alphas, normalmap, mdepth, campos, radii,
+                                 geomBuffer, R, binningBuffer, imageBuffer, tileBuffer, require_depth, debug):
+    L = _load()
+    P = means3D.size(0)
+    H, W = dL_dout_color.size(1), dL_dout_color.size(2)
+    SHM = sh.size(1) if sh is not None and sh.size(0) != 0 else 0
+    SGM = sg_color.size(1) if sg_color is not None and sg_color.size(0) != 0 else 0
+    dev = means3D.device
+    fopt = dict(dtype=torch.float32, device=dev)
+    alloc = torch.zeros if P == 0 else torch.empty  # the kernels overwrite every element
+    outs = dict(dmeans3D=alloc(P, 3, **fopt), dmeans2D=alloc(P, 3, **fopt), dcolors=alloc(P, 3, **fopt),
+                dopacity=alloc(P, 1, **fopt), dcov3D=alloc(P, 6, **fopt), dsh=alloc(P, SHM, 3, **fopt),
+                dsg_axis=alloc(P, SGM, 3, **fopt), dsg_sharpness=alloc(P, SGM, **fopt),
+                dsg_color=alloc(P, SGM, 3, **fopt), dscales=alloc(P, 3, **fopt), drotations=alloc(P, 4, **fopt))
+    if P != 0:
+        a = {k: _dev_contig(v, k) for k, v in dict(
+            background=background, means3D=means3D, colors=colors, opacity=opacity, scales=scales,
+            rotations=rotations, cov3D_precomp=cov3D_precomp, sh=sh, sg_axis=sg_axis, sg_sharpness=sg_sharpness,
+            sg_color=sg_color, viewmatrix=viewmatrix, projmatrix=projmatrix, campos=campos, alphas=alphas,
+            normalmap=normalmap, mdepth=mdepth, dL_dout_color=dL_dout_color, dL_dout_mdepth=dL_dout_mdepth,
+            dL_dout_alpha=dL_dout_alpha, dL_dout_normal=dL_dout_normal).items()}
+        radii = radii.contiguous()
+        scratch = _ByteBuffer(dev)
+        with torch.cuda.device(dev):
+            rc = L.gsr_rasterize_backward(
+                scratch.cb, None, P, int(sh_degree), SHM, int(sg_degree), SGM, int(R), _ptr(a["background"]), W, H,
+                _ptr(a["means3D"]), _ptr(a["colors"]), _ptr(a["opacity"]), _ptr(a["scales"]), _ptr(a["rotations"]),
+                _ptr(a["cov3D_precomp"]), _ptr(a["sh"]), _ptr(a["sg_axis"]), _ptr(a["sg_sharpness"]),
+                _ptr(a["sg_color"]), float(scale_modifier), _ptr(a["viewmatrix"]), _ptr(a["projmatrix"]),
+                _ptr(a["campos"]), float(tan_fovx), float(tan_fovy), float(kernel_size), _ptr(radii),
+                _ptr(a["alphas"]), _ptr(a["normalmap"]), _ptr(a["mdepth"]), _ptr(geomBuffer), _ptr(binningBuffer),
+                _ptr(imageBuffer), _ptr(tileBuffer), _ptr(a["dL_dout_color"]), _ptr(a["dL_dout_mdepth"]),
+                _ptr(a["dL_dout_alpha"]), _ptr(a["dL_dout_normal"]), _ptr(outs["dmeans3D"]), _ptr(outs["dmeans2D"]),
+                _ptr(outs["dcolors"]), _ptr(outs["dopacity"]), _ptr(outs["dscales"]), _ptr(outs["drotations"]),
+                _ptr(outs["dcov3D"]), _ptr(outs["dsh"]), _ptr(outs["dsg_axis"]), _ptr(outs["dsg_sharpness"]),
+                _ptr(outs["dsg_color"]), int(bool(require_depth)), int(bool(debug)), _stream(dev))
+        _check(rc)
+    return (outs["dmeans2D"], outs["dcolors"], outs["dopacity"], outs["dmeans3D"], outs["dcov3D"], outs["dsh"],
+            outs["dsg_axis"], outs["dsg_sharpness"], outs["dsg_color"], outs["dscales"], outs["drotations"])
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    L = _load()
+    P = means3D.size(0)
+    present = torch.zeros(P, dtype=torch.bool, device=means3D.device)
+    if P != 0:
+        m = _dev_contig(means3D, "means3D")
+        v = _dev_contig(viewmatrix, "viewmatrix")
+        p = _dev_contig(projmatrix, "projmatrix")
+        with torch.cuda.device(means3D.device):
+            _check(L.gsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(means3D.device)))
+    return present

@@ -1,0 +1,149 @@
+"""MI355X drop-in for the reference's `diff_gaussian_rasterization` package.
+
+Same public surface as DGR/diff_gaussian_rasterization/__init__.py:
+  rasterize_gaussians(...)                 (:23-50)
+  _RasterizeGaussians (autograd.Function)  (:53-251)
+  GaussianRasterizationSettings (15 fields, same order)  (:254-269)
+  GaussianRasterizer (nn.Module): forward, markVisible   (:272-336)
+so `from diff_gaussian_rasterization import GaussianRasterizationSettings,
+GaussianRasterizer` (gaussian_renderer/__init__.py:14) works unchanged once
+this directory's parent is on sys.path.  The compute lives in libgsr.so
+(hand-written HIP for gfx950) behind `_C`.
+
+The point-query entry points of the reference (integrate, evaluate_sdf,
+sample_depth, DGR/__init__.py:338-655) are the next rows of the build
+(SURVEY.md §8(f)); they raise NotImplementedError here.
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+import torch
+import torch.nn as nn
+
+from . import _C
+
+
+def cpu_deep_copy_tuple(input_tuple):
+    copied_tensors = [item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple]
+    return tuple(copied_tensors)
+
+
+def rasterize_gaussians(means3D, means2D, sh, sg_axis, sg_sharpness, sg_color, colors_precomp, opacities, scales,
+                        rotations, cov3Ds_precomp, raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, sg_axis, sg_sharpness, sg_color, colors_precomp,
+                                     opacities, scales, rotations, cov3Ds_precomp, raster_settings)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, sg_axis, sg_sharpness, sg_color, colors_precomp, opacities, scales,
+                rotations, cov3Ds_precomp, raster_settings):
+        s = raster_settings
+        args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis,
+                sg_sharpness, sg_color, s.sh_degree, s.sg_degree, s.scale_modifier, s.viewmatrix, s.projmatrix,
+                s.tanfovx, s.tanfovy, s.kernel_size, s.image_height, s.image_width, s.campos, s.prefiltered,
+                s.require_depth, s.debug)
+        if s.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                out = _C.rasterize_gaussians(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_fw.dump")
+                print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
+                raise ex
+        else:
+            out = _C.rasterize_gaussians(*args)
+        num_rendered, color, alpha, normal, mdepth, radii, geomBuffer, binningBuffer, imgBuffer, tileBuffer = out
+        ctx.raster_settings = raster_settings
+        ctx.num_rendered = num_rendered
+        ctx.save_for_backward(means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis,
+                              sg_sharpness, sg_color, alpha, normal, mdepth, radii, geomBuffer, binningBuffer,
+                              imgBuffer, tileBuffer)
+        return color, radii, mdepth, alpha, normal
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_radii, grad_mdepth, grad_alpha, grad_normal):
+        num_rendered = ctx.num_rendered
+        s = ctx.raster_settings
+        (means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis, sg_sharpness, sg_color,
+         alpha, normal, mdepth, radii, geomBuffer, binningBuffer, imgBuffer, tileBuffer) = ctx.saved_tensors
+        args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis,
+                sg_sharpness, sg_color, s.sh_degree, s.sg_degree, s.scale_modifier, s.viewmatrix, s.projmatrix,
+                s.tanfovx, s.tanfovy, s.kernel_size, grad_color, grad_mdepth, grad_alpha, grad_normal, alpha, normal,
+                mdepth, s.campos, radii, geomBuffer, num_rendered, binningBuffer, imgBuffer, tileBuffer,
+                s.require_depth, s.debug)
+        if s.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                g = _C.rasterize_gaussians_backward(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_bw.dump")
+                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
+                raise ex
+        else:
+            g = _C.rasterize_gaussians_backward(*args)
+        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
+         grad_sg_axis, grad_sg_sharpness, grad_sg_color, grad_scales, grad_rotations) = g
+        return (grad_means3D, grad_means2D, grad_sh, grad_sg_axis, grad_sg_sharpness, grad_sg_color,
+                grad_colors_precomp, grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None)
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    kernel_size: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    sg_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    require_depth: bool
+    debug: bool
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        with torch.no_grad():
+            s = self.raster_settings
+            visible = _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
+        return visible
+
+    def forward(self, means3D, means2D, opacities, shs=None, sg_axis=None, sg_sharpness=None, sg_color=None,
+                colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None):
+        raster_settings = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception("Please provide excatly one of either SHs or precomputed colors!")
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or (
+                (scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        if shs is None:
+            shs = torch.Tensor([])
+        if colors_precomp is None:
+            colors_precomp = torch.Tensor([])
+        if scales is None:
+            scales = torch.Tensor([])
+        if rotations is None:
+            rotations = torch.Tensor([])
+        if cov3D_precomp is None:
+            cov3D_precomp = torch.Tensor([])
+        return rasterize_gaussians(means3D, means2D, shs, sg_axis, sg_sharpness, sg_color, colors_precomp,
+                                   opacities, scales, rotations, cov3D_precomp, raster_settings)
+
+    def integrate(self, *args, **kwargs):
+        raise NotImplementedError("integrate (DGR/__init__.py:338-380) is a next-round row (SURVEY.md §8(f))")
+
+    def evaluate_sdf(self, *args, **kwargs):
+        raise NotImplementedError("evaluate_sdf (DGR/__init__.py:382-440) is a next-round row (SURVEY.md §8(f))")
+
+    def sample_depth(self, *args, **kwargs):
+        raise NotImplementedError("sample_depth (DGR/__init__.py:442-483) is a next-round row (SURVEY.md §8(f))")

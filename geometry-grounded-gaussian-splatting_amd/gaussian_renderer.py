@@ -1,0 +1,49 @@
+"""render() — the caller of the rasterizer, mirroring the reference's
+gaussian_renderer/__init__.py:18-98 (argument meaning, settings construction,
+returned dict).  Differences: the screen-space dummy tensor is created on the
+Gaussians' device instead of a hard-coded "cuda", and `pipe` may be any object
+with a `debug` attribute.  integrate / evaluate_sdf / sample_depth (:101-278)
+are next-round rows.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+
+
+def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, kernel_size, scaling_modifier=1.0,
+           require_depth: bool = True):
+    """Render the scene.  `pc` exposes the GaussianModel getters
+    (get_xyz, get_scaling_n_opacity_with_3D_filter, get_rotation, get_features,
+    get_sg_axis, get_sg_sharpness, get_sg_color, active_sh_degree,
+    active_sg_degree) as properties or zero-argument methods."""
+
+    def _get(name):
+        v = getattr(pc, name)
+        return v() if callable(v) else v
+
+    xyz = _get("get_xyz")
+    tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
+    tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device) + 0
+    try:
+        screenspace_points.retain_grad()
+    except Exception:  # noqa: BLE001 - same tolerance as the reference
+        pass
+    raster_settings = GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+        tanfovx=tanfovx, tanfovy=tanfovy, kernel_size=kernel_size, bg=bg_color, scale_modifier=scaling_modifier,
+        viewmatrix=viewpoint_camera.world_view_transform, projmatrix=viewpoint_camera.full_proj_transform,
+        sh_degree=pc.active_sh_degree, sg_degree=pc.active_sg_degree, campos=viewpoint_camera.camera_center,
+        prefiltered=False, require_depth=require_depth, debug=getattr(pipe, "debug", False))
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    scales, opacity = _get("get_scaling_n_opacity_with_3D_filter")
+    image, radii, median_depth, alpha, normal = rasterizer(
+        means3D=xyz, means2D=screenspace_points, shs=_get("get_features"), sg_axis=_get("get_sg_axis"),
+        sg_sharpness=_get("get_sg_sharpness"), sg_color=_get("get_sg_color"), colors_precomp=None,
+        opacities=opacity, scales=scales, rotations=_get("get_rotation"), cov3D_precomp=None)
+    return {"render": image, "mask": alpha, "median_depth": median_depth, "viewspace_points": screenspace_points,
+            "visibility_filter": radii > 0, "radii": radii, "normal": normal}
