@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Benchmark: differentiable Gaussian-splatting raster, forward + backward.
+
+BASELINE.json metric: "train iters/sec (fwd+bwd raster) at 1080p, 1M Gaussians;
+HBM GB/s vs peak".  One step = one GaussianRasterizer forward + autograd
+backward (the reference's render() call pattern) over one 1920x1080
+view of 1M synthetic Gaussians (SH degree 3, require_depth=True, the state
+after iteration 7000).  Inputs are activated tensors already resident in HBM;
+losses, optimiser and the Python getters are outside the step.
+
+  python bench.py [--gpus N --steps K --warmup W]
+
+With N > 1 (launched by torch.distributed.run, one rank per GPU) every rank
+renders its own view (C4: cameras orbiting the scene) of the same Gaussians
+and the per-Gaussian gradients are summed with one RCCL all_reduce per step
+(the only exchange of view-parallel training).  `value` = views/s over all
+ranks, time = max over ranks.
+
+Rank 0 prints one JSON line: the contract fields, a `roofline` object for the
+dominant kernel (algorithmic bytes per launch / its HIP-event-timed average
+duration, vs 8 TB/s HBM peak; `traffic` from the committed rocprofv3 PMC
+summary when present) and a `cpu_baseline` object (the C oracle on the host
+cores, bounded sample, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd")
+sys.path.insert(0, PKG)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--sh-degree", type=int, default=3)
+    ap.add_argument("--sg-degree", type=int, default=0)
+    ap.add_argument("--no-depth", action="store_true", help="require_depth=False (iterations < 7000)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-tile-stride", type=int, default=0, help="0 = auto")
+    return ap.parse_args()
+
+
+def stage_bytes(P, K, HW, shm, sgm, geom):
+    """Algorithmic (compulsory) HBM bytes per launch of each stage, from the
+    per-unit figures of SURVEY.md §8(d)."""
+    Bp = 44 + 12 * shm + 28 * sgm
+    G = 64 if geom else 36
+    Opx = 36 if geom else 20
+    Ipx = 56 if geom else 24
+    A = 68 if geom else 40
+    return {
+        "preprocess": P * (Bp + 80),
+        "scan": P * 8,
+        "emit_keys": P * 20 + K * 12,
+        "sort": K * 24,
+        "tile_ranges": K * 8,
+        "render_fwd": K * (4 + G) + HW * Opx,
+        "bwd_clear": P * A,
+        "render_bwd": HW * Ipx + K * (4 + G),
+        "preprocess_bwd": P * (A + Bp + 8 + Bp),
+    }
+
+
+def load_pmc_traffic(kernel_stage):
+    """HBM bytes per launch of `kernel_stage` from profiles/pmc_summary.json
+    (written by tools/profile.sh from separate rocprofv3 --pmc passes, with
+    the gfx950 FETCH_SIZE x2 correction already applied)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["stages"][kernel_stage]["hbm_bytes_per_launch"]
+    except Exception:  # noqa: BLE001 - absent or stale summary -> null
+        return None
+
+
+def cpu_baseline(args, inputs_cpu, cam, tanx, tany, grads_cpu):
+    """Time the C oracle (tests' checker) on this host: full per-Gaussian work
+    and binning, every s-th tile rendered forward and backward, tile time
+    extrapolated x s."""
+    sys.path.insert(0, ROOT)
+    from oracle import gsr_oracle as O
+
+    cores = min(16, os.cpu_count() or 1)
+    O.set_threads(cores)
+    tiles = ((args.width + 15) // 16) * ((args.height + 15) // 16)
+    stride = args.cpu_tile_stride or 1  # default: the whole iteration, no extrapolation
+    O.set_tile_stride(stride)
+    geom = not args.no_depth
+    a = (torch.zeros(3), inputs_cpu["means3D"], None, inputs_cpu["opacities"], inputs_cpu["scales"],
+         inputs_cpu["rotations"], None, inputs_cpu["shs"], inputs_cpu["sg_axis"], inputs_cpu["sg_sharpness"],
+         inputs_cpu["sg_color"], args.sh_degree, args.sg_degree, 1.0, cam.world_view_transform,
+         cam.full_proj_transform, tanx, tany, 0.0)
+    t0 = time.time()
+    o = O.forward(*a, args.height, args.width, cam.camera_center, False, geom)
+    tf = O.last_times()
+    O.backward(o["state"], *a, grads_cpu["color"], grads_cpu["mdepth"], grads_cpu["alpha"], grads_cpu["normal"],
+               o["alpha"], o["normal"], o["mdepth"], cam.camera_center, o["radii"])
+    tb = O.last_times()
+    wall = time.time() - t0
+    O.set_tile_stride(1)
+    per_iter = tf["preprocess_binning"] + stride * tf["render"] + stride * tb["render_bwd"] + tb["preprocess_bwd"]
+    return {"value": round(1.0 / per_iter, 6), "unit": "iters/s", "cores": cores, "kind": "port",
+            "sample": (f"C oracle (oracle/gsr_oracle.c), full C3 scene: per-Gaussian preprocess, binning/sort and "
+                       f"per-Gaussian backward measured in full; forward+backward tile rendering on every "
+                       f"{stride}th of {tiles} tiles, extrapolated x{stride}; {wall:.1f} s wall; "
+                       f"split s: {tf['preprocess_binning']:.2f} pre+bin, {tf['render'] * stride:.2f} render, "
+                       f"{tb['render_bwd'] * stride:.2f} render_bwd, {tb['preprocess_bwd']:.2f} pre_bwd")}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    import gsr_scene as S
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from diff_gaussian_rasterization import _C
+
+    W, H, P = args.width, args.height, args.P
+    geom = not args.no_depth
+    if world > 1:
+        cam_cpu = S.orbit_cameras(8, W, H)[rank % 8]
+        workload = f"C4: {P} Gaussians, one {W}x{H} view per GPU (orbit), fwd+bwd + RCCL grad all_reduce"
+    else:
+        cam_cpu = S.make_camera(W, H)
+        workload = f"C3: {P} Gaussians, {W}x{H}, fwd+bwd"
+    raw = S.make_gaussians(P, sh_degree=args.sh_degree, sg_degree=args.sg_degree, aspect=H / W)
+    inputs_cpu = {k: v.detach().contiguous() for k, v in S.activated_inputs(raw).items()}
+    grads_cpu = S.upstream_grads(H, W)
+    cam = cam_cpu.to(dev)
+    tanx, tany = math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5)
+    params = {k: v.to(dev).requires_grad_(True) for k, v in inputs_cpu.items()}
+    means2D = torch.zeros(P, 3, device=dev, requires_grad=True)
+    g_color = grads_cpu["color"].to(dev)
+    g_mdepth = grads_cpu["mdepth"].to(dev)
+    g_normal = grads_cpu["normal"].to(dev)
+    settings = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=tanx, tanfovy=tany, kernel_size=0.0, bg=torch.zeros(3, device=dev),
+        scale_modifier=1.0, viewmatrix=cam.world_view_transform, projmatrix=cam.full_proj_transform,
+        sh_degree=args.sh_degree, sg_degree=args.sg_degree, campos=cam.camera_center, prefiltered=False,
+        require_depth=geom, debug=False)
+    rasterizer = GaussianRasterizer(settings)
+    grad_keys = ["means3D", "shs", "sg_axis", "sg_sharpness", "sg_color", "opacities", "scales", "rotations"]
+    reducer = None
+    if world > 1:
+        from gsr_dist import ViewParallelGrads
+        reducer = ViewParallelGrads([params[k] for k in grad_keys])
+    state = {}
+
+    def step():
+        for t in list(params.values()) + [means2D]:
+            t.grad = None
+        color, radii, mdepth, alpha, normal = rasterizer(
+            means3D=params["means3D"], means2D=means2D, opacities=params["opacities"], shs=params["shs"],
+            sg_axis=params["sg_axis"], sg_sharpness=params["sg_sharpness"], sg_color=params["sg_color"],
+            scales=params["scales"], rotations=params["rotations"])
+        outs, gs = [color], [g_color]
+        if geom:
+            outs += [mdepth, normal]
+            gs += [g_mdepth, g_normal]
+        torch.autograd.backward(outs, gs)
+        if reducer is not None:  # view-parallel gradient exchange
+            reducer.all_reduce()
+        state["radii"] = radii
+
+    log(f"[bench] rank {rank}/{world} device {torch.cuda.get_device_name(dev)} P={P} {W}x{H} geom={geom}")
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    _C.timing_collect()  # discard
+    _C.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _C.timing_enable(False)
+    stages = _C.timing_collect()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # K of this view (one extra forward, outside the timed region)
+    with torch.no_grad():
+        K = _C.rasterize_gaussians(settings.bg, params["means3D"], torch.Tensor([]), params["opacities"],
+                                   params["scales"], params["rotations"], torch.Tensor([]), params["shs"],
+                                   params["sg_axis"], params["sg_sharpness"], params["sg_color"], args.sh_degree,
+                                   args.sg_degree, 1.0, cam.world_view_transform, cam.full_proj_transform, tanx,
+                                   tany, 0.0, H, W, cam.camera_center, False, geom, False)[0]
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * args.steps / elapsed
+    shm = (args.sh_degree + 1) ** 2
+    algo = stage_bytes(P, K, W * H, shm, args.sg_degree, geom)
+    per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in stages.items()}
+    dom = max(per_launch, key=lambda k: per_launch[k])
+    achieved = algo[dom] / (per_launch[dom] * 1e-3) / 1e9
+    traffic = load_pmc_traffic(dom)
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                "traffic": traffic, "algorithmic_bytes_per_launch": int(algo[dom]),
+                "avg_launch_ms": round(per_launch[dom], 4),
+                "stage_ms": {k: round(v, 4) for k, v in per_launch.items()}}
+    total_algo = sum(algo.values())
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args, inputs_cpu, cam_cpu, tanx, tany, grads_cpu)
+        except Exception as e:  # noqa: BLE001 - report, never hide
+            cpu = {"value": None, "error": repr(e)}
+    if rank == 0:
+        line = {
+            "metric": "train iters/sec (fwd+bwd raster) at 1080p, 1M Gaussians; HBM GB/s vs peak",
+            "value": round(value, 3), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": workload, "P": P, "width": W, "height": H, "sh_degree": args.sh_degree,
+                       "sg_degree": args.sg_degree, "require_depth": geom, "num_rendered": int(K),
+                       "parallelism": f"view-parallel dp{world}" if world > 1 else "single",
+                       "step_algorithmic_GBps": round(total_algo / (ms_per_step * 1e-3) / 1e9, 2)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -9,7 +9,9 @@
 // allocation (all scratch comes from the caller's allocation callbacks).
 #include <stdio.h>
 
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/gsr.h"
 #include "gsr_kernels.h"
@@ -148,6 +150,47 @@ const char* check_params(const FwdParams& p) {
     return nullptr;
 }
 
+// ---- per-stage timing (gsr_timing_*) -------------------------------------
+struct TimingRec {
+    int stage;
+    hipEvent_t e0, e1;
+};
+std::mutex g_tmu;
+bool g_timing = false;
+std::vector<TimingRec> g_recs;
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t pool_event() {
+    if (!g_pool.empty()) {
+        hipEvent_t e = g_pool.back();
+        g_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+struct StageTimer {
+    hipStream_t stream;
+    int stage;
+    hipEvent_t e0 = nullptr;
+    StageTimer(int st, hipStream_t s) : stream(s), stage(st) {
+        std::lock_guard<std::mutex> lk(g_tmu);
+        if (!g_timing) return;
+        e0 = pool_event();
+        if (e0) (void)hipEventRecord(e0, stream);
+    }
+    ~StageTimer() {
+        if (!e0) return;
+        std::lock_guard<std::mutex> lk(g_tmu);
+        hipEvent_t e1 = pool_event();
+        if (!e1) return;
+        (void)hipEventRecord(e1, stream);
+        g_recs.push_back({stage, e0, e1});
+    }
+};
+
 #define GSR_TRY(expr, what)                                   \
     do {                                                      \
         hipError_t _e = (expr);                               \
@@ -158,11 +201,52 @@ const char* check_params(const FwdParams& p) {
         }                                                     \
     } while (0)
 
+#define GSR_STAGE(stage, expr, what)                          \
+    do {                                                      \
+        StageTimer _t(stage, stream);                         \
+        GSR_TRY(expr, what);                                  \
+    } while (0)
+
 }  // namespace
 
 extern "C" {
 
-int gsr_abi_version(void) { return 1; }
+int gsr_abi_version(void) { return 2; }
+
+int gsr_timing_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_timing = on != 0;
+    return GSR_OK;
+}
+
+int gsr_timing_collect(double* ms, int* launches) {
+    std::vector<TimingRec> recs;
+    {
+        std::lock_guard<std::mutex> lk(g_tmu);
+        recs.swap(g_recs);
+    }
+    int rc = GSR_OK;
+    for (const TimingRec& r : recs) {
+        float t = 0.f;
+        hipError_t e = hipEventSynchronize(r.e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(&t, r.e0, r.e1);
+        if (e != hipSuccess) rc = fail(GSR_ERR_HIP, "timing", e);
+        if (ms) ms[r.stage] += t;
+        if (launches) launches[r.stage] += 1;
+    }
+    std::lock_guard<std::mutex> lk(g_tmu);
+    for (const TimingRec& r : recs) {
+        g_pool.push_back(r.e0);
+        g_pool.push_back(r.e1);
+    }
+    return rc;
+}
+
+const char* gsr_stage_name(int stage) {
+    static const char* names[GSR_NUM_STAGES] = {"preprocess", "scan", "emit_keys", "sort", "tile_ranges",
+                                                 "render_fwd", "bwd_clear", "render_bwd", "preprocess_bwd"};
+    return (stage >= 0 && stage < GSR_NUM_STAGES) ? names[stage] : "?";
+}
 
 const char* gsr_last_error(void) { return g_last_error.c_str(); }
 
@@ -215,8 +299,8 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
         return GSR_OK;
     }
 
-    GSR_TRY(launch_preprocess_fwd(p, gs, radii, stream), "preprocess");
-    GSR_TRY(launch_scan(gs, P, stream), "scan");
+    GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, radii, stream), "preprocess");
+    GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
     uint32_t K = 0;
     GSR_TRY(hipMemcpyAsync(&K, gs.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
     {
@@ -228,10 +312,11 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, end_bit, bs));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
     carve_binning(aligned_base(bbuf), (int)K, end_bit, bs);
-    GSR_TRY(launch_emit_keys(p, gs, radii, bs, stream), "emit keys");
-    GSR_TRY(launch_sort(bs, (int)K, end_bit, stream), "sort");
-    GSR_TRY(launch_tile_ranges(bs, (int)K, ts, tiles, stream), "tile ranges");
-    GSR_TRY(launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
+    GSR_STAGE(GSR_STAGE_EMIT_KEYS, launch_emit_keys(p, gs, radii, bs, stream), "emit keys");
+    GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K, end_bit, stream), "sort");
+    GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K, ts, tiles, stream), "tile ranges");
+    GSR_STAGE(GSR_STAGE_RENDER_FWD,
+              launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
     if (num_rendered) *num_rendered = (int)K;
     return GSR_OK;
 }
@@ -305,9 +390,9 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
     if (!wbuf) return fail(GSR_ERR_ALLOC, "backward buffer allocation failed");
     void* wb = aligned_base(wbuf);
     carve_bwd(wb, P, ws);
-    GSR_TRY(hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
-    GSR_TRY(launch_render_bwd(b, gs, bs, is, ts, ws, stream), "render backward");
-    GSR_TRY(launch_preprocess_bwd(b, gs, ws, stream), "preprocess backward");
+    GSR_STAGE(GSR_STAGE_BWD_CLEAR, hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
+    GSR_STAGE(GSR_STAGE_RENDER_BWD, launch_render_bwd(b, gs, bs, is, ts, ws, stream), "render backward");
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_bwd(b, gs, ws, stream), "preprocess backward");
     return GSR_OK;
 }
 

@@ -10,6 +10,12 @@
 // depth (= |p_view|, the sort key, render_forward.cu:380), clamped bits, and
 // the Splat record (only for Gaussians with radius > 0; the others are never
 // gathered).
+// Bit-exact integer outputs (radii, tiles_touched, K, sort keys) need the
+// same fp32 operation sequence as the oracle: no FMA contraction in this
+// translation unit (set before the includes so the inlined helpers of
+// gsr_math.h are covered too).
+#pragma clang fp contract(off)
+
 #include "gsr_kernels.h"
 #include "gsr_math.h"
 
@@ -66,24 +72,40 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
     float cinv[9];  // cov_cam_inv (row-major, symmetric)
     float cov00, cov01, cov11;
     bool well_conditioned = true;
+    // T = W J in the reference's glm product order: Tc[j][i] is column j,
+    // row i.  Only columns 0 and 1 are non-zero (J's third column is 0).
+    // Evaluated with contraction off (file-level pragma) so the 2D covariance,
+    // and with it det == 0, the radius and the tile rect, are bit-identical to
+    // the oracle's glm-order restatement: radii / tiles_touched / K / the
+    // sorted instance list are integer outputs and must match exactly.
+    const float j00 = fx / tz, j02 = -(fx * g.tx) / (tz * tz);
+    const float j11 = fy / tz, j12 = -(fy * g.ty) / (tz * tz);
+    float Tc0[3], Tc1[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        // W column c = (V[c], V[4+c], V[8+c]) -> W.c[c][i] = V[4*i + c]
+        Tc0[i] = V[4 * i] * j00 + V[4 * i + 2] * j02;
+        Tc1[i] = V[4 * i + 1] * j11 + V[4 * i + 2] * j12;
+    }
     if (a.scales) {
         const float* q = a.rotations + 4 * idx;
         rot_view(V, q[0], q[1], q[2], q[3], A, Rq);
         s[0] = a.scale_modifier * a.scales[3 * idx];
         s[1] = a.scale_modifier * a.scales[3 * idx + 1];
         s[2] = a.scale_modifier * a.scales[3 * idx + 2];
-        // B = J A S (2x3): J rows (fx/tz, 0, -fx tx/tz^2), (0, fy/tz, -fy ty/tz^2)
-        const float j00 = fx * itz, j02 = -(fx * g.tx) / (tz * tz);
-        const float j11 = fy * itz, j12 = -(fy * g.ty) / (tz * tz);
-        float B0[3], B1[3];
+        // glm R column j = row j of R_q: R.c[j][i] = Rq[3*j + i]; (S R).c[j][i] = s_i * R.c[j][i]
+        // M = (S R) T: M.c[j][i] = SR.c[0][i] T.c[j][0] + SR.c[1][i] T.c[j][1] + SR.c[2][i] T.c[j][2]
+        float M0[3], M1[3];
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            B0[k] = (j00 * A[k] + j02 * A[6 + k]) * s[k];
-            B1[k] = (j11 * A[3 + k] + j12 * A[6 + k]) * s[k];
+        for (int i = 0; i < 3; i++) {
+            const float sr0 = s[i] * Rq[i], sr1 = s[i] * Rq[3 + i], sr2 = s[i] * Rq[6 + i];
+            M0[i] = sr0 * Tc0[0] + sr1 * Tc0[1] + sr2 * Tc0[2];
+            M1[i] = sr0 * Tc1[0] + sr1 * Tc1[1] + sr2 * Tc1[2];
         }
-        cov00 = B0[0] * B0[0] + B0[1] * B0[1] + B0[2] * B0[2];
-        cov01 = B0[0] * B1[0] + B0[1] * B1[1] + B0[2] * B1[2];
-        cov11 = B1[0] * B1[0] + B1[1] * B1[1] + B1[2] * B1[2];
+        // cov = M^T M: cov.c[j][i] = sum_k M.c[i][k] M.c[j][k]
+        cov00 = M0[0] * M0[0] + M0[1] * M0[1] + M0[2] * M0[2];
+        cov01 = M1[0] * M0[0] + M1[1] * M0[1] + M1[2] * M0[2];
+        cov11 = M1[0] * M1[0] + M1[1] * M1[1] + M1[2] * M1[2];
         const float is2[3] = {1.0f / (s[0] * s[0]), 1.0f / (s[1] * s[1]), 1.0f / (s[2] * s[2])};
 #pragma unroll
         for (int i = 0; i < 3; i++)
@@ -99,29 +121,23 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
         const float Vk[9] = {c[0], c[1], c[2], c[1], c[3], c[4], c[2], c[4], c[5]};
         float Vinv[9];
         well_conditioned = sym3_inverse_or_null_projector(Vk, Vinv);
-        // cov2D = J W_r Vrk W_r^T J^T ; cov_cam_inv = W_r Vinv W_r^T
+        // cov2D = (T^T Vrk^T) T in glm order (render_forward.cu:168); cov_cam_inv = W_r Vinv W_r^T
         float Wr[9];
 #pragma unroll
         for (int i = 0; i < 3; i++)
 #pragma unroll
             for (int j = 0; j < 3; j++) Wr[3 * i + j] = V[4 * j + i];
-        const float j00 = fx * itz, j02 = -(fx * g.tx) / (tz * tz);
-        const float j11 = fy * itz, j12 = -(fy * g.ty) / (tz * tz);
-        float T0[3], T1[3];  // rows of J W_r
+        const float Tc[3][3] = {{Tc0[0], Tc0[1], Tc0[2]}, {Tc1[0], Tc1[1], Tc1[2]}, {0.f, 0.f, 0.f}};
+        // Vrk.c[k] = column k (symmetric); C.c[k][i] = sum_m T.c[i][m] Vrk.c[k][m]
+        float C[3][2];
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            T0[k] = j00 * Wr[k] + j02 * Wr[6 + k];
-            T1[k] = j11 * Wr[3 + k] + j12 * Wr[6 + k];
-        }
-        float VT0[3], VT1[3];
+        for (int kk = 0; kk < 3; kk++)
 #pragma unroll
-        for (int i = 0; i < 3; i++) {
-            VT0[i] = Vk[3 * i] * T0[0] + Vk[3 * i + 1] * T0[1] + Vk[3 * i + 2] * T0[2];
-            VT1[i] = Vk[3 * i] * T1[0] + Vk[3 * i + 1] * T1[1] + Vk[3 * i + 2] * T1[2];
-        }
-        cov00 = T0[0] * VT0[0] + T0[1] * VT0[1] + T0[2] * VT0[2];
-        cov01 = T0[0] * VT1[0] + T0[1] * VT1[1] + T0[2] * VT1[2];
-        cov11 = T1[0] * VT1[0] + T1[1] * VT1[1] + T1[2] * VT1[2];
+            for (int i = 0; i < 2; i++)
+                C[kk][i] = Tc[i][0] * Vk[3 * kk] + Tc[i][1] * Vk[3 * kk + 1] + Tc[i][2] * Vk[3 * kk + 2];
+        cov00 = C[0][0] * Tc[0][0] + C[1][0] * Tc[0][1] + C[2][0] * Tc[0][2];
+        cov01 = C[0][1] * Tc[0][0] + C[1][1] * Tc[0][1] + C[2][1] * Tc[0][2];
+        cov11 = C[0][1] * Tc[1][0] + C[1][1] * Tc[1][1] + C[2][1] * Tc[1][2];
         float WV[9];
 #pragma unroll
         for (int i = 0; i < 3; i++)

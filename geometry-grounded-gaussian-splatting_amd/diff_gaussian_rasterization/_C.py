@@ -48,6 +48,10 @@ def _load():
                                          + [f] * 3 + [vp] * 4 + [vp] * 4 + [vp] * 4 + [vp] * 11 + [i, i, vp])
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
+    L.gsr_timing_enable.argtypes = [i]
+    L.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i)]
+    L.gsr_stage_name.restype = ctypes.c_char_p
+    L.gsr_stage_name.argtypes = [i]
     L.gsr_last_error.restype = ctypes.c_char_p
     L.gsr_abi_version.restype = i
     _lib = L
@@ -57,6 +61,23 @@ def _load():
 def loaded_library_path() -> str:
     _load()
     return LIB_PATH
+
+
+NUM_STAGES = 9
+
+
+def timing_enable(on: bool = True) -> None:
+    """Bracket every kernel stage with hipEvents on its stream (gsr_timing_enable)."""
+    _load().gsr_timing_enable(int(bool(on)))
+
+
+def timing_collect() -> dict:
+    """{stage name: (total ms, launches)} since the last collect (gsr_timing_collect)."""
+    L = _load()
+    ms = (ctypes.c_double * NUM_STAGES)()
+    n = (ctypes.c_int * NUM_STAGES)()
+    _check(L.gsr_timing_collect(ms, n))
+    return {L.gsr_stage_name(k).decode(): (ms[k], n[k]) for k in range(NUM_STAGES)}
 
 
 class _ByteBuffer:

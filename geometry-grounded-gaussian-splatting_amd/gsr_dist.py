@@ -1,0 +1,104 @@
+"""View-parallel training step: one process per GPU, RCCL over xGMI.
+
+The reference trains on one GPU, one view per iteration (utils/general_utils.py:135,
+train.py:142-192).  The MI355X build shards *views* across ranks (SURVEY §5,
+§8(e)): every rank holds a full replica of the Gaussians, rasterises its own
+view forward + backward with no communication, and the per-Gaussian gradients
+are summed with all_reduce(SUM) — the only exchange step.  The step gradient is
+then the sum over the ranks' views, i.e. the gradient of sum_v L_v.
+
+Gradients are packed into a few large flat fp32 buckets (bucket_mb, default
+256 MB: at 1M Gaussians / SH3 the whole 236 MB gradient is one bucket, so one
+ring all-reduce per step; xGMI links are point-to-point, so few large
+collectives keep every link busy).  With `async_op=True` buckets are posted as
+they fill so a caller can overlap them with other work; `finish()` waits and
+scatters the sums back into the .grad tensors.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class ViewParallelGrads:
+    def __init__(self, params: Iterable[torch.Tensor], bucket_mb: float = 256.0,
+                 group: Optional[dist.ProcessGroup] = None, average: bool = False):
+        self.params: List[torch.Tensor] = [p for p in params if p.requires_grad]
+        self.group = group
+        self.average = average
+        cap = max(1, int(bucket_mb * 1024 * 1024 // 4))
+        self.buckets: List[List[torch.Tensor]] = []
+        cur, n = [], 0
+        for p in self.params:
+            if cur and n + p.numel() > cap:
+                self.buckets.append(cur)
+                cur, n = [], 0
+            cur.append(p)
+            n += p.numel()
+        if cur:
+            self.buckets.append(cur)
+        self._flat: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
+        self._work = []
+
+    def _pack(self, i: int) -> torch.Tensor:
+        ps = self.buckets[i]
+        n = sum(p.numel() for p in ps)
+        dev = ps[0].device
+        if self._flat[i] is None or self._flat[i].numel() != n or self._flat[i].device != dev:
+            self._flat[i] = torch.empty(n, dtype=torch.float32, device=dev)
+        flat = self._flat[i]
+        off = 0
+        for p in ps:
+            k = p.numel()
+            if p.grad is None:
+                flat[off:off + k].zero_()
+            else:
+                flat[off:off + k].copy_(p.grad.reshape(-1))
+            off += k
+        return flat
+
+    def all_reduce(self, async_op: bool = False):
+        """Sum every parameter's .grad over the ranks of the group."""
+        self._work = []
+        for i in range(len(self.buckets)):
+            flat = self._pack(i)
+            w = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            self._work.append((i, w))
+        if not async_op:
+            self.finish()
+
+    def finish(self):
+        ws = dist.get_world_size(self.group) if self.average else 1
+        for i, w in self._work:
+            if w is not None:
+                w.wait()
+            flat = self._flat[i]
+            if self.average:
+                flat.div_(ws)
+            off = 0
+            for p in self.buckets[i]:
+                k = p.numel()
+                src = flat[off:off + k].view_as(p)
+                if p.grad is None:
+                    p.grad = src.clone()
+                else:
+                    p.grad.copy_(src)
+                off += k
+        self._work = []
+
+    @property
+    def bucket_bytes(self) -> List[int]:
+        return [4 * sum(p.numel() for p in b) for b in self.buckets]
+
+
+def reduce_densification_stats(grad_norm_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
+                               group: Optional[dist.ProcessGroup] = None) -> None:
+    """Densification statistics of the views seen since the last densify step
+    (gaussian_model.py:818-821, train.py:236): sums for the accumulated
+    screen-space gradient norms and visibility counts, max for the radii.
+    Called only at densification steps (every 100 iterations), not per step."""
+    dist.all_reduce(grad_norm_accum, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(denom, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX, group=group)

@@ -152,6 +152,31 @@ class RawGaussians:
         return self.sg_color
 
 
+@torch.no_grad()
+def compute_filter_3D(xyz: torch.Tensor, cameras) -> torch.Tensor:
+    """Mip-Splatting 3D filter, restating gaussian_model.py:225-262: per
+    Gaussian the smallest depth over the training cameras that see it (in front
+    of z = 0.2 and within 1.15x the half field of view), over the largest focal
+    length, times sqrt(0.2).  `cameras` expose R [3,3] (stored transposed, as
+    the reference keeps it), T [3], image_width, image_height, Fx, Fy."""
+    distance = torch.full((xyz.shape[0],), float("inf"), device=xyz.device)
+    valid_points = torch.zeros(xyz.shape[0], device=xyz.device, dtype=torch.bool)
+    focal_length = 0.0
+    for cam in cameras:
+        xyz_cam = torch.addmm(cam.T[None, :].to(xyz), xyz, cam.R.to(xyz))
+        z = xyz_cam[:, 2]
+        valid_depth = z > 0.2
+        uv_abs = torch.abs(xyz_cam[:, :2] / z.unsqueeze(-1))
+        bx = cam.image_width / cam.Fx * 0.575
+        by = cam.image_height / cam.Fy * 0.575
+        valid = valid_depth & (uv_abs[:, 0] <= bx) & (uv_abs[:, 1] <= by)
+        distance = torch.where(valid, torch.minimum(distance, z), distance)
+        valid_points = valid_points | valid
+        focal_length = max(focal_length, cam.Fx)
+    distance[~valid_points] = distance[valid_points].max()
+    return (distance / focal_length * (0.2 ** 0.5))[..., None]
+
+
 def make_gaussians(P: int, sh_degree: int = 3, sg_degree: int = 0, seed: int = 0, fovx_deg: float = 60.0,
                    aspect: float = 1080 / 1920, z_range=(2.0, 10.0), log_scale_mean: float = math.log(0.02),
                    log_scale_std: float = 0.5, opacity_std: float = 1.5) -> RawGaussians:

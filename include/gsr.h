@@ -99,6 +99,30 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream);
 
+/*
+ * Per-stage GPU timing (no reference equivalent; SURVEY §5 "tracing").  While
+ * enabled, every kernel stage of the calls above is bracketed by two hipEvents
+ * on the call's stream.  gsr_timing_collect() waits for the recorded events,
+ * adds each stage's total milliseconds and launch count into the caller's
+ * arrays (length GSR_NUM_STAGES, indexed by enum gsr_stage) and clears the
+ * record.  Process-wide, thread-safe.
+ */
+enum gsr_stage {
+    GSR_STAGE_PREPROCESS = 0,
+    GSR_STAGE_SCAN,
+    GSR_STAGE_EMIT_KEYS,
+    GSR_STAGE_SORT,
+    GSR_STAGE_TILE_RANGES,
+    GSR_STAGE_RENDER_FWD,
+    GSR_STAGE_BWD_CLEAR,
+    GSR_STAGE_RENDER_BWD,
+    GSR_STAGE_PREPROCESS_BWD,
+    GSR_NUM_STAGES
+};
+int gsr_timing_enable(int on);
+int gsr_timing_collect(double* ms, int* launches);
+const char* gsr_stage_name(int stage);
+
 /* Human-readable message for the last non-OK status on this thread. */
 const char* gsr_last_error(void);
 

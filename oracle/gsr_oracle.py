@@ -54,6 +54,9 @@ def lib():
             + [_f] * 7 + [_f] * 11)
         L.gsro_free.argtypes = [ctypes.c_void_p]
         L.gsro_set_threads.argtypes = [ctypes.c_int]
+        L.gsro_set_tile_stride.argtypes = [ctypes.c_int]
+        L.gsro_last_times.argtypes = [_d]
+        L.gsro_eval_color.argtypes = [ctypes.c_int] * 4 + [_f] * 6 + [_f, _u8]
         L.gsro_max_threads.restype = ctypes.c_int
         L.gsro_higher_msb.argtypes = [ctypes.c_uint32]
         L.gsro_higher_msb.restype = ctypes.c_uint32
@@ -71,6 +74,19 @@ def lib():
 
 def set_threads(n: int) -> None:
     lib().gsro_set_threads(int(n))
+
+
+def set_tile_stride(n: int) -> None:
+    """Bounded-sample mode: render/backpropagate only every n-th tile."""
+    lib().gsro_set_tile_stride(int(n))
+
+
+def last_times() -> dict:
+    """Seconds spent in the last forward/backward: per-Gaussian + binning,
+    tile render, backward tile render, per-Gaussian backward."""
+    t = np.zeros(4)
+    lib().gsro_last_times(_p(t, _d))
+    return dict(preprocess_binning=t[0], render=t[1], render_bwd=t[2], preprocess_bwd=t[3])
 
 
 def max_threads() -> int:
@@ -221,6 +237,22 @@ def mark_visible(means3D, viewmatrix) -> np.ndarray:
     if P:
         lib().gsro_mark_visible(P, _p(m), _p(_np(viewmatrix)), _p(out, _u8))
     return out.astype(bool)
+
+
+def eval_color(D, mean, campos, sh, sg_axis=None, sg_sharpness=None, sg_color=None, sgd=0):
+    """Colour of one Gaussian: sh [SHM,3], sg_* [SGM,3]/[SGM]. Returns (rgb, clamped)."""
+    sh = np.ascontiguousarray(sh, np.float32)
+    SHM = sh.shape[0]
+    SGM = 0 if sg_color is None else np.asarray(sg_color).shape[0]
+    rgb = np.zeros(3, np.float32)
+    cl = np.zeros(3, np.uint8)
+    m, c = np.ascontiguousarray(mean, np.float32), np.ascontiguousarray(campos, np.float32)
+    ax = None if sg_axis is None else np.ascontiguousarray(sg_axis, np.float32)
+    shp = None if sg_sharpness is None else np.ascontiguousarray(sg_sharpness, np.float32)
+    col = None if sg_color is None else np.ascontiguousarray(sg_color, np.float32)
+    lib().gsro_eval_color(int(D), SHM, int(sgd), SGM, _p(m), _p(c), _p(sh), _p(ax), _p(shp), _p(col), _p(rgb),
+                          _p(cl, _u8))
+    return rgb, cl.astype(bool)
 
 
 def higher_msb(n: int) -> int:

@@ -1,0 +1,281 @@
+"""GPU parity tests: the HIP path (libgsr.so through the reference's `_C`
+API) against the C oracle on identical seeded inputs.
+
+Tolerances (north star: 1e-4 relative on identical inputs):
+  * integer outputs (num_rendered, radii, n_contrib-driven structure): exact;
+  * images (color, alpha, normal, median depth): max|a-b| / max|b| <= 1e-4;
+  * gradients: ||a-b|| / ||b|| <= 1e-4 and max|a-b| / max|b| <= 1e-3.  The
+    oracle backward is fed the GPU's own forward images (alpha, normal,
+    mdepth are inputs of the reference backward, rasterize_points.cu:166-168),
+    so the comparison isolates the backward kernels; per-Gaussian sums are
+    accumulated by float atomics on the GPU (order-dependent at ~1 ulp, as
+    in the reference) and in double in the oracle.
+Full-size (C3: 1M Gaussians, 1080p) checks use size-independent properties:
+determinism, radii/K equality with the oracle preprocess, tile-sampled image
+parity and linearity of the backward in the upstream gradients.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import gsr_scene as S
+import helpers as Hh
+from oracle import gsr_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+GRAD_NAMES = ["dmeans2D", "dcolors", "dopacity", "dmeans3D", "dcov3D", "dsh", "dsg_axis", "dsg_sharpness",
+              "dsg_color", "dscales", "drotations"]
+
+
+def _gpu(x):
+    if isinstance(x, torch.Tensor):
+        return x.to(DEV)
+    return torch.Tensor([]) if x is None else x
+
+
+def _fwd_args(c, colors_precomp=None, cov3D=None, scale_modifier=1.0):
+    a = list(Hh.oracle_args(c, colors_precomp=colors_precomp))
+    a[13] = scale_modifier
+    if cov3D is not None:
+        a[4], a[5], a[6] = None, None, cov3D
+    return a
+
+
+def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True):
+    from diff_gaussian_rasterization import _C
+
+    a = _fwd_args(c, colors_precomp, cov3D, scale_modifier)
+    o = O.forward(*a)
+    ga = [_gpu(x) for x in a] + [False]
+    out = _C.rasterize_gaussians(*ga)
+    K, color, alpha, normal, mdepth, radii = out[:6]
+    assert K == o["num_rendered"]
+    assert np.array_equal(radii.cpu().numpy(), o["radii"])
+    geom = c["require_depth"]
+    for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
+        if not geom and name in ("normal", "mdepth"):
+            assert float(t.abs().max()) == 0.0
+            continue
+        assert Hh.rel_err(t.cpu().numpy(), o[name]) <= 1e-4, name
+    if not check_bwd:
+        return
+    g = S.upstream_grads(c["H"], c["W"])
+    g["alpha"] = torch.randn(1, c["H"], c["W"], generator=torch.Generator().manual_seed(5)) * 1e-3
+    al, nm, md = alpha.cpu(), normal.cpu(), mdepth.cpu()
+    b = O.backward(o["state"], *a[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], al, nm, md,
+                   c["cam"].camera_center, o["radii"])
+    gb = _C.rasterize_gaussians_backward(*ga[:19], _gpu(g["color"]), _gpu(g["mdepth"]), _gpu(g["alpha"]),
+                                         _gpu(g["normal"]), alpha, normal, mdepth, _gpu(c["cam"].camera_center),
+                                         radii, out[6], K, out[7], out[8], out[9], geom, False)
+    for name, t in zip(GRAD_NAMES, gb):
+        mine, ref = t.cpu().numpy().astype(np.float64), b[name]
+        assert mine.shape == ref.shape, name
+        if ref.size == 0:
+            continue
+        if not np.any(ref):
+            assert not np.any(mine), name
+            continue
+        l2 = np.linalg.norm(mine - ref) / np.linalg.norm(ref)
+        assert l2 <= 1e-4, (name, l2)
+        assert Hh.rel_err(mine, ref) <= 1e-3, (name, Hh.rel_err(mine, ref))
+
+
+SMALL = [
+    dict(P=40, W=40, H=24, seed=0),
+    dict(P=300, W=64, H=48, seed=1),
+    dict(P=500, W=100, H=70, seed=2, kernel_size=0.1),
+    dict(P=400, W=61, H=53, seed=3, sgm=3, sg_degree=2),
+    dict(P=400, W=64, H=48, seed=4, sh_degree=1),
+    dict(P=400, W=64, H=48, seed=5, require_depth=False),
+    dict(P=400, W=64, H=48, seed=6, bg=(0.3, 0.6, 0.9)),
+    dict(P=10000, W=256, H=256, seed=7, log_scale=math.log(0.03)),  # C1
+    dict(P=10000, W=256, H=256, seed=8, log_scale=math.log(0.03), require_depth=False),
+]
+
+
+@pytest.mark.parametrize("case", SMALL, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_parity_small(case):
+    case = dict(case)
+    ks = case.pop("kernel_size", 0.0)
+    _run(Hh.small_case(kernel_size=ks, **case))
+
+
+def test_parity_colors_precomp():
+    c = Hh.small_case(P=400, W=64, H=48, seed=12)
+    cols = torch.rand(400, 3, generator=torch.Generator().manual_seed(3))
+    _run(c, colors_precomp=cols)
+
+
+def test_parity_scale_modifier():
+    _run(Hh.small_case(P=400, W=64, H=48, seed=13), scale_modifier=1.3)
+
+
+def test_parity_cov3D_precomp():
+    """cov3D_precomp path (render_forward.cu:162-189): Sigma = R S^2 R^T given directly."""
+    c = Hh.small_case(P=300, W=64, H=48, seed=14)
+    s = c["inp"]["scales"].double()
+    q = c["inp"]["rotations"].double()
+    r, x, y, z = q.unbind(1)
+    Rm = torch.stack([torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y)], 1),
+                      torch.stack([2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x)], 1),
+                      torch.stack([2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], 1)], 1)
+    Sig = Rm @ torch.diag_embed(s * s) @ Rm.transpose(1, 2)
+    cov = torch.stack([Sig[:, 0, 0], Sig[:, 0, 1], Sig[:, 0, 2], Sig[:, 1, 1], Sig[:, 1, 2], Sig[:, 2, 2]], 1).float()
+    _run(c, cov3D=cov.contiguous())
+
+
+def test_degenerate_scenes():
+    from diff_gaussian_rasterization import _C
+
+    cam = S.make_camera(48, 32)
+    tx, ty = math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2)
+    bg = torch.tensor([0.25, 0.5, 0.75])
+    # all Gaussians behind the near plane -> background, no instances
+    means = torch.tensor([[0.0, 0.0, 0.1], [0.2, 0.0, -3.0]])
+    out = _C.rasterize_gaussians(bg.to(DEV), means.to(DEV), torch.ones(2, 3, device=DEV), torch.full((2, 1), 0.5,
+                                 device=DEV), torch.full((2, 3), 0.1, device=DEV),
+                                 torch.tensor([[1.0, 0, 0, 0]] * 2, device=DEV), torch.Tensor([]), torch.Tensor([]),
+                                 torch.zeros(2, 0, 3), torch.zeros(2, 0), torch.zeros(2, 0, 3), 0, 0, 1.0,
+                                 cam.world_view_transform.to(DEV), cam.full_proj_transform.to(DEV), tx, ty, 0.0, 32,
+                                 48, cam.camera_center.to(DEV), False, True, False)
+    assert out[0] == 0 and int(out[5].abs().sum()) == 0
+    torch.testing.assert_close(out[1].cpu(), bg[:, None, None].expand(3, 32, 48))
+    assert float(out[2].abs().max()) == 0 and float(out[3].abs().max()) == 0 and float(out[4].abs().max()) == 0
+    # one Gaussian
+    _run(Hh.small_case(P=1, W=32, H=32, seed=3, z_range=(2.0, 2.5)))
+
+
+def test_mark_visible_matches_oracle():
+    from diff_gaussian_rasterization import _C
+
+    c = Hh.small_case(P=2000, W=64, H=48, seed=15, z_range=(-1.0, 6.0))
+    m = c["inp"]["means3D"]
+    got = _C.mark_visible(m.to(DEV), c["cam"].world_view_transform.to(DEV), c["cam"].full_proj_transform.to(DEV))
+    assert np.array_equal(got.cpu().numpy(), O.mark_visible(m, c["cam"].world_view_transform))
+
+
+def test_autograd_render_end_to_end():
+    """gaussian_renderer.render() -> GaussianRasterizer -> autograd, with the
+    GaussianModel getters in front: gradients reach the raw parameters and the
+    viewspace dummy equals dL/dmeans2D from the direct _C call."""
+    import gaussian_renderer as GR
+
+    W, H = 96, 64
+    cam = S.make_camera(W, H).to(DEV)
+    raw = S.make_gaussians(3000, aspect=H / W, z_range=(2.0, 5.0), log_scale_mean=math.log(0.03)).to(DEV)
+    raw.requires_grad_()
+
+    class PC:
+        active_sh_degree, active_sg_degree = 3, 0
+        get_xyz = property(lambda self: raw.xyz)
+        get_scaling_n_opacity_with_3D_filter = property(lambda self: raw.get_scaling_n_opacity_with_3D_filter())
+        get_rotation = property(lambda self: raw.get_rotation())
+        get_features = property(lambda self: raw.get_features())
+        get_sg_axis = property(lambda self: raw.get_sg_axis())
+        get_sg_sharpness = property(lambda self: raw.get_sg_sharpness())
+        get_sg_color = property(lambda self: raw.get_sg_color())
+
+    class Pipe:
+        debug = True
+
+    pkg = GR.render(cam, PC(), Pipe(), torch.zeros(3, device=DEV), 0.0)
+    loss = pkg["render"].square().mean() + pkg["median_depth"].mean() + pkg["normal"].abs().mean()
+    loss.backward()
+    for name in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity"):
+        g = getattr(raw, name).grad
+        assert g is not None and torch.isfinite(g).all() and float(g.abs().sum()) > 0, name
+    vs = pkg["viewspace_points"].grad
+    assert vs is not None and vs.shape == (3000, 3) and float(vs[:, 2].min()) >= 0
+    assert torch.equal(pkg["visibility_filter"], pkg["radii"] > 0)
+
+
+def test_timing_api():
+    from diff_gaussian_rasterization import _C
+
+    c = Hh.small_case(P=500, W=64, H=48, seed=16)
+    ga = [_gpu(x) for x in Hh.oracle_args(c)] + [False]
+    _C.timing_collect()
+    _C.timing_enable(True)
+    _C.rasterize_gaussians(*ga)
+    _C.timing_enable(False)
+    st = _C.timing_collect()
+    for k in ("preprocess", "scan", "emit_keys", "sort", "tile_ranges", "render_fwd"):
+        assert st[k][1] == 1 and st[k][0] > 0, k
+
+
+# ------------------------------------------------------------- full size
+@pytest.fixture(scope="module")
+def c3():
+    W, H, P = 1920, 1080, 1_000_000
+    cam = S.make_camera(W, H)
+    raw = S.make_gaussians(P, aspect=H / W)
+    inp = {k: v.detach().contiguous() for k, v in S.activated_inputs(raw).items()}
+    c = dict(bg=torch.zeros(3), inp=inp, cam=cam, W=W, H=H, sh_degree=3, sg_degree=0, kernel_size=0.0,
+             require_depth=True, tanx=math.tan(cam.FoVx / 2), tany=math.tan(cam.FoVy / 2))
+    return c
+
+
+def test_c3_full_size_properties(c3):
+    from diff_gaussian_rasterization import _C
+
+    args = Hh.oracle_args(c3)
+    ga = [_gpu(x) for x in args] + [False]
+    out1 = _C.rasterize_gaussians(*ga)
+    out2 = _C.rasterize_gaussians(*ga)
+    for k in range(1, 6):  # forward is deterministic (no atomics)
+        assert torch.equal(out1[k], out2[k])
+    K, color, alpha, normal, mdepth, radii = out1[:6]
+    assert torch.isfinite(color).all() and float(alpha.min()) >= 0 and float(alpha.max()) < 1
+    O.set_threads(16)
+    stride = 97  # bounded sample of tiles
+    O.set_tile_stride(stride)
+    try:
+        o = O.forward(*args)
+    finally:
+        O.set_tile_stride(1)
+    assert K == o["num_rendered"]
+    assert np.array_equal(radii.cpu().numpy(), o["radii"])
+    gx = (1920 + 15) // 16
+    mask = np.zeros((1080, 1920), bool)
+    for t in range(0, gx * ((1080 + 15) // 16), stride):
+        ty, tx = divmod(t, gx)
+        mask[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16] = True
+    for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
+        a = t.cpu().numpy()[:, mask]
+        b = o[name][:, mask]
+        bad = np.abs(a - b) > 1e-4 * np.abs(b).max()
+        assert bad.mean() <= 1e-4, (name, bad.mean())  # isolated float-decision flips only
+
+
+def test_c3_backward_linearity(c3):
+    """bwd(g1 + 2 g2) == bwd(g1) + 2 bwd(g2): every gradient is linear in the
+    upstream image gradients (holds at any size; checks nothing is dropped or
+    double-counted in the atomic accumulation)."""
+    from diff_gaussian_rasterization import _C
+
+    ga = [_gpu(x) for x in Hh.oracle_args(c3)] + [False]
+    out = _C.rasterize_gaussians(*ga)
+    K, color, alpha, normal, mdepth, radii = out[:6]
+    g1 = {k: v.to(DEV) for k, v in S.upstream_grads(1080, 1920, seed=1).items()}
+    g2 = {k: v.to(DEV) for k, v in S.upstream_grads(1080, 1920, seed=2).items()}
+
+    def bwd(g):
+        return _C.rasterize_gaussians_backward(*ga[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], alpha,
+                                               normal, mdepth, _gpu(c3["cam"].camera_center), radii, out[6], K,
+                                               out[7], out[8], out[9], True, False)
+
+    b1, b2 = bwd(g1), bwd(g2)
+    b12 = bwd({k: g1[k] + 2 * g2[k] for k in g1})
+    for name, x, y, z in zip(GRAD_NAMES, b1, b2, b12):
+        if name == "dmeans2D":  # the |.| channel is not linear
+            x, y, z = x[:, :2], y[:, :2], z[:, :2]
+        if x.numel() == 0:
+            continue
+        want = (x + 2 * y).double()
+        err = float((z.double() - want).norm() / want.norm().clamp_min(1e-30))
+        assert err <= 1e-4, (name, err)

@@ -1,0 +1,324 @@
+"""CPU tests: pin the C oracle (oracle/gsr_oracle.c) before it is trusted as
+the parity checker of the HIP path.
+
+  * golden fixtures produced by the reference's own Python (tests/golden/):
+    SH evaluation, camera matrices, GaussianModel getters;
+  * an independent float64 torch-autograd restatement (tests/torch_ref.py):
+    forward outputs and every gradient;
+  * closed-form known-answer tests (single isotropic Gaussian, depth ties,
+    tile-rect borders, getHigherMsb).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import gsr_scene as S
+import helpers as Hh
+import torch_ref as R
+from oracle import gsr_oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+# ---------------------------------------------------------------- fixtures
+def test_sh_matches_reference_eval_sh():
+    """oracle colour == reference utils/sh_utils.eval_sh + 0.5, clamped (render_forward.cu:22-78)."""
+    d = np.load(os.path.join(GOLD, "sh_eval.npz"))
+    for deg in range(4):
+        sh, dirs, ref = d[f"sh_{deg}"], d[f"dirs_{deg}"], d[f"out_{deg}"]
+        for i in range(sh.shape[0]):
+            mean = dirs[i] * 3.0  # campos = 0 -> normalised direction == dirs[i]
+            rgb, cl = O.eval_color(deg, mean, np.zeros(3), sh[i].T.copy())
+            want = ref[i] + 0.5
+            np.testing.assert_allclose(rgb, np.maximum(want, 0.0), rtol=2e-6, atol=2e-6)
+            assert (cl == (want < 0)).all()
+
+
+def test_cameras_match_reference():
+    d = np.load(os.path.join(GOLD, "cameras.npz"))
+    for i in range(3):
+        W, H = (int(v) for v in d[f"wh_{i}"])
+        fovx, fovy = d[f"fov_{i}"]
+        cam = S.make_camera(W, H, R=d[f"R_{i}"], T=d[f"T_{i}"], fovx_deg=math.degrees(fovx))
+        assert abs(cam.FoVy - fovy) < 1e-12
+        np.testing.assert_allclose(cam.world_view_transform.numpy(), d[f"world_view_{i}"], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(cam.full_proj_transform.numpy(), d[f"full_proj_{i}"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(cam.camera_center.numpy(), d[f"center_{i}"], rtol=0, atol=1e-5)
+
+
+def test_getters_and_filter3d_match_reference():
+    d = np.load(os.path.join(GOLD, "getters.npz"))
+    t = lambda k: torch.tensor(d["raw_" + k])  # noqa: E731
+
+    class Cam:
+        def __init__(self, R, T, whf):
+            self.R, self.T = torch.tensor(R), torch.tensor(T)
+            self.image_width, self.image_height, self.Fx = float(whf[0]), float(whf[1]), float(whf[2])
+            self.Fy = self.Fx
+
+    cams = [Cam(d["cam_R"][k], d["cam_T"][k], d["cam_WHF"][k]) for k in range(2)]
+    filt = S.compute_filter_3D(t("xyz"), cams)
+    np.testing.assert_allclose(filt.numpy(), d["filter_3D"], rtol=1e-6, atol=0)
+    raw = S.RawGaussians(t("xyz"), t("features_dc"), t("features_rest"), t("scaling"), t("rotation"), t("opacity"),
+                         t("sg_axis"), t("sg_sharpness"), t("sg_color"), torch.tensor(d["filter_3D"]))
+    scales, opac = raw.get_scaling_n_opacity_with_3D_filter()
+    np.testing.assert_array_equal(scales.numpy(), d["scales"])
+    np.testing.assert_array_equal(opac.numpy(), d["opacity"])
+    np.testing.assert_array_equal(raw.get_rotation().numpy(), d["rotation_out"])
+    np.testing.assert_array_equal(raw.get_features().numpy(), d["features"])
+    np.testing.assert_array_equal(raw.get_sg_axis().numpy(), d["sg_axis_out"])
+    np.testing.assert_array_equal(raw.get_sg_sharpness().numpy(), d["sg_sharpness_out"])
+    np.testing.assert_array_equal(raw.get_sg_color().numpy(), d["sg_color_out"])
+
+
+# ------------------------------------------------- oracle vs float64 autograd
+def _torch_ref(c, require_depth=True, colors_precomp=None, sgd=0, kernel_size=0.0, mdepth=None):
+    P = c["inp"]["means3D"].shape[0]
+    inp = {k: v.double().clone().requires_grad_(True) for k, v in c["inp"].items()}
+    cp = None if colors_precomp is None else colors_precomp.double().clone().requires_grad_(True)
+    m2d = torch.zeros(P, 3, dtype=torch.float64, requires_grad=True)
+    cam = c["cam"]
+    pre = R.preprocess(inp["means3D"], inp["scales"], inp["rotations"], inp["opacities"], inp["shs"],
+                       inp["sg_axis"], inp["sg_sharpness"], inp["sg_color"], m2d, cam.world_view_transform.double(),
+                       cam.full_proj_transform.double(), cam.camera_center.double(), c["W"], c["H"], c["tanx"],
+                       c["tany"], kernel_size, c["sh_degree"], sgd, colors_precomp=cp)
+    lists, radii = R.binning(pre, c["W"], c["H"])
+    out = R.render(pre, lists, c["W"], c["H"], c["bg"].double(), require_depth=require_depth,
+                   mdepth_override=None if mdepth is None else torch.as_tensor(mdepth).double())
+    return inp, m2d, cp, out, radii
+
+
+CASES = [
+    dict(P=40, W=40, H=24, seed=0),
+    dict(P=60, W=48, H=40, seed=3, kernel_size=0.1),
+    dict(P=50, W=37, H=29, seed=5, sgm=2, sg_degree=2),
+    dict(P=45, W=40, H=24, seed=7, require_depth=False),
+    dict(P=45, W=40, H=24, seed=9, bg=(0.2, 0.5, 1.0)),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_oracle_matches_float64_autograd(case):
+    case = dict(case)
+    ks = case.pop("kernel_size", 0.0)
+    geom = case.get("require_depth", True)
+    c = Hh.small_case(kernel_size=ks, **case)
+    o = O.forward(*Hh.oracle_args(c))
+    # the median-depth gradient is evaluated at the oracle's own median depth
+    # (it is an input of the backward); the forward mdepth is compared above
+    inp, m2d, _, out, radii = _torch_ref(c, require_depth=geom, sgd=c["sg_degree"], kernel_size=ks,
+                                         mdepth=o["mdepth"] if geom else None)
+    assert (radii == o["radii"]).all()
+    assert (out["n_contrib"] == o["state"].n_contrib()).all()
+    for k in ("color", "alpha") + (("normal", "mdepth") if geom else ()):
+        assert Hh.rel_err(o[k], out[k].detach().numpy()) < 5e-5, k
+    g = S.upstream_grads(c["H"], c["W"])
+    L = (out["color"] * g["color"].double()).sum() + (out["alpha"] * g["alpha"].double()).sum()
+    if geom:
+        L = L + (out["normal"] * g["normal"].double()).sum() + R.median_depth_surrogate(out, g["mdepth"].double())
+    L.backward()
+    b = O.backward(o["state"], *Hh.oracle_args(c)[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], o["alpha"],
+                   o["normal"], o["mdepth"], c["cam"].camera_center, o["radii"])
+    q = c["inp"]["rotations"].double().numpy()
+    tang = lambda v: v - q * (q * v).sum(1, keepdims=True)  # noqa: E731 - dL/dq is defined up to the radial part
+    checks = {
+        "dmeans3D": (b["dmeans3D"], inp["means3D"].grad.numpy()),
+        "dscales": (b["dscales"], inp["scales"].grad.numpy()),
+        "drotations": (tang(b["drotations"]), tang(inp["rotations"].grad.numpy())),
+        "dopacity": (b["dopacity"], inp["opacities"].grad.numpy()),
+        "dsh": (b["dsh"], inp["shs"].grad.numpy()),
+        "dmeans2D": (b["dmeans2D"][:, :2], m2d.grad[:, :2].numpy()),
+    }
+    if c["sg_degree"]:
+        checks.update(dsg_axis=(b["dsg_axis"], inp["sg_axis"].grad.numpy()),
+                      dsg_sharpness=(b["dsg_sharpness"], inp["sg_sharpness"].grad.numpy()),
+                      dsg_color=(b["dsg_color"], inp["sg_color"].grad.numpy()))
+    for k, (mine, ref) in checks.items():
+        assert Hh.rel_err(mine, ref) < 2e-4, (k, Hh.rel_err(mine, ref))
+
+
+def test_oracle_colors_precomp_path():
+    c = Hh.small_case(P=40, W=40, H=24, seed=11)
+    cols = torch.rand(40, 3, generator=torch.Generator().manual_seed(1))
+    o = O.forward(*Hh.oracle_args(c, colors_precomp=cols))
+    inp, m2d, cp, out, _ = _torch_ref(c, colors_precomp=cols, mdepth=o["mdepth"])
+    assert Hh.rel_err(o["color"], out["color"].detach().numpy()) < 5e-5
+    g = S.upstream_grads(c["H"], c["W"])
+    L = (out["color"] * g["color"].double()).sum() + (out["normal"] * g["normal"].double()).sum()
+    L = L + R.median_depth_surrogate(out, g["mdepth"].double())
+    L.backward()
+    args = Hh.oracle_args(c, colors_precomp=cols)
+    b = O.backward(o["state"], *args[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], o["alpha"], o["normal"],
+                   o["mdepth"], c["cam"].camera_center, o["radii"])
+    assert Hh.rel_err(b["dcolors"], cp.grad.numpy()) < 1e-5
+    assert Hh.rel_err(b["dmeans3D"], inp["means3D"].grad.numpy()) < 2e-4
+    assert b["dsh"].size == 0
+
+
+def test_median_depth_gradient_is_implicit_derivative():
+    """The reference's median-depth gradient (render_backward.cu:835-880,
+    983-999) equals the finite-difference derivative of the float64 bisection
+    result w.r.t. a Gaussian's opacity (implicit-function theorem)."""
+    c = Hh.small_case(P=30, W=32, H=32, seed=4)
+    cam = c["cam"]
+
+    def mdepth_sum(op_scale, idx):
+        inp = {k: v.double().clone() for k, v in c["inp"].items()}
+        inp["opacities"][idx] *= op_scale
+        m2d = torch.zeros(30, 3, dtype=torch.float64)
+        pre = R.preprocess(inp["means3D"], inp["scales"], inp["rotations"], inp["opacities"], inp["shs"],
+                           inp["sg_axis"], inp["sg_sharpness"], inp["sg_color"], m2d,
+                           cam.world_view_transform.double(), cam.full_proj_transform.double(),
+                           cam.camera_center.double(), 32, 32, c["tanx"], c["tany"], 0.0, 3, 0)
+        lists, _ = R.binning(pre, 32, 32)
+        return R.render(pre, lists, 32, 32, c["bg"].double(), iters=12)
+
+    base = mdepth_sum(1.0, 0)
+    md = base["mdepth"].detach()
+    inp = {k: v.double().clone().requires_grad_(True) for k, v in c["inp"].items()}
+    m2d = torch.zeros(30, 3, dtype=torch.float64)
+    pre = R.preprocess(inp["means3D"], inp["scales"], inp["rotations"], inp["opacities"], inp["shs"], inp["sg_axis"],
+                       inp["sg_sharpness"], inp["sg_color"], m2d, cam.world_view_transform.double(),
+                       cam.full_proj_transform.double(), cam.camera_center.double(), 32, 32, c["tanx"], c["tany"],
+                       0.0, 3, 0)
+    lists, _ = R.binning(pre, 32, 32)
+    out = R.render(pre, lists, 32, 32, c["bg"].double(), iters=12)
+    w = (md > 0).double()  # pixels with a defined median depth
+    R.median_depth_surrogate(out, w).backward()
+    # pick the Gaussian with the largest analytic sensitivity
+    g = inp["opacities"].grad[:, 0].abs()
+    idx = int(torch.argmax(g))
+    eps = 1e-5
+    fp = mdepth_sum(1 + eps, idx)["mdepth"]
+    fm = mdepth_sum(1 - eps, idx)["mdepth"]
+    fd = float(((fp - fm) * w).sum() / (2 * eps * float(c["inp"]["opacities"][idx])))
+    an = float(inp["opacities"].grad[idx, 0])
+    assert abs(an) > 0
+    assert abs(fd - an) <= 2e-2 * abs(an) + 1e-9, (fd, an)
+
+
+# ------------------------------------------------------------------- KATs
+def test_kat_single_isotropic_gaussian():
+    """One isotropic Gaussian on the optical axis (SURVEY §8(c) KAT 1)."""
+    W = H = 64
+    cam = S.make_camera(W, H)
+    z, s, o = 4.0, 0.05, 0.8
+    means = torch.tensor([[0.0, 0.0, z]])
+    scales = torch.full((1, 3), s)
+    rot = torch.tensor([[1.0, 0.0, 0.0, 0.0]])
+    op = torch.tensor([[o]])
+    sh = torch.zeros(1, 16, 3)
+    sh[0, 0] = torch.tensor([0.2, -0.1, 0.4]) / 0.28209479177387814  # colour = sh0*C0 + 0.5
+    tanx = math.tan(cam.FoVx / 2)
+    tany = math.tan(cam.FoVy / 2)
+    bg = torch.tensor([0.1, 0.2, 0.3])
+    out = O.forward(bg, means, None, op, scales, rot, None, sh, torch.zeros(1, 0, 3), torch.zeros(1, 0),
+                    torch.zeros(1, 0, 3), 0, 0, 1.0, cam.world_view_transform, cam.full_proj_transform, tanx, tany, 0.0,
+                    H, W, cam.camera_center, False, True)
+    f = W / (2 * tanx)
+    sigma_px = s * f / z
+    lam = sigma_px ** 2 + 0.0
+    assert out["radii"][0] == math.ceil(3 * math.sqrt(lam + math.sqrt(0.1)))  # mid^2-det clamped at 0.1
+    # the centre ((W-1)/2) falls between pixels; check the 4 central pixels
+    rgb = np.array([0.7, 0.4, 0.9])
+    c = (W - 1) / 2
+    for py in (31, 32):
+        for px in (31, 32):
+            d2 = (px - c) ** 2 + (py - c) ** 2
+            a = min(0.99, o * math.exp(-0.5 * d2 / lam))
+            np.testing.assert_allclose(out["color"][:, py, px], a * rgb + (1 - a) * bg.numpy(), rtol=2e-5)
+            np.testing.assert_allclose(out["alpha"][0, py, px], a, rtol=2e-5)
+            np.testing.assert_allclose(out["normal"][:, py, px], [0, 0, -1], atol=2e-3)
+            if a >= 0.55:  # T <= 0.45 -> median depth defined: the Gaussian's depth along the pixel ray
+                pnx, pny = (px - c) / f, (py - c) / f
+                ray = math.sqrt(pnx ** 2 + pny ** 2 + 1)
+                assert abs(out["mdepth"][0, py, px] * ray - z) < 3 * s
+
+
+def test_kat_depth_ties_keep_index_order():
+    """Equal sort keys keep emission (Gaussian index) order: stable LSD sort."""
+    W = H = 32
+    cam = S.make_camera(W, H)
+    P = 4
+    means = torch.tensor([[0.0, 0.0, 3.0]] * P)  # identical depth, identical tile
+    scales = torch.full((P, 3), 0.03)
+    rot = torch.tensor([[1.0, 0.0, 0.0, 0.0]] * P)
+    op = torch.full((P, 1), 0.3)
+    cols = torch.rand(P, 3, generator=torch.Generator().manual_seed(0))
+    out = O.forward(torch.zeros(3), means, cols, op, scales, rot, None, None, None, None, None, 0, 0, 1.0,
+                    cam.world_view_transform, cam.full_proj_transform, math.tan(cam.FoVx / 2),
+                    math.tan(cam.FoVy / 2), 0.0, H, W, cam.camera_center, False, False)
+    b = out["state"].binning()
+    keys, plist = b["keys"], b["point_list"]
+    for t in np.unique(keys >> np.uint64(32)):
+        sel = plist[(keys >> np.uint64(32)) == t]
+        assert list(sel) == sorted(sel)
+    assert out["num_rendered"] == 4 * out["state"].geometry()["tiles_touched"][0]
+
+
+def test_kat_rect_at_borders():
+    """tiles_touched equals the getRect area (auxiliary.h:42-49), including
+    Gaussians hanging over the image border and fully off-screen ones."""
+    W, H = 50, 34  # ragged last tiles
+    cam = S.make_camera(W, H)
+    rng = np.random.default_rng(3)
+    P = 400
+    z = rng.uniform(1.5, 4.0, P)
+    tx = math.tan(cam.FoVx / 2)
+    ty = math.tan(cam.FoVy / 2)
+    means = np.stack([rng.uniform(-1.6, 1.6, P) * z * tx, rng.uniform(-1.6, 1.6, P) * z * ty, z], 1)
+    scales = np.exp(rng.normal(math.log(0.05), 0.5, (P, 3)))
+    rot = rng.normal(size=(P, 4))
+    rot /= np.linalg.norm(rot, axis=1, keepdims=True)
+    cols = rng.uniform(size=(P, 3))
+    out = O.forward(torch.zeros(3), means, cols, np.full((P, 1), 0.5), scales, rot, None, None, None, None, None,
+                    0, 0, 1.0, cam.world_view_transform, cam.full_proj_transform, tx, ty, 0.0, H, W,
+                    cam.camera_center, False, False)
+    g = out["state"].geometry()
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    for i in range(P):
+        r = int(out["radii"][i])
+        if r == 0:
+            assert g["tiles_touched"][i] == 0
+            continue
+        x, y = g["means2D"][i]
+        x0 = min(gx, max(0, int((x - r) / 16)))
+        y0 = min(gy, max(0, int((y - r) / 16)))
+        x1 = min(gx, max(0, int((x + r + 15) / 16)))
+        y1 = min(gy, max(0, int((y + r + 15) / 16)))
+        assert g["tiles_touched"][i] == (x1 - x0) * (y1 - y0)
+    assert (out["radii"] == 0).sum() > 0 and (out["radii"] > 0).sum() > 0
+
+
+@pytest.mark.parametrize("n,want", [(1, 1), (2, 2), (255, 8), (256, 9), (2500, 12), (8160, 13), (65536, 17)])
+def test_higher_msb(n, want):
+    assert O.higher_msb(n) == want
+
+
+def test_empty_and_all_culled():
+    W, H = 32, 16
+    cam = S.make_camera(W, H)
+    out = O.forward(torch.zeros(3), np.zeros((0, 3)), None, np.zeros((0, 1)), np.zeros((0, 3)), np.zeros((0, 4)),
+                    None, np.zeros((0, 16, 3)), None, None, None, 3, 0, 1.0, cam.world_view_transform,
+                    cam.full_proj_transform, 0.5, 0.3, 0.0, H, W, cam.camera_center, False, True)
+    assert out["num_rendered"] == 0 and out["color"].sum() == 0
+    # every Gaussian behind the near plane
+    means = np.array([[0.0, 0.0, 0.1], [0.0, 0.0, -2.0]])
+    out = O.forward(torch.tensor([0.5, 0.5, 0.5]), means, np.ones((2, 3)), np.full((2, 1), 0.5),
+                    np.full((2, 3), 0.1), np.array([[1.0, 0, 0, 0]] * 2), None, None, None, None, None, 0, 0, 1.0,
+                    cam.world_view_transform, cam.full_proj_transform, 0.5, 0.3, 0.0, H, W, cam.camera_center, False,
+                    True)
+    assert out["num_rendered"] == 0 and (out["radii"] == 0).all()
+    np.testing.assert_allclose(out["color"], 0.5)
+    assert (out["alpha"] == 0).all() and (out["mdepth"] == 0).all() and (out["normal"] == 0).all()
+
+
+def test_mark_visible():
+    cam = S.make_camera(16, 16)
+    means = np.array([[0, 0, 0.1], [0, 0, 0.3], [5, 5, 1.0], [0, 0, -1]], np.float32)
+    assert list(O.mark_visible(means, cam.world_view_transform)) == [False, True, True, False]

@@ -18,6 +18,9 @@ of its forward, this file reproduces the reference and says so:
       (render_backward.cu:1012) -> tests keep o*G < 0.99.
   Q4  rsigma = sqrt(vb / |uvh|^2): the backward omits d rsigma / d(u, v)
       through vb (render_backward.cu:484-490) -> `vb_rs` below.
+  Q5  Mip-filter coefficient coef = sqrt(det0/det1): the backward uses
+      dL/ddet1 = -dL/ddet0 * coef instead of * coef**2 (render_backward.cu:551)
+      -> `_QuirkCoef`.  Exact when kernel_size = 0 (coef = 1).
 Discrete decisions (culling, rect, skip/stop rules, bisection interval
 choice) follow CR/render_forward.cu; their thresholds are evaluated in float64
 here and in float32 in the oracle, so tests use scenes away from the edges.
@@ -51,6 +54,24 @@ class _QuirkNormalize(torch.autograd.Function):
 
 def _quirk_normalize(x):
     return _QuirkNormalize.apply(x)
+
+
+class _QuirkCoef(torch.autograd.Function):
+    """coef = sqrt(det0 / det1) with the reference's backward
+    (render_backward.cu:548-551): dL/ddet1 = -dL/ddet0 * coef, where the exact
+    derivative has coef**2; and the 1e-6 guard in 0.5 / (coef + 1e-6)."""
+
+    @staticmethod
+    def forward(ctx, det0, det1):
+        coef = torch.sqrt(det0 / det1)
+        ctx.save_for_backward(coef, det1)
+        return coef
+
+    @staticmethod
+    def backward(ctx, g):
+        coef, det1 = ctx.saved_tensors
+        d0 = g * 0.5 / (coef + 1e-6) / det1
+        return d0, -d0 * coef
 
 
 def _sh_color(shs, sg_axis, sg_sharp, sg_color, means, campos, deg, sgd):
@@ -116,7 +137,7 @@ def preprocess(means3D, scales, rotations, opacities, shs, sg_axis, sg_sharp, sg
     a0, b0, c0 = cov[:, 0, 0], cov[:, 0, 1], cov[:, 1, 1]
     det0 = torch.clamp(a0 * c0 - b0 * b0, min=1e-6)
     det1 = torch.clamp((a0 + kernel_size) * (c0 + kernel_size) - b0 * b0, min=1e-6)
-    coef = torch.sqrt(det0 / det1)
+    coef = _QuirkCoef.apply(det0, det1)
     a, b, c = a0 + kernel_size, b0, c0 + kernel_size
     det = a * c - b * b
     conic = torch.stack([c / det, -b / det, a / det], 1)
@@ -187,7 +208,7 @@ def binning(pre, W, H):
     return lists, radii
 
 
-def render(pre, lists, W, H, bg, require_depth=True, split=8, iters=5, sample_range=0.4):
+def render(pre, lists, W, H, bg, require_depth=True, split=8, iters=5, sample_range=0.4, mdepth_override=None):
     """Dense composite per tile (render_forward.cu:412-670); returns outputs and
     the median-depth surrogate pieces for the implicit gradient."""
     gx = (W + 15) // 16
@@ -284,6 +305,10 @@ def render(pre, lists, W, H, bg, require_depth=True, split=8, iters=5, sample_ra
         pny = (py - (H - 1) / 2.0) / fy
         rln = 1.0 / torch.sqrt(pnx ** 2 + pny ** 2 + 1)
         mdepth.view(-1)[lin] = tm * rln
+        if mdepth_override is not None:
+            # evaluate the implicit gradient at a given median depth (the backward
+            # receives mdepth as an input, render_backward.cu:828)
+            tm = torch.as_tensor(mdepth_override, dtype=dt).reshape(-1)[lin] / rln
         # implicit-gradient surrogate pieces (render_backward.cu:835-880, 983-999)
         logT = torch.zeros(npx, dtype=dt)
         dlogT_dt = torch.zeros(npx, dtype=dt)

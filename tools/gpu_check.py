@@ -28,7 +28,9 @@ def run(P, W, H, require_depth=True, seed=0, **kw):
     names = ["dmeans2D","dcolors","dopacity","dmeans3D","dcov3D","dsh","dsg_axis","dsg_sharpness","dsg_color","dscales","drotations"]
     for n_, t in zip(names, gb):
         a = t.cpu().numpy(); bb = b[n_]
-        if a.size: print(f"   {n_}: relmax={Hh.rel_err(a,bb):.3e} frac>1e-3={Hh.frac_bad(a,bb,1e-3,1e-3*np.abs(bb).max()):.2e}")
+        if a.size:
+            l2 = np.linalg.norm(a.astype(np.float64) - bb) / max(np.linalg.norm(bb), 1e-30)
+            print(f"   {n_}: relmax={Hh.rel_err(a,bb):.3e} relL2={l2:.3e} frac>1e-3={Hh.frac_bad(a,bb,1e-3,1e-3*np.abs(bb).max()):.2e}")
 
 def bench(P=1_000_000, W=1920, H=1080, require_depth=True, iters=10):
     dev = torch.device("cuda")

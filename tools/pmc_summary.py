@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output of tools/profile.sh into profiles/.
+
+  python tools/pmc_summary.py gpurun_out/prof_r1 profiles r1
+
+Writes
+  profiles/<tag>_kernel_stats.csv   (rocprofv3 --kernel-trace --stats summary, copied)
+  profiles/<tag>_stages.json        per-stage average duration and HBM bytes per launch
+  profiles/pmc_summary.json         same content; bench.py reads `traffic` from it
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come
+from separate --pmc passes, in KiB; on gfx950 FETCH_SIZE reports half the bytes
+of wide coalesced reads, so hbm = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+(Infinity-Cache hits are included in the fabric counters.)
+"""
+from __future__ import annotations
+
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def stage_of(name: str) -> str | None:
+    n = name
+    if "preprocess_fwd_kernel" in n:
+        return "preprocess"
+    if "preprocess_bwd_kernel" in n:
+        return "preprocess_bwd"
+    if "emit_keys_kernel" in n:
+        return "emit_keys"
+    if "tile_ranges_kernel" in n:
+        return "tile_ranges"
+    if "render_fwd_kernel" in n:
+        return "render_fwd"
+    if "render_bwd_kernel" in n:
+        return "render_bwd"
+    if "radix_sort" in n or "onesweep" in n:
+        return "sort"
+    if "scan" in n:
+        return "scan"
+    return None
+
+
+def per_stage_counter(path: str, counter: str, n_calls: dict) -> dict:
+    tot = defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        st = stage_of(r["Kernel_Name"])
+        if st:
+            tot[st] += float(r["Counter_Value"])
+    return {k: v / max(1, n_calls.get(k, 1)) for k, v in tot.items()}
+
+
+def launches(path: str, counter: str) -> dict:
+    """Number of forward / backward calls seen in a counter pass."""
+    seen = defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        st = stage_of(r["Kernel_Name"])
+        if st:
+            seen[st].add(r["Dispatch_Id"])
+    calls = {k: len(v) for k, v in seen.items()}
+    fwd = calls.get("preprocess", 1)
+    bwd = calls.get("preprocess_bwd", 1)
+    out = {}
+    for k in calls:
+        out[k] = bwd if k in ("render_bwd", "preprocess_bwd") else fwd
+    return out
+
+
+def main():
+    src, dst, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    # average duration per stage call from the kernel trace (skip each stage's
+    # first call: one-time initialisation inside the warm-up)
+    dur = defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
+        st = stage_of(r["Kernel_Name"])
+        if st:
+            dur[st].append((int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    fetch_csv = os.path.join(src, "fetch", "run_counter_collection.csv")
+    write_csv = os.path.join(src, "write", "run_counter_collection.csv")
+    nf = launches(fetch_csv, "FETCH_SIZE")
+    nw = launches(write_csv, "WRITE_SIZE")
+    fetch = per_stage_counter(fetch_csv, "FETCH_SIZE", nf)
+    write = per_stage_counter(write_csv, "WRITE_SIZE", nw)
+    stages = {}
+    ncalls_trace = defaultdict(int)
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
+        if stage_of(r["Kernel_Name"]) == "preprocess":
+            ncalls_trace["fwd"] += 1
+        if stage_of(r["Kernel_Name"]) == "preprocess_bwd":
+            ncalls_trace["bwd"] += 1
+    for st, lst in dur.items():
+        lst.sort()
+        n = ncalls_trace["bwd" if st in ("render_bwd", "preprocess_bwd") else "fwd"]
+        per_call = max(1, len(lst) // max(1, n))
+        calls = [sum(d for _, d in lst[i:i + per_call]) for i in range(0, len(lst), per_call)]
+        calls.sort()
+        avg_ns = calls[len(calls) // 2]  # median call: robust to one-off stalls
+        f = fetch.get(st)
+        w = write.get(st)
+        hbm = None if f is None or w is None else (2.0 * f + w) * 1024.0
+        stages[st] = {"avg_call_ms": round(avg_ns / 1e6, 4), "max_call_ms": round(calls[-1] / 1e6, 4),
+                      "calls": len(calls), "dispatches_per_call": per_call,
+                      "fetch_kib_per_call": f, "write_kib_per_call": w, "hbm_bytes_per_launch": hbm}
+    out = {"tag": tag, "source": src, "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950)",
+           "stages": stages}
+    for name in (f"{tag}_stages.json", "pmc_summary.json"):
+        with open(os.path.join(dst, name), "w") as fh:
+            json.dump(out, fh, indent=1)
+    for st, v in sorted(stages.items(), key=lambda kv: -kv[1]["avg_call_ms"]):
+        print(f"{st:16s} {v['avg_call_ms']:8.3f} ms  hbm/call={v['hbm_bytes_per_launch']}")
+
+
+if __name__ == "__main__":
+    main()
