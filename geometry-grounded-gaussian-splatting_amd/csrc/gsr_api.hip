@@ -209,7 +209,24 @@ struct StageTimer {
 
 }  // namespace
 
+namespace gsr {
+static int g_options[kNumOptions] = {1, 0, 0, 0, 0, 0, 0, 0};
+int option(int which) { return (which >= 0 && which < kNumOptions) ? g_options[which] : 0; }
+}  // namespace gsr
+
 extern "C" {
+
+int gsr_debug_render_stats(unsigned long long* out8, int reset) {
+    hipError_t e = gsr::read_render_stats(out8, reset != 0);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "render stats", e);
+}
+
+int gsr_set_option(int opt, int value) {
+    if (opt < 0 || opt >= gsr::kNumOptions) return fail(GSR_ERR_ARGS, "unknown option");
+    gsr::g_options[opt] = value;
+    return GSR_OK;
+}
+
 
 int gsr_abi_version(void) { return 2; }
 

@@ -38,14 +38,37 @@ struct RenderFwdArgs {
     float* out_alpha;
     float* out_normal;
     float* out_mdepth;
+    float one;  // 1.0f, passed at run time so rsq(1.0) is evaluated by the hardware
 };
 
-template <bool FIRST>
+// One contributor's factor on the bisection samples (render_forward.cu:610-621):
+//   T_p[s] *= (ts > t_peak ? 1 - a : 1 - a g) * rsqrt(1 - a g),  g = exp(-delta^2 / 2)
+// Exact shortcut (SKIP): when every sample of the window has |delta| > 7,
+// a*g < e^-24.5 < 2^-25, so 1 - a*g rounds to exactly 1.0f and the factor is
+// exactly (1 - a) * rsq(1) in front of the window or rsq(1) behind it (the
+// samples are monotone in s, so the two window ends decide).  rsq1 is the
+// hardware's rsq(1.0) so the shortcut is bit-identical to the full path.
+template <bool FIRST, bool SKIP>
 __device__ __forceinline__ void bisect_step(float (&Tp)[kSplit + 1], float dmin, float interval, float alpha,
-                                            float t_peak, float rsig) {
+                                            float t_peak, float rsig, float rsq1) {
     constexpr int START = FIRST ? 0 : 1;
     constexpr int END = FIRST ? kSplit + 1 : kSplit;
     const bool ball = rsig > 0.f;
+    if constexpr (SKIP) {
+        const float d_lo = ((dmin + interval * START) - t_peak) * rsig;
+        const float d_hi = ((dmin + interval * (END - 1)) - t_peak) * rsig;
+        if (ball && d_lo > 7.f) {
+            const float f = (1.f - alpha) * rsq1;
+#pragma unroll
+            for (int s = START; s < END; s++) Tp[s] *= f;
+            return;
+        }
+        if (ball && d_hi < -7.f) {
+#pragma unroll
+            for (int s = START; s < END; s++) Tp[s] *= rsq1;
+            return;
+        }
+    }
 #pragma unroll
     for (int s = START; s < END; s++) {
         const float ts = dmin + interval * s;
@@ -57,7 +80,13 @@ __device__ __forceinline__ void bisect_step(float (&Tp)[kSplit + 1], float dmin,
     }
 }
 
-template <bool GEOM>
+// Diagnostic counters (STATS builds only, option GSR_OPT_RENDER_STATS):
+// [0] bisection wave-visits, [1] lanes reaching a bisection step,
+// [2] wave-visits with any lane on the full path, [3] lanes on the full path,
+// [4] composite wave-visits, [5] composite active lanes.
+__device__ unsigned long long g_render_stats[8];
+
+template <bool GEOM, bool SKIP, bool STATS = false>
 __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 256 x 16 B = 16 KB) aliased with the
     // bisection cache (3 x 512 x 16 B = 24 KB).
@@ -145,7 +174,9 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
 
     float mDepth = 0.f;
     if constexpr (GEOM) {
+        unsigned long long st[4] = {0, 0, 0, 0};
         float Tp[kSplit + 1];
+        const float rsq1 = __builtin_amdgcn_rsqf(a.one);  // hardware rsq(1.0) (kept opaque to the compiler)
         float dmin = fmaxf(m_init - kSampleRange, 0.f);
         float dmax = fmaxf(m_init + kSampleRange, 0.f);
         bool in_range = T <= kMinTransmittance;
@@ -191,6 +222,10 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 for (int j = 0; !bdone && j < n; j++) {
                     c++;
                     bdone = c >= last;
+                    if constexpr (STATS) {
+                        const unsigned long long m = __ballot(1);
+                        if ((tid & 63) == __builtin_ctzll(m)) st[0] += 1;
+                    }
                     const float4 w0 = c_w0[j];
                     const float dx = w0.x - pixx, dy = w0.y - pixy;
                     const float4 w1 = c_w1[j];
@@ -200,8 +235,21 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                     if (alpha < 1.0f / 255.0f) continue;
                     const float4 w2 = c_w2[j];
                     const float t_peak = w1.z * dx + w1.w * dy + w2.x;
-                    if (first) bisect_step<true>(Tp, dmin, interval, alpha, t_peak, w2.y);
-                    else bisect_step<false>(Tp, dmin, interval, alpha, t_peak, w2.y);
+                    if constexpr (STATS) {
+                        const int START = first ? 0 : 1, END = first ? kSplit + 1 : kSplit;
+                        const float d_lo = ((dmin + interval * START) - t_peak) * w2.y;
+                        const float d_hi = ((dmin + interval * (END - 1)) - t_peak) * w2.y;
+                        const bool full = !(w2.y > 0.f && (d_lo > 7.f || d_hi < -7.f));
+                        const unsigned long long m = __ballot(1);
+                        const unsigned long long f = __ballot(full);
+                        if ((tid & 63) == __builtin_ctzll(m)) {
+                            st[1] += __popcll(m);
+                            st[2] += f != 0ull;
+                            st[3] += __popcll(f);
+                        }
+                    }
+                    if (first) bisect_step<true, SKIP>(Tp, dmin, interval, alpha, t_peak, w2.y, rsq1);
+                    else bisect_step<false, SKIP>(Tp, dmin, interval, alpha, t_peak, w2.y, rsq1);
                 }
             }
             if (first) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
@@ -219,6 +267,10 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             dmin = dmin + (start_id + 0) * interval;
             Tp[0] = lo;
             Tp[kSplit] = hi;
+        }
+        if constexpr (STATS) {
+            for (int q = 0; q < 4; q++)
+                if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
         }
         float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
         w_max = fminf(fmaxf(w_max, 0.f), 1.f);  // __saturatef (NaN -> 0)
@@ -273,12 +325,28 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.out_alpha = out_alpha;
     a.out_normal = out_normal;
     a.out_mdepth = out_mdepth;
+    a.one = 1.0f;
     if (a.num_tiles == 0) return hipSuccess;
-    if (p.require_depth)
-        hipLaunchKernelGGL(render_fwd_kernel<true>, dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
-    else
-        hipLaunchKernelGGL(render_fwd_kernel<false>, dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+    if (p.require_depth) {
+        if (option(kOptRenderStats))
+            hipLaunchKernelGGL((render_fwd_kernel<true, true, true>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+        else if (option(kOptBisectSkip))
+            hipLaunchKernelGGL((render_fwd_kernel<true, true>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+        else
+            hipLaunchKernelGGL((render_fwd_kernel<true, false>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+    } else {
+        hipLaunchKernelGGL((render_fwd_kernel<false, false>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+    }
     return hipGetLastError();
+}
+
+hipError_t read_render_stats(unsigned long long* out, bool reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_render_stats), sizeof(unsigned long long) * 8);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_render_stats), z, sizeof(z));
+    }
+    return e;
 }
 
 }  // namespace gsr

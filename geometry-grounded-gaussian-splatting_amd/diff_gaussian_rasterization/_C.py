@@ -48,6 +48,8 @@ def _load():
                                          + [f] * 3 + [vp] * 4 + [vp] * 4 + [vp] * 4 + [vp] * 11 + [i, i, vp])
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
+    L.gsr_set_option.argtypes = [i, i]
+    L.gsr_debug_render_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i]
     L.gsr_timing_enable.argtypes = [i]
     L.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i)]
     L.gsr_stage_name.restype = ctypes.c_char_p
@@ -64,6 +66,20 @@ def loaded_library_path() -> str:
 
 
 NUM_STAGES = 9
+OPT_BISECT_SKIP = 0
+OPT_RENDER_STATS = 1
+
+
+def debug_render_stats(reset: bool = True) -> list:
+    """Counters of forward launches made with OPT_RENDER_STATS (render_fwd.hip)."""
+    out = (ctypes.c_ulonglong * 8)()
+    _check(_load().gsr_debug_render_stats(out, int(bool(reset))))
+    return list(out)
+
+
+def set_option(opt: int, value: int) -> None:
+    """Select an A/B kernel variant (gsr_set_option); variants are bit-identical."""
+    _check(_load().gsr_set_option(int(opt), int(value)))
 
 
 def timing_enable(on: bool = True) -> None:

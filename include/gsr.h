@@ -123,6 +123,17 @@ int gsr_timing_enable(int on);
 int gsr_timing_collect(double* ms, int* launches);
 const char* gsr_stage_name(int stage);
 
+/*
+ * Process-wide switches selecting A/B variants of a kernel, for measuring one
+ * against the other in the same process (all variants give bit-identical
+ * results).  GSR_OPT_BISECT_SKIP (default 1): exact shortcut for bisection
+ * samples far from a Gaussian's ray peak (render_fwd.hip).
+ */
+enum gsr_option { GSR_OPT_BISECT_SKIP = 0, GSR_OPT_RENDER_STATS = 1 };
+int gsr_set_option(int opt, int value);
+/* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (8 values, see render_fwd.hip). */
+int gsr_debug_render_stats(unsigned long long* out8, int reset);
+
 /* Human-readable message for the last non-OK status on this thread. */
 const char* gsr_last_error(void);
 

@@ -252,6 +252,23 @@ def test_c3_full_size_properties(c3):
         assert bad.mean() <= 1e-4, (name, bad.mean())  # isolated float-decision flips only
 
 
+def test_c3_bisection_shortcut_is_bit_exact(c3):
+    """The far-sample shortcut of the median-depth bisection (render_fwd.hip
+    bisect_step<SKIP>) changes no bit of any output."""
+    from diff_gaussian_rasterization import _C
+
+    ga = [_gpu(x) for x in Hh.oracle_args(c3)] + [False]
+    try:
+        _C.set_option(_C.OPT_BISECT_SKIP, 0)
+        ref = _C.rasterize_gaussians(*ga)
+        _C.set_option(_C.OPT_BISECT_SKIP, 1)
+        got = _C.rasterize_gaussians(*ga)
+    finally:
+        _C.set_option(_C.OPT_BISECT_SKIP, 1)
+    for k in range(1, 6):
+        assert torch.equal(ref[k], got[k]), k
+
+
 def test_c3_backward_linearity(c3):
     """bwd(g1 + 2 g2) == bwd(g1) + 2 bwd(g2): every gradient is linear in the
     upstream image gradients (holds at any size; checks nothing is dropped or

@@ -53,9 +53,18 @@ def bench(P=1_000_000, W=1920, H=1080, require_depth=True, iters=10):
     print(f"bench P={P} {W}x{H} geom={require_depth}: K={K} {dt*1e3:.2f} ms/iter = {1/dt:.1f} it/s")
 
 if __name__ == "__main__":
-    run(40, 40, 24)
-    run(300, 64, 48, seed=1)
-    run(10000, 256, 256, seed=2, log_scale=math.log(0.03))
-    run(10000, 256, 256, seed=2, log_scale=math.log(0.03), require_depth=False)
-    bench(require_depth=True)
+    _C.set_option(_C.OPT_RENDER_STATS, 1)
+    _C.debug_render_stats(True)
+    bench(require_depth=True, iters=1)
+    st = _C.debug_render_stats(True)
+    _C.set_option(_C.OPT_RENDER_STATS, 0)
+    print("stats per forward (4 calls):", [v / 4 for v in st[:4]],
+          "lanes/visit=%.1f full-visit-frac=%.3f full-lane-frac=%.3f" % (st[1] / max(st[0], 1), st[2] / max(st[0], 1), st[3] / max(st[1], 1)))
+    for opt in (0, 1, 0, 1):
+        _C.set_option(_C.OPT_BISECT_SKIP, opt)
+        print("bisect skip", opt)
+        bench(require_depth=True)
     bench(require_depth=False)
+    _C.timing_enable(True)
+    bench(require_depth=True, iters=5)
+    print({k: round(v[0] / max(v[1], 1), 3) for k, v in _C.timing_collect().items()})
