@@ -164,4 +164,21 @@ __device__ inline uint32_t xcd_remap(uint32_t b, uint32_t n) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
+// Footprint of a splat record at a pixel offset (dx, dy) = (mean - pixel):
+//   power  = -0.5 (a dx^2 + c dy^2) - b dx dy   (render_forward.cu:486-487)
+//   t_peak = plane.x dx + plane.y dy + |t|      (render_forward.cu:513, 603)
+// Every rounding is spelled out (explicit fma, contraction off) so the
+// composite, the median-depth bisection and the backward — compiled in
+// different contexts — agree bit for bit on alpha and on which
+// (pixel, splat) pairs contribute.
+__device__ __forceinline__ float splat_power(const float4& w0, const float4& w1, float dx, float dy) {
+#pragma clang fp contract(off)
+    const float q = __builtin_fmaf(w1.x * dy, dy, (w0.z * dx) * dx);
+    return __builtin_fmaf(-0.5f, q, -((w0.w * dx) * dy));
+}
+__device__ __forceinline__ float splat_tpeak(const float4& w1, const float4& w2, float dx, float dy) {
+#pragma clang fp contract(off)
+    return __builtin_fmaf(w1.w, dy, w1.z * dx) + w2.x;
+}
+
 }  // namespace gsr

@@ -108,12 +108,12 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
                 const float4 w0 = s_w0[j];
                 const float dx = w0.x - pixx, dy = w0.y - pixy;
                 const float4 w1 = s_w1[j];
-                const float power = -0.5f * (w0.z * dx * dx + w1.x * dy * dy) - w0.w * dx * dy;
+                const float power = splat_power(w0, w1, dx, dy);
                 if (power > 0.0f) continue;
                 const float alpha = fminf(0.99f, w1.y * __expf(power));
                 if (alpha < 1.0f / 255.0f) continue;
                 const float4 w2 = s_w2[j];
-                const float t_peak = w1.z * dx + w1.w * dy + w2.x;
+                const float t_peak = splat_tpeak(w1, w2, dx, dy);
                 const float rsig = w2.y;
                 const float t_delta = (mDepth - t_peak) * rsig;
                 const float G_exp = __expf(-0.5f * t_delta * t_delta);
@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
             const float4 w0 = s_w0[j];
             const float dx = w0.x - pixx, dy = w0.y - pixy;
             const float4 w1 = s_w1[j];
-            const float power = -0.5f * (w0.z * dx * dx + w1.x * dy * dy) - w0.w * dx * dy;
+            const float power = splat_power(w0, w1, dx, dy);
             const float G = __expf(power);
             const float alpha = fminf(0.99f, w1.y * G);
             const bool valid = inside && !(contributor >= last || power > 0.0f || alpha < 1.0f / 255.0f);
@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
                     f[kAccNormal + 0] = bw * dLn0;
                     f[kAccNormal + 1] = bw * dLn1;
                     f[kAccNormal + 2] = bw * dLn2;
-                    const float t_peak = w1.z * dx + w1.w * dy + w2.x;
+                    const float t_peak = splat_tpeak(w1, w2, dx, dy);
                     const float rsig = w2.y;
                     const float t_delta = (mDepth - t_peak) * rsig;
                     const float G_exp = __expf(-0.5f * t_delta * t_delta);

@@ -14,15 +14,30 @@
 //
 // GEOM: after the composite the tile's max contributor is reduced across the
 // block and the median depth is found by the reference's 5 x 8-way bisection
-// of the vacancy transmittance (render_forward.cu:549-645).  When the tile's
-// contributing prefix fits (<= kResident records) it is staged into LDS once
-// (48 B per record: w0, w1, w2) and all five bisection passes run out of LDS
-// with no further barriers; longer lists are restaged per pass.
+// of the vacancy transmittance (render_forward.cu:549-645).  The bisection
+// only multiplies in the contributors a pixel actually blended (the others
+// fail the same power/alpha test in every pass), so the composite records
+// them as a per-pixel bitmask in LDS.  When the tile's contributing prefix
+// fits (<= kResident records) it is staged into LDS once (48 B per record:
+// w0, w1, w2) and every lane walks its own bitmask in increasing order —
+// the lanes of a wave then do useful work on every step instead of idling
+// on the ~2/3 of (pixel, contributor) pairs that fail the test (measured on
+// C3 with GSR_OPT_RENDER_STATS).  Longer lists keep the wave-uniform walk
+// with the records restaged per pass.
+// Contraction is off for this file: every fma below is written out, so each
+// template instance rounds identically (the SKIP/no-SKIP outputs are compared
+// bit for bit in tests/test_gpu_parity.py).
+#pragma clang fp contract(off)
+
+#include <type_traits>
+
 #include "gsr_kernels.h"
 
 namespace gsr {
 
-constexpr int kResident = 512;
+constexpr int kResident = 384;
+constexpr int kMaskWords = kResident / 32;
+constexpr int kMaskStride = kMaskWords + 1;  // odd row stride: conflict-free LDS rows
 
 struct RenderFwdArgs {
     const uint2* ranges;
@@ -43,22 +58,33 @@ struct RenderFwdArgs {
 
 // One contributor's factor on the bisection samples (render_forward.cu:610-621):
 //   T_p[s] *= (ts > t_peak ? 1 - a : 1 - a g) * rsqrt(1 - a g),  g = exp(-delta^2 / 2)
+// Evaluated two samples at a time with packed fp32 (v_pk_{add,mul,fma}_f32).
+// Rewrites that keep every rounding of the scalar form:
+//  * exp(-delta^2/2) = exp2(round(delta*delta) * (-0.5 * log2e)): __expf is
+//    v_exp_f32(x * log2e) and scaling by -0.5 is exact, so the product folds
+//    into one constant;
+//  * a non-ball splat (rsigma <= 0, g = 0 in the reference) runs with
+//    alpha_g = 0 and rsigma = 0: delta = 0, g = 1, 1 - 0*g = 1 exactly.
 // Exact shortcut (SKIP): when every sample of the window has |delta| > 7,
 // a*g < e^-24.5 < 2^-25, so 1 - a*g rounds to exactly 1.0f and the factor is
 // exactly (1 - a) * rsq(1) in front of the window or rsq(1) behind it (the
 // samples are monotone in s, so the two window ends decide).  rsq1 is the
 // hardware's rsq(1.0) so the shortcut is bit-identical to the full path.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr float kHalfNegLog2e = -0.5f * 1.44269502162933349609375f;  // -0.5 * (float)log2(e), exact
+
 template <bool FIRST, bool SKIP>
-__device__ __forceinline__ void bisect_step(float (&Tp)[kSplit + 1], float dmin, float interval, float alpha,
+__device__ __forceinline__ void bisect_step(float (&Tp)[kSplit + 1], const float (&ts)[kSplit + 1], float alpha,
                                             float t_peak, float rsig, float rsq1) {
     constexpr int START = FIRST ? 0 : 1;
     constexpr int END = FIRST ? kSplit + 1 : kSplit;
     const bool ball = rsig > 0.f;
+    const float om = 1.f - alpha;
     if constexpr (SKIP) {
-        const float d_lo = ((dmin + interval * START) - t_peak) * rsig;
-        const float d_hi = ((dmin + interval * (END - 1)) - t_peak) * rsig;
+        const float d_lo = (ts[START] - t_peak) * rsig;
+        const float d_hi = (ts[END - 1] - t_peak) * rsig;
         if (ball && d_lo > 7.f) {
-            const float f = (1.f - alpha) * rsq1;
+            const float f = om * rsq1;
 #pragma unroll
             for (int s = START; s < END; s++) Tp[s] *= f;
             return;
@@ -69,21 +95,36 @@ __device__ __forceinline__ void bisect_step(float (&Tp)[kSplit + 1], float dmin,
             return;
         }
     }
+    const float ag = ball ? alpha : 0.f;
+    const float rg = ball ? rsig : 0.f;
+    const f32x2 ag2 = {ag, ag}, rg2 = {rg, rg}, tp2 = {t_peak, t_peak};
+    const f32x2 c2 = {kHalfNegLog2e, kHalfNegLog2e}, one2 = {1.f, 1.f};
 #pragma unroll
-    for (int s = START; s < END; s++) {
-        const float ts = dmin + interval * s;
-        const float delta = (ts - t_peak) * rsig;
-        const float gg = ball ? __expf(-0.5f * delta * delta) : 0.f;
-        const float omg = 1.f - alpha * gg;
-        const float rv = __builtin_amdgcn_rsqf(omg);
-        Tp[s] *= (ts > t_peak ? (1.f - alpha) : omg) * rv;
+    for (int s = START; s + 1 < END; s += 2) {
+        const f32x2 t = {ts[s], ts[s + 1]};
+        const f32x2 delta = (t - tp2) * rg2;
+        const f32x2 e = (delta * delta) * c2;
+        const f32x2 g = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+        const f32x2 omg = __builtin_elementwise_fma(-ag2, g, one2);
+        const f32x2 rv = {__builtin_amdgcn_rsqf(omg.x), __builtin_amdgcn_rsqf(omg.y)};
+        const f32x2 sel = {t.x > t_peak ? om : omg.x, t.y > t_peak ? om : omg.y};
+        f32x2 T2 = {Tp[s], Tp[s + 1]};
+        T2 *= sel * rv;
+        Tp[s] = T2.x;
+        Tp[s + 1] = T2.y;
+    }
+    if constexpr (((END - START) & 1) != 0) {
+        constexpr int s = END - 1;
+        const float delta = (ts[s] - t_peak) * rg;
+        const float g = __builtin_amdgcn_exp2f((delta * delta) * kHalfNegLog2e);
+        const float omg = __builtin_fmaf(-ag, g, 1.f);
+        Tp[s] *= (ts[s] > t_peak ? om : omg) * __builtin_amdgcn_rsqf(omg);
     }
 }
 
 // Diagnostic counters (STATS builds only, option GSR_OPT_RENDER_STATS):
-// [0] bisection wave-visits, [1] lanes reaching a bisection step,
-// [2] wave-visits with any lane on the full path, [3] lanes on the full path,
-// [4] composite wave-visits, [5] composite active lanes.
+// [0] bisection wave-steps and [1] active lanes on the per-lane (resident)
+// walk; [2] wave-steps and [3] active lanes on the wave-uniform walk.
 __device__ unsigned long long g_render_stats[8];
 
 template <bool GEOM, bool SKIP, bool STATS = false>
@@ -91,6 +132,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 256 x 16 B = 16 KB) aliased with the
     // bisection cache (3 x 512 x 16 B = 24 KB).
     __shared__ float4 s_rec[3 * kResident];
+    __shared__ uint32_t s_mask[GEOM ? kTilePixels * kMaskStride : 1];  // blended contributors per pixel
     __shared__ int s_alive[2][4];
     __shared__ uint32_t s_max[4];
 
@@ -109,7 +151,17 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     float4* s_w0 = s_rec;
     float4* s_w1 = s_rec + kTilePixels;
     float4* s_w2 = s_rec + 2 * kTilePixels;
-    float4* s_w3 = s_rec + 3 * kTilePixels;  // within the 24 KB (3*512 float4 >= 4*256)
+    float4* s_w3 = s_rec + 3 * kTilePixels;  // within the 18 KB (3*384 float4 >= 4*256)
+    static_assert(3 * kResident >= 4 * kTilePixels, "composite staging must fit in the bisection cache");
+
+    // each lane owns one mask row: no barrier needed between init, writes and reads
+    uint32_t* my_mask = s_mask + (GEOM ? tid * kMaskStride : 0);
+    uint32_t mask_cur = 0;
+    int mask_w = 0;
+    if constexpr (GEOM) {
+#pragma unroll
+        for (int q = 0; q < kMaskWords; q++) my_mask[q] = 0u;
+    }
 
     float T = 1.0f;
     uint32_t contributor = 0, last = 0;
@@ -139,7 +191,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             const float4 w0 = s_w0[j];
             const float dx = w0.x - pixx, dy = w0.y - pixy;
             const float4 w1 = s_w1[j];
-            const float power = -0.5f * (w0.z * dx * dx + w1.x * dy * dy) - w0.w * dx * dy;
+            const float power = splat_power(w0, w1, dx, dy);
             if (power > 0.0f) continue;
             const float alpha = fminf(0.99f, w1.y * __expf(power));
             if (alpha < 1.0f / 255.0f) continue;
@@ -151,20 +203,31 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             const float aT = alpha * T;
             const float4 w2 = s_w2[j];
             const float4 w3 = s_w3[j];
-            C0 += w2.z * aT;
-            C1 += w2.w * aT;
-            C2 += w3.x * aT;
+            C0 = __builtin_fmaf(w2.z, aT, C0);
+            C1 = __builtin_fmaf(w2.w, aT, C1);
+            C2 = __builtin_fmaf(w3.x, aT, C2);
             if constexpr (GEOM) {
-                const float t = w1.z * dx + w1.w * dy + w2.x;
-                N0 += w3.y * aT;
-                N1 += w3.z * aT;
-                N2 += w3.w * aT;
+                const float t = splat_tpeak(w1, w2, dx, dy);
+                N0 = __builtin_fmaf(w3.y, aT, N0);
+                N1 = __builtin_fmaf(w3.z, aT, N1);
+                N2 = __builtin_fmaf(w3.w, aT, N2);
                 m_init = T > 0.5f ? t : m_init;
+                const int g = i * kTilePixels + j;
+                if (g < kResident) {
+                    if ((g >> 5) != mask_w) {
+                        my_mask[mask_w] = mask_cur;
+                        mask_cur = 0u;
+                        mask_w = g >> 5;
+                    }
+                    mask_cur |= 1u << (g & 31);
+                }
             }
             T = test_T;
             last = contributor;
         }
     }
+
+    if constexpr (GEOM) my_mask[mask_w] = mask_cur;
 
     // block max of last contributor (cub BlockReduce in the reference)
     const uint32_t wmax = wave_max_u(last);
@@ -199,10 +262,11 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             stage(0);
             __syncthreads();
         }
-#pragma unroll 1
-        for (int it = 0; it < kSplitIterations; it++) {
-            const bool first = it == 0;
-            if (first) {
+        // one bisection pass; FIRST evaluates all 9 samples, later passes
+        // reuse the bracketing ends (render_forward.cu:560-645)
+        auto pass = [&](auto first_c) {
+            constexpr bool FIRST = decltype(first_c)::value;
+            if (FIRST) {
 #pragma unroll
                 for (int s = 0; s <= kSplit; s++) Tp[s] = 1.f;
             } else {
@@ -210,49 +274,68 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 for (int s = 1; s < kSplit; s++) Tp[s] = 1.f;
             }
             const float interval = (dmax - dmin) * (1.f / (float)kSplit);
-            bool bdone = !in_range;
-            uint32_t c = 0;
-            for (int ch = 0; ch < chunks; ch++) {
-                if (!resident) {
-                    __syncthreads();
-                    stage(ch * chunk);
-                    __syncthreads();
-                }
-                const int n = min(chunk, (int)max_contrib - ch * chunk);
-                for (int j = 0; !bdone && j < n; j++) {
-                    c++;
-                    bdone = c >= last;
+            float ts[kSplit + 1];
+#pragma unroll
+            for (int s = 0; s <= kSplit; s++) ts[s] = __builtin_fmaf(interval, (float)s, dmin);
+            if (resident) {
+                // per-lane walk over the blended contributors, increasing index
+                // (same multiplication order as the reference's c = 1..last loop)
+                const int nwords = in_range ? (int)((last + 31) >> 5) : 0;
+                int w = 0;
+                uint32_t bits = nwords ? my_mask[0] : 0u;
+                while (true) {
+                    while (bits == 0u && w + 1 < nwords) bits = my_mask[++w];
+                    if (bits == 0u) break;
+                    const int j = (w << 5) + __builtin_ctz(bits);
+                    bits &= bits - 1u;
                     if constexpr (STATS) {
                         const unsigned long long m = __ballot(1);
-                        if ((tid & 63) == __builtin_ctzll(m)) st[0] += 1;
+                        if ((tid & 63) == __builtin_ctzll(m)) {
+                            st[0] += 1;
+                            st[1] += __popcll(m);
+                        }
                     }
                     const float4 w0 = c_w0[j];
                     const float dx = w0.x - pixx, dy = w0.y - pixy;
                     const float4 w1 = c_w1[j];
-                    const float power = -0.5f * (w0.z * dx * dx + w1.x * dy * dy) - w0.w * dx * dy;
-                    if (power > 0.0f) continue;
+                    const float power = splat_power(w0, w1, dx, dy);
                     const float alpha = fminf(0.99f, w1.y * __expf(power));
-                    if (alpha < 1.0f / 255.0f) continue;
                     const float4 w2 = c_w2[j];
-                    const float t_peak = w1.z * dx + w1.w * dy + w2.x;
-                    if constexpr (STATS) {
-                        const int START = first ? 0 : 1, END = first ? kSplit + 1 : kSplit;
-                        const float d_lo = ((dmin + interval * START) - t_peak) * w2.y;
-                        const float d_hi = ((dmin + interval * (END - 1)) - t_peak) * w2.y;
-                        const bool full = !(w2.y > 0.f && (d_lo > 7.f || d_hi < -7.f));
-                        const unsigned long long m = __ballot(1);
-                        const unsigned long long f = __ballot(full);
-                        if ((tid & 63) == __builtin_ctzll(m)) {
-                            st[1] += __popcll(m);
-                            st[2] += f != 0ull;
-                            st[3] += __popcll(f);
+                    const float t_peak = splat_tpeak(w1, w2, dx, dy);
+                    bisect_step<FIRST, SKIP>(Tp, ts, alpha, t_peak, w2.y, rsq1);
+                }
+            } else {
+                bool bdone = !in_range;
+                uint32_t c = 0;
+                for (int ch = 0; ch < chunks; ch++) {
+                    __syncthreads();
+                    stage(ch * chunk);
+                    __syncthreads();
+                    const int n = min(chunk, (int)max_contrib - ch * chunk);
+                    for (int j = 0; !bdone && j < n; j++) {
+                        c++;
+                        bdone = c >= last;
+                        const float4 w0 = c_w0[j];
+                        const float dx = w0.x - pixx, dy = w0.y - pixy;
+                        const float4 w1 = c_w1[j];
+                        const float power = splat_power(w0, w1, dx, dy);
+                        if (power > 0.0f) continue;
+                        const float alpha = fminf(0.99f, w1.y * __expf(power));
+                        if (alpha < 1.0f / 255.0f) continue;
+                        const float4 w2 = c_w2[j];
+                        const float t_peak = splat_tpeak(w1, w2, dx, dy);
+                        if constexpr (STATS) {
+                            const unsigned long long m = __ballot(1);
+                            if ((tid & 63) == __builtin_ctzll(m)) {
+                                st[2] += 1;
+                                st[3] += __popcll(m);
+                            }
                         }
+                        bisect_step<FIRST, SKIP>(Tp, ts, alpha, t_peak, w2.y, rsq1);
                     }
-                    if (first) bisect_step<true, SKIP>(Tp, dmin, interval, alpha, t_peak, w2.y, rsq1);
-                    else bisect_step<false, SKIP>(Tp, dmin, interval, alpha, t_peak, w2.y, rsq1);
                 }
             }
-            if (first) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
+            if (FIRST) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
             int start_id = 0;
 #pragma unroll
             for (int p = 1; p < kSplit; p++) start_id = Tp[p] >= 0.5f ? p : start_id;
@@ -263,11 +346,14 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 lo = start_id == p ? Tp[p] : lo;
                 hi = start_id == p ? Tp[p + 1] : hi;
             }
-            dmax = dmin + (start_id + 1) * interval;
-            dmin = dmin + (start_id + 0) * interval;
+            dmax = __builtin_fmaf((float)(start_id + 1), interval, dmin);
+            dmin = __builtin_fmaf((float)start_id, interval, dmin);
             Tp[0] = lo;
             Tp[kSplit] = hi;
-        }
+        };
+        pass(std::true_type{});
+#pragma unroll 1
+        for (int it = 1; it < kSplitIterations; it++) pass(std::false_type{});
         if constexpr (STATS) {
             for (int q = 0; q < 4; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
@@ -275,16 +361,16 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
         w_max = fminf(fmaxf(w_max, 0.f), 1.f);  // __saturatef (NaN -> 0)
         const float w_min = 1.f - w_max;
-        mDepth = in_range ? w_max * dmax + w_min * dmin : 0.f;
+        mDepth = in_range ? __builtin_fmaf(w_max, dmax, w_min * dmin) : 0.f;
     }
 
     if (inside) {
         const int HW = a.H * a.W;
         const int pix = a.W * py + px;
         a.n_contrib[pix] = last;
-        a.out_color[pix] = C0 + T * a.bg[0];
-        a.out_color[HW + pix] = C1 + T * a.bg[1];
-        a.out_color[2 * HW + pix] = C2 + T * a.bg[2];
+        a.out_color[pix] = __builtin_fmaf(T, a.bg[0], C0);
+        a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], C1);
+        a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2);
         a.out_alpha[pix] = 1.f - T;
         if constexpr (GEOM) {
             const float pnx = (pixx - (float)(a.W - 1) / 2.f) / a.focal_x;
