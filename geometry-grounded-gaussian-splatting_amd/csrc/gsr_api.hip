@@ -50,21 +50,27 @@ size_t carve_geom(void* base, int P, GeomState& g) {
     g.splats = c.take<Splat>(P);
     g.depths = c.take<float>(P);
     g.tiles_touched = c.take<uint32_t>(P);
+    g.order = c.take<uint32_t>(P);
+    g.depth_keys_sorted = c.take<uint32_t>(P);
+    g.counts = c.take<uint32_t>(P);
     g.offsets = c.take<uint32_t>(P);
     g.radii = c.take<int>(P);
     g.clamped = c.take<uint8_t>(P);
     g.scan_tmp_bytes = scan_temp_bytes(P);
     g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
+    g.dsort_tmp_bytes = depth_sort_temp_bytes(P);
+    g.dsort_tmp = c.take<char>(g.dsort_tmp_bytes);
     return c.off + 256;
 }
 
-size_t carve_binning(void* base, int K, int end_bit, BinningState& b) {
+size_t carve_binning(void* base, int K, int tile_bits, BinningState& b) {
     Carver c(base);
-    b.keys_unsorted = c.take<uint64_t>(K);
-    b.keys = c.take<uint64_t>(K);
+    b.key_bytes = tile_key_bytes(tile_bits);
+    b.keys_unsorted = c.take<char>((size_t)K * b.key_bytes);
+    b.keys = c.take<char>((size_t)K * b.key_bytes);
     b.values_unsorted = c.take<uint32_t>(K);
     b.point_list = c.take<uint32_t>(K);
-    b.sort_tmp_bytes = sort_temp_bytes(K, end_bit);
+    b.sort_tmp_bytes = sort_temp_bytes(K, tile_bits);
     b.sort_tmp = c.take<char>(b.sort_tmp_bytes);
     return c.off + 256;
 }
@@ -221,6 +227,26 @@ int gsr_debug_render_stats(unsigned long long* out8, int reset) {
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "render stats", e);
 }
 
+int gsr_debug_binning(const void* binning_buffer, const void* tile_buffer, int R, int width, int height,
+                      uint32_t* point_list_out, uint32_t* ranges_out, void* stream_ptr) {
+    if (!binning_buffer || !tile_buffer || R < 0 || width <= 0 || height <= 0)
+        return fail(GSR_ERR_ARGS, "invalid arguments");
+    const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
+    const int tiles = (int)(gx * gy);
+    BinningState bs;
+    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, (int)higher_msb((uint32_t)tiles), bs);
+    TileState ts;
+    carve_tiles(aligned_base(const_cast<void*>(tile_buffer)), tiles, ts);
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    hipError_t e = hipSuccess;
+    if (point_list_out && R > 0)
+        e = hipMemcpyAsync(point_list_out, bs.point_list, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess && ranges_out)
+        e = hipMemcpyAsync(ranges_out, ts.ranges, sizeof(uint2) * tiles, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "debug binning", e);
+}
+
 int gsr_set_option(int opt, int value) {
     if (opt < 0 || opt >= gsr::kNumOptions) return fail(GSR_ERR_ARGS, "unknown option");
     gsr::g_options[opt] = value;
@@ -228,7 +254,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 2; }
+int gsr_abi_version(void) { return 3; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -261,7 +287,7 @@ int gsr_timing_collect(double* ms, int* launches) {
 
 const char* gsr_stage_name(int stage) {
     static const char* names[GSR_NUM_STAGES] = {"preprocess", "scan", "emit_keys", "sort", "tile_ranges",
-                                                 "render_fwd", "bwd_clear", "render_bwd", "preprocess_bwd"};
+                                                 "render_fwd", "bwd_clear", "render_bwd", "preprocess_bwd", "depth_order"};
     return (stage >= 0 && stage < GSR_NUM_STAGES) ? names[stage] : "?";
 }
 
@@ -309,14 +335,15 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
         if (e == hipSuccess) e = hipMemsetAsync(ts.max_contrib, 0, sizeof(uint32_t) * tiles, stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "memset", e);
         BinningState bs;
-        void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, 0, 32, bs));
+        void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, 0, 16, bs));
         if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-        carve_binning(aligned_base(bbuf), 0, 32, bs);
+        carve_binning(aligned_base(bbuf), 0, 16, bs);
         GSR_TRY(launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
         return GSR_OK;
     }
 
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, radii, stream), "preprocess");
+    GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_order(gs, P, stream), "depth order");
     GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
     uint32_t K = 0;
     GSR_TRY(hipMemcpyAsync(&K, gs.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
@@ -324,13 +351,13 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
     }
-    const int end_bit = 32 + (int)higher_msb((uint32_t)tiles);
+    const int tile_bits = (int)higher_msb((uint32_t)tiles);
     BinningState bs;
-    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, end_bit, bs));
+    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, tile_bits, bs));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-    carve_binning(aligned_base(bbuf), (int)K, end_bit, bs);
+    carve_binning(aligned_base(bbuf), (int)K, tile_bits, bs);
     GSR_STAGE(GSR_STAGE_EMIT_KEYS, launch_emit_keys(p, gs, radii, bs, stream), "emit keys");
-    GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K, end_bit, stream), "sort");
+    GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K, tile_bits, stream), "sort");
     GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K, ts, tiles, stream), "tile ranges");
     GSR_STAGE(GSR_STAGE_RENDER_FWD,
               launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
@@ -392,11 +419,11 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
     b.dL_dsg_color = dL_dsg_color;
 
     const int tiles = (int)(b.f.grid_x * b.f.grid_y);
-    const int end_bit = 32 + (int)higher_msb((uint32_t)tiles);
+    const int tile_bits = (int)higher_msb((uint32_t)tiles);
     GeomState gs;
     carve_geom(aligned_base(const_cast<void*>(geom_buffer)), P, gs);
     BinningState bs;
-    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, end_bit, bs);
+    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, tile_bits, bs);
     ImageState is;
     carve_image(aligned_base(const_cast<void*>(image_buffer)), width * height, is);
     TileState ts;

@@ -65,16 +65,24 @@ struct GeomState {
     Splat* splats;
     float* depths;
     uint32_t* tiles_touched;
-    uint32_t* offsets;  // inclusive scan of tiles_touched
-    int* radii;         // internal copy when the caller passes radii == NULL
-    uint8_t* clamped;   // bit c set: colour channel c was clamped at 0
+    uint32_t* order;              // Gaussian indices in (depth bits, index) order
+    uint32_t* depth_keys_sorted;  // sorted depth bit patterns (sort output, unused after)
+    uint32_t* counts;             // tiles_touched in depth order
+    uint32_t* offsets;            // inclusive scan of counts
+    int* radii;                   // internal copy when the caller passes radii == NULL
+    uint8_t* clamped;             // bit c set: colour channel c was clamped at 0
     void* scan_tmp;
     size_t scan_tmp_bytes;
+    void* dsort_tmp;
+    size_t dsort_tmp_bytes;
 };
 // ---- per-instance state (replaces BinningState) ----
+// tile ids as 16-bit sort keys when the grid allows (<= 65536 tiles)
+inline int tile_key_bytes(int tile_bits) { return tile_bits <= 16 ? 2 : 4; }
 struct BinningState {
-    uint64_t* keys_unsorted;
-    uint64_t* keys;
+    int key_bytes;        // 2 or 4 (tile_key_bytes)
+    void* keys_unsorted;  // tile id per instance, emission (depth) order
+    void* keys;           // tile ids sorted
     uint32_t* values_unsorted;
     uint32_t* point_list;
     void* sort_tmp;

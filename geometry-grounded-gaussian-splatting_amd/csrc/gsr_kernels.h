@@ -63,11 +63,13 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
 
 // binning.hip
 size_t scan_temp_bytes(int P);
-size_t sort_temp_bytes(int K, int end_bit);
+size_t depth_sort_temp_bytes(int P);
+size_t sort_temp_bytes(int K, int tile_bits);
+hipError_t launch_depth_order(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_scan(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_emit_keys(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
                             hipStream_t stream);
-hipError_t launch_sort(const BinningState& bs, int K, int end_bit, hipStream_t stream);
+hipError_t launch_sort(const BinningState& bs, int K, int tile_bits, hipStream_t stream);
 hipError_t launch_tile_ranges(const BinningState& bs, int K, const TileState& ts, int tiles, hipStream_t stream);
 
 // render_fwd.hip

@@ -49,6 +49,7 @@ def _load():
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     L.gsr_set_option.argtypes = [i, i]
+    L.gsr_debug_binning.argtypes = [vp, vp, i, i, i, vp, vp, vp]
     L.gsr_debug_render_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i]
     L.gsr_timing_enable.argtypes = [i]
     L.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i)]
@@ -65,7 +66,7 @@ def loaded_library_path() -> str:
     return LIB_PATH
 
 
-NUM_STAGES = 9
+NUM_STAGES = 10
 OPT_BISECT_SKIP = 0
 OPT_RENDER_STATS = 1
 
@@ -75,6 +76,22 @@ def debug_render_stats(reset: bool = True) -> list:
     out = (ctypes.c_ulonglong * 8)()
     _check(_load().gsr_debug_render_stats(out, int(bool(reset))))
     return list(out)
+
+
+def debug_binning(binningBuffer, tileBuffer, R: int, image_height: int, image_width: int):
+    """(point_list [R] uint32, ranges [tiles, 2] uint32) of a forward's buffers
+    (gsr_debug_binning), as numpy arrays."""
+    import numpy as np
+
+    tiles = ((image_width + 15) // 16) * ((image_height + 15) // 16)
+    plist = np.zeros(max(R, 0), np.uint32)
+    ranges = np.zeros((tiles, 2), np.uint32)
+    stream = torch.cuda.current_stream(binningBuffer.device).cuda_stream
+    _check(_load().gsr_debug_binning(ctypes.c_void_p(binningBuffer.data_ptr()),
+                                     ctypes.c_void_p(tileBuffer.data_ptr()), int(R), int(image_width),
+                                     int(image_height), plist.ctypes.data_as(ctypes.c_void_p),
+                                     ranges.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream)))
+    return plist, ranges
 
 
 def set_option(opt: int, value: int) -> None:

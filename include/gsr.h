@@ -117,6 +117,7 @@ enum gsr_stage {
     GSR_STAGE_BWD_CLEAR,
     GSR_STAGE_RENDER_BWD,
     GSR_STAGE_PREPROCESS_BWD,
+    GSR_STAGE_DEPTH_ORDER, /* stable depth sort of the Gaussians feeding the tile sort (binning.hip) */
     GSR_NUM_STAGES
 };
 int gsr_timing_enable(int on);
@@ -134,10 +135,19 @@ int gsr_set_option(int opt, int value);
 /* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (8 values, see render_fwd.hip). */
 int gsr_debug_render_stats(unsigned long long* out8, int reset);
 
+/*
+ * Introspection of a forward's opaque buffers (test hook, no reference
+ * equivalent): copies the per-tile depth-ordered Gaussian list (R entries,
+ * R = num_rendered) and the tile ranges (2 x tiles uint32, tiles =
+ * ceil(W/16) * ceil(H/16)) to host memory; synchronises `stream`.
+ */
+int gsr_debug_binning(const void* binning_buffer, const void* tile_buffer, int R, int width, int height,
+                      uint32_t* point_list_out, uint32_t* ranges_out, void* stream);
+
 /* Human-readable message for the last non-OK status on this thread. */
 const char* gsr_last_error(void);
 
-/* ABI version of this header (bumped on any signature change). */
+/* ABI version of this header (bumped on any signature or enum change). */
 int gsr_abi_version(void);
 
 #ifdef __cplusplus

@@ -46,6 +46,17 @@ def _fwd_args(c, colors_precomp=None, cov3D=None, scale_modifier=1.0):
     return a
 
 
+def _check_binning(out, o, H, W):
+    """Per-tile Gaussian lists and tile ranges equal the oracle's (the
+    reference's stable (tile, depth) sort order), element for element."""
+    from diff_gaussian_rasterization import _C
+
+    plist, ranges = _C.debug_binning(out[7], out[9], out[0], H, W)
+    ob = o["state"].binning()
+    assert np.array_equal(plist, ob["point_list"])
+    assert np.array_equal(ranges, o["state"].tile_state()["ranges"])
+
+
 def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True):
     from diff_gaussian_rasterization import _C
 
@@ -56,6 +67,7 @@ def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True)
     K, color, alpha, normal, mdepth, radii = out[:6]
     assert K == o["num_rendered"]
     assert np.array_equal(radii.cpu().numpy(), o["radii"])
+    _check_binning(out, o, c["H"], c["W"])
     geom = c["require_depth"]
     for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
         if not geom and name in ("normal", "mdepth"):
@@ -204,7 +216,7 @@ def test_timing_api():
     _C.rasterize_gaussians(*ga)
     _C.timing_enable(False)
     st = _C.timing_collect()
-    for k in ("preprocess", "scan", "emit_keys", "sort", "tile_ranges", "render_fwd"):
+    for k in ("preprocess", "depth_order", "scan", "emit_keys", "sort", "tile_ranges", "render_fwd"):
         assert st[k][1] == 1 and st[k][0] > 0, k
 
 
@@ -240,6 +252,7 @@ def test_c3_full_size_properties(c3):
         O.set_tile_stride(1)
     assert K == o["num_rendered"]
     assert np.array_equal(radii.cpu().numpy(), o["radii"])
+    _check_binning(out1, o, 1080, 1920)  # binning is computed in full for every tile
     gx = (1920 + 15) // 16
     mask = np.zeros((1080, 1920), bool)
     for t in range(0, gx * ((1080 + 15) // 16), stride):

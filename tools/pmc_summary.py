@@ -37,8 +37,10 @@ def stage_of(name: str) -> str | None:
         return "render_fwd"
     if "render_bwd_kernel" in n:
         return "render_bwd"
+    if "gather_counts_kernel" in n:
+        return "depth_order"
     if "radix_sort" in n or "onesweep" in n:
-        return "sort"
+        return "sort"  # (depth sort of P and tile sort of K share rocPRIM kernels)
     if "scan" in n:
         return "scan"
     return None
