@@ -124,13 +124,44 @@ __device__ inline float wave_sum_f(float v) {
     return v;
 }
 
+// DPP lane moves (VOP_DPP, folded into the consuming v_add by the compiler):
+// quad_perm xor 1 / xor 2 within quads, row_half_mirror (l ^ 7 within 8
+// lanes) and row_mirror (l ^ 15 within a 16-lane row).  No LDS traffic,
+// unlike __shfl_xor (ds_bpermute_b32).
+enum : int { kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppRowMirror = 0x140, kDppRowHalfMirror = 0x141 };
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// a_l + a_{l ^ 16} and a_l + a_{l ^ 32} through gfx950's permlane swaps
+__device__ __forceinline__ float add_lane_xor16(float a) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float add_lane_xor32(float a) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Sum over the 64 lanes of a wave, result in every lane; VALU only.  Within
+// a 16-lane row the partners are l^15, l^7 (mirrors: each stage pairs the two
+// halves of a group bijectively, so each lane is counted once), then l^2, l^1.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v += dpp_mov<kDppRowMirror>(v);
+    v += dpp_mov<kDppRowHalfMirror>(v);
+    v += dpp_mov<kDppXor2>(v);
+    v += dpp_mov<kDppXor1>(v);
+    return add_lane_xor32(add_lane_xor16(v));
+}
+
 // Transposed butterfly reduction of 16 per-lane values over the 64 lanes of
 // a wave.  Stage 1/2 use gfx950's v_permlane32_swap / v_permlane16_swap (one
 // swap moves half of a pair across the 32- or 16-lane boundary, so each stage
-// halves the number of live values); stages 3/4 use xor shuffles with a
-// keep/send select; the last two stages are plain xor adds.  On return lane
-// l (l % 4 == 0) holds the full wave sum of field (l >> 2); 17 cross-lane ops
-// instead of 16 x 6 for independent reductions.
+// halves the number of live values); stages 3/4 pair the halves of 16- and
+// 8-lane groups with DPP mirrors (keep/send select: field bit 1 <- lane bit 3,
+// field bit 0 <- lane bit 2); the last two stages are DPP quad adds.  On
+// return lane l (all four lanes of each quad) holds the full wave sum of field
+// (l >> 2); every cross-lane move is a VALU op.
 __device__ inline float wave_transpose_reduce16(const float (&v)[16]) {
     const int lane = threadIdx.x & 63;
     float a[8];
@@ -146,21 +177,22 @@ __device__ inline float wave_transpose_reduce16(const float (&v)[16]) {
         auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[i]), __float_as_uint(a[i + 4]), false, false);
         b[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
-    // field bit 2 <- lane bit 4
+    // field bit 1 <- lane bit 3 (partner l ^ 15: opposite bit 3, same row)
     const bool hi8 = (lane & 8) != 0;
     float c[2];
 #pragma unroll
     for (int i = 0; i < 2; i++) {
-        float keep = hi8 ? b[i + 2] : b[i];
-        float send = hi8 ? b[i] : b[i + 2];
-        c[i] = keep + __shfl_xor(send, 8, 64);
+        const float keep = hi8 ? b[i + 2] : b[i];
+        const float send = hi8 ? b[i] : b[i + 2];
+        c[i] = keep + dpp_mov<kDppRowMirror>(send);
     }
+    // field bit 0 <- lane bit 2 (partner l ^ 7: opposite bit 2, same 8 lanes)
     const bool hi4 = (lane & 4) != 0;
-    float keep = hi4 ? c[1] : c[0];
-    float send = hi4 ? c[0] : c[1];
-    float d = keep + __shfl_xor(send, 4, 64);
-    d += __shfl_xor(d, 2, 64);
-    d += __shfl_xor(d, 1, 64);
+    const float keep = hi4 ? c[1] : c[0];
+    const float send = hi4 ? c[0] : c[1];
+    float d = keep + dpp_mov<kDppRowHalfMirror>(send);
+    d += dpp_mov<kDppXor2>(d);
+    d += dpp_mov<kDppXor1>(d);
     return d;
 }
 

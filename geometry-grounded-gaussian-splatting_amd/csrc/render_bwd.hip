@@ -6,9 +6,9 @@
 // Same tile/workgroup geometry as render_fwd.hip.  Per (pixel, Gaussian) the
 // kernel recomputes alpha and produces up to 17 gradient terms; they are
 // summed over the 64 pixels of a wave with one transposed butterfly
-// (wave_transpose_reduce16: v_permlane32_swap / v_permlane16_swap + xor
-// shuffles), after which lanes 0, 4, ..., 60 hold the 16 field totals and
-// issue ONE 16-lane global_atomic_add_f32 that covers the Gaussian's 64-B
+// (wave_transpose_reduce16: v_permlane32_swap / v_permlane16_swap, then DPP
+// mirrors and quad perms, all VALU), after which lanes 0, 4, ..., 60 hold the
+// 16 field totals and issue ONE 16-lane global_atomic_add_f32 that covers the Gaussian's 64-B
 // accumulator record (a single 64-B atomic request), plus one lane for the
 // |dmean2D| channel.  The reference (32-lane cg::reduce per field, then 17
 // scalar atomics from lane 0) issues 17 single-lane atomic requests per warp
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
                 f[kAccConic + 3] = G * dL_dopa;
             }
             const float red = wave_transpose_reduce16(f);
-            const float abs_red = wave_sum_f(fabs_sum);
+            const float abs_red = wave_sum_dpp(fabs_sum);
             const uint32_t g = s_id[j];
             if ((lane & 3) == 0) {
                 const int field = lane >> 2;

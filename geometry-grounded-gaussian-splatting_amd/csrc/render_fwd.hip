@@ -53,29 +53,32 @@ struct RenderFwdArgs {
     float* out_alpha;
     float* out_normal;
     float* out_mdepth;
-    float one;  // 1.0f, passed at run time so rsq(1.0) is evaluated by the hardware
 };
 
 // One contributor's factor on the bisection samples (render_forward.cu:610-621):
 //   T_p[s] *= (ts > t_peak ? 1 - a : 1 - a g) * rsqrt(1 - a g),  g = exp(-delta^2 / 2)
-// Evaluated two samples at a time with packed fp32 (v_pk_{add,mul,fma}_f32).
-// Rewrites that keep every rounding of the scalar form:
+// The product over contributors is kept as two products,
+//   A[s] = prod (ts > t_peak ? 1 - a : 1 - a g),   B[s] = prod (1 - a g),
+// and T_p[s] = A[s] * rsqrt(B[s]) once per pass: one rsqrt per sample and
+// pass instead of one per contributor (the reassociation moves T_p by a few
+// ulp; both products stay >= the pixel's final transmittance >= 1e-4, so
+// nothing underflows).  Samples are evaluated two at a time with packed
+// fp32 (v_pk_{add,mul,fma}_f32), and
 //  * exp(-delta^2/2) = exp2(round(delta*delta) * (-0.5 * log2e)): __expf is
 //    v_exp_f32(x * log2e) and scaling by -0.5 is exact, so the product folds
 //    into one constant;
 //  * a non-ball splat (rsigma <= 0, g = 0 in the reference) runs with
 //    alpha_g = 0 and rsigma = 0: delta = 0, g = 1, 1 - 0*g = 1 exactly.
 // Exact shortcut (SKIP): when every sample of the window has |delta| > 7,
-// a*g < e^-24.5 < 2^-25, so 1 - a*g rounds to exactly 1.0f and the factor is
-// exactly (1 - a) * rsq(1) in front of the window or rsq(1) behind it (the
-// samples are monotone in s, so the two window ends decide).  rsq1 is the
-// hardware's rsq(1.0) so the shortcut is bit-identical to the full path.
+// a*g < e^-24.5 < 2^-25, so 1 - a*g rounds to exactly 1.0f: B is unchanged
+// and A gains (1 - a) in front of the window, nothing behind it (the samples
+// are monotone in s, so the two window ends decide).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float kHalfNegLog2e = -0.5f * 1.44269502162933349609375f;  // -0.5 * (float)log2(e), exact
 
 template <bool FIRST, bool SKIP>
-__device__ __forceinline__ void bisect_step(float (&Tp)[kSplit + 1], const float (&ts)[kSplit + 1], float alpha,
-                                            float t_peak, float rsig, float rsq1) {
+__device__ __forceinline__ void bisect_step(float (&A)[kSplit + 1], float (&B)[kSplit + 1],
+                                            const float (&ts)[kSplit + 1], float alpha, float t_peak, float rsig) {
     constexpr int START = FIRST ? 0 : 1;
     constexpr int END = FIRST ? kSplit + 1 : kSplit;
     const bool ball = rsig > 0.f;
@@ -84,16 +87,11 @@ __device__ __forceinline__ void bisect_step(float (&Tp)[kSplit + 1], const float
         const float d_lo = (ts[START] - t_peak) * rsig;
         const float d_hi = (ts[END - 1] - t_peak) * rsig;
         if (ball && d_lo > 7.f) {
-            const float f = om * rsq1;
 #pragma unroll
-            for (int s = START; s < END; s++) Tp[s] *= f;
+            for (int s = START; s < END; s++) A[s] *= om;
             return;
         }
-        if (ball && d_hi < -7.f) {
-#pragma unroll
-            for (int s = START; s < END; s++) Tp[s] *= rsq1;
-            return;
-        }
+        if (ball && d_hi < -7.f) return;
     }
     const float ag = ball ? alpha : 0.f;
     const float rg = ball ? rsig : 0.f;
@@ -106,19 +104,22 @@ __device__ __forceinline__ void bisect_step(float (&Tp)[kSplit + 1], const float
         const f32x2 e = (delta * delta) * c2;
         const f32x2 g = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
         const f32x2 omg = __builtin_elementwise_fma(-ag2, g, one2);
-        const f32x2 rv = {__builtin_amdgcn_rsqf(omg.x), __builtin_amdgcn_rsqf(omg.y)};
         const f32x2 sel = {t.x > t_peak ? om : omg.x, t.y > t_peak ? om : omg.y};
-        f32x2 T2 = {Tp[s], Tp[s + 1]};
-        T2 *= sel * rv;
-        Tp[s] = T2.x;
-        Tp[s + 1] = T2.y;
+        f32x2 A2 = {A[s], A[s + 1]}, B2 = {B[s], B[s + 1]};
+        A2 *= sel;
+        B2 *= omg;
+        A[s] = A2.x;
+        A[s + 1] = A2.y;
+        B[s] = B2.x;
+        B[s + 1] = B2.y;
     }
     if constexpr (((END - START) & 1) != 0) {
         constexpr int s = END - 1;
         const float delta = (ts[s] - t_peak) * rg;
         const float g = __builtin_amdgcn_exp2f((delta * delta) * kHalfNegLog2e);
         const float omg = __builtin_fmaf(-ag, g, 1.f);
-        Tp[s] *= (ts[s] > t_peak ? om : omg) * __builtin_amdgcn_rsqf(omg);
+        A[s] *= ts[s] > t_peak ? om : omg;
+        B[s] *= omg;
     }
 }
 
@@ -238,8 +239,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     float mDepth = 0.f;
     if constexpr (GEOM) {
         unsigned long long st[4] = {0, 0, 0, 0};
-        float Tp[kSplit + 1];
-        const float rsq1 = __builtin_amdgcn_rsqf(a.one);  // hardware rsq(1.0) (kept opaque to the compiler)
+        float Tp[kSplit + 1], A[kSplit + 1], B[kSplit + 1];
         float dmin = fmaxf(m_init - kSampleRange, 0.f);
         float dmax = fmaxf(m_init + kSampleRange, 0.f);
         bool in_range = T <= kMinTransmittance;
@@ -266,13 +266,10 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         // reuse the bracketing ends (render_forward.cu:560-645)
         auto pass = [&](auto first_c) {
             constexpr bool FIRST = decltype(first_c)::value;
-            if (FIRST) {
+            constexpr int START = FIRST ? 0 : 1;
+            constexpr int END = FIRST ? kSplit + 1 : kSplit;
 #pragma unroll
-                for (int s = 0; s <= kSplit; s++) Tp[s] = 1.f;
-            } else {
-#pragma unroll
-                for (int s = 1; s < kSplit; s++) Tp[s] = 1.f;
-            }
+            for (int s = START; s < END; s++) A[s] = B[s] = 1.f;
             const float interval = (dmax - dmin) * (1.f / (float)kSplit);
             float ts[kSplit + 1];
 #pragma unroll
@@ -302,7 +299,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                     const float alpha = fminf(0.99f, w1.y * __expf(power));
                     const float4 w2 = c_w2[j];
                     const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                    bisect_step<FIRST, SKIP>(Tp, ts, alpha, t_peak, w2.y, rsq1);
+                    bisect_step<FIRST, SKIP>(A, B, ts, alpha, t_peak, w2.y);
                 }
             } else {
                 bool bdone = !in_range;
@@ -331,10 +328,12 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                                 st[3] += __popcll(m);
                             }
                         }
-                        bisect_step<FIRST, SKIP>(Tp, ts, alpha, t_peak, w2.y, rsq1);
+                        bisect_step<FIRST, SKIP>(A, B, ts, alpha, t_peak, w2.y);
                     }
                 }
             }
+#pragma unroll
+            for (int s = START; s < END; s++) Tp[s] = A[s] * __builtin_amdgcn_rsqf(B[s]);
             if (FIRST) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
             int start_id = 0;
 #pragma unroll
@@ -411,7 +410,6 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.out_alpha = out_alpha;
     a.out_normal = out_normal;
     a.out_mdepth = out_mdepth;
-    a.one = 1.0f;
     if (a.num_tiles == 0) return hipSuccess;
     if (p.require_depth) {
         if (option(kOptRenderStats))

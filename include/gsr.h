@@ -127,8 +127,9 @@ const char* gsr_stage_name(int stage);
 /*
  * Process-wide switches selecting A/B variants of a kernel, for measuring one
  * against the other in the same process (all variants give bit-identical
- * results).  GSR_OPT_BISECT_SKIP (default 1): exact shortcut for bisection
- * samples far from a Gaussian's ray peak (render_fwd.hip).
+ * results).  GSR_OPT_BISECT_SKIP (default 0): exact shortcut for bisection
+ * samples far from a Gaussian's ray peak (render_fwd.hip; slower on the
+ * fog-like benchmark scene, where most samples are near a peak).
  */
 enum gsr_option { GSR_OPT_BISECT_SKIP = 0, GSR_OPT_RENDER_STATS = 1 };
 int gsr_set_option(int opt, int value);

@@ -277,7 +277,7 @@ def test_c3_bisection_shortcut_is_bit_exact(c3):
         _C.set_option(_C.OPT_BISECT_SKIP, 1)
         got = _C.rasterize_gaussians(*ga)
     finally:
-        _C.set_option(_C.OPT_BISECT_SKIP, 1)
+        _C.set_option(_C.OPT_BISECT_SKIP, 0)
     for k in range(1, 6):
         assert torch.equal(ref[k], got[k]), k
 

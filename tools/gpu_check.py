@@ -61,11 +61,17 @@ if __name__ == "__main__":
     print("stats per forward (4 calls):", [v / 4 for v in st[:4]],
           "lanes/step per-lane walk=%.1f uniform walk=%.1f" % (st[1] / max(st[0], 1), st[3] / max(st[2], 1)))
     run(20000, 320, 240)
-    for opt in (0, 1, 0, 1):
+    for opt in (0, 1):
         _C.set_option(_C.OPT_BISECT_SKIP, opt)
         print("bisect skip", opt)
         bench(require_depth=True)
+        _C.timing_enable(True)
+        bench(require_depth=True, iters=5)
+        _C.timing_enable(False)
+        print({k: round(v[0] / max(v[1], 1), 3) for k, v in _C.timing_collect().items()})
+    _C.set_option(_C.OPT_BISECT_SKIP, 0)
     bench(require_depth=False)
     _C.timing_enable(True)
-    bench(require_depth=True, iters=5)
+    bench(require_depth=False, iters=5)
+    _C.timing_enable(False)
     print({k: round(v[0] / max(v[1], 1), 3) for k, v in _C.timing_collect().items()})
