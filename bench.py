@@ -61,20 +61,23 @@ def parse():
     return ap.parse_args()
 
 
-def stage_bytes(P, K, HW, shm, sgm, geom):
+def stage_bytes(P, K, HW, shm, sgm, geom, tiles):
     """Algorithmic (compulsory) HBM bytes per launch of each stage, from the
-    per-unit figures of SURVEY.md §8(d)."""
+    per-unit figures of SURVEY.md §8(d), with the binning terms of this
+    build's pipeline (depth order of P, 16-bit tile keys)."""
     Bp = 44 + 12 * shm + 28 * sgm
     G = 64 if geom else 36
     Opx = 36 if geom else 20
     Ipx = 56 if geom else 24
     A = 68 if geom else 40
+    kb = 2 if tiles <= 65536 else 4
     return {
         "preprocess": P * (Bp + 80),
+        "depth_order": P * 28,  # depth bits in, (key, index) out, tiles_touched gathered into depth order
         "scan": P * 8,
-        "emit_keys": P * 20 + K * 12,
-        "sort": K * 24,
-        "tile_ranges": K * 8,
+        "emit_keys": P * 28 + K * (kb + 4),
+        "sort": K * (kb + 4) * 2,
+        "tile_ranges": K * kb + tiles * 8,
         "render_fwd": K * (4 + G) + HW * Opx,
         "bwd_clear": P * A,
         "render_bwd": HW * Ipx + K * (4 + G),
@@ -83,16 +86,16 @@ def stage_bytes(P, K, HW, shm, sgm, geom):
 
 
 def load_pmc_traffic(kernel_stage):
-    """HBM bytes per launch of `kernel_stage` from profiles/pmc_summary.json
-    (written by tools/profile.sh from separate rocprofv3 --pmc passes, with
-    the gfx950 FETCH_SIZE x2 correction already applied)."""
+    """(HBM bytes per launch, VALU busy fraction) of `kernel_stage` from
+    profiles/pmc_summary.json (written by tools/profile.sh from separate
+    rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2 correction applied)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d["stages"][kernel_stage]["hbm_bytes_per_launch"]
+            st = json.load(f)["stages"][kernel_stage]
+        return st["hbm_bytes_per_launch"], st.get("valu_busy")
     except Exception:  # noqa: BLE001 - absent or stale summary -> null
-        return None
+        return None, None
 
 
 def cpu_baseline(args, inputs_cpu, cam, tanx, tany, grads_cpu):
@@ -223,16 +226,17 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.steps / elapsed
     shm = (args.sh_degree + 1) ** 2
-    algo = stage_bytes(P, K, W * H, shm, args.sg_degree, geom)
+    algo = stage_bytes(P, K, W * H, shm, args.sg_degree, geom, ((W + 15) // 16) * ((H + 15) // 16))
     per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in stages.items()}
     dom = max(per_launch, key=lambda k: per_launch[k])
     achieved = algo[dom] / (per_launch[dom] * 1e-3) / 1e9
-    traffic = load_pmc_traffic(dom)
+    traffic, valu = load_pmc_traffic(dom)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(algo[dom]),
                 "avg_launch_ms": round(per_launch[dom], 4),
-                "stage_ms": {k: round(v, 4) for k, v in per_launch.items()}}
+                "stage_ms": {k: round(v, 4) for k, v in per_launch.items()},
+                "valu_busy": valu}
     total_algo = sum(algo.values())
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -36,9 +36,14 @@ size_t scan_temp_bytes(int P) {
     return bytes;
 }
 
+// rocPRIM picks a merge sort below 1M items for 32-bit keys (10 merge passes
+// at P = 1M); a merge-sort limit of 0 keeps the 4-pass onesweep radix sort.
+using DepthSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                   rocprim::default_config, 0>;
+
 size_t depth_sort_temp_bytes(int P) {
     size_t bytes = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+    (void)rocprim::radix_sort_pairs<DepthSortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                     rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)P, 0u, 32u);
     return bytes;
 }
@@ -66,7 +71,7 @@ __global__ void __launch_bounds__(256)
 hipError_t launch_depth_order(const GeomState& gs, int P, hipStream_t stream) {
     if (P == 0) return hipSuccess;
     size_t bytes = gs.dsort_tmp_bytes;
-    hipError_t e = rocprim::radix_sort_pairs(gs.dsort_tmp, bytes, reinterpret_cast<const uint32_t*>(gs.depths),
+    hipError_t e = rocprim::radix_sort_pairs<DepthSortConfig>(gs.dsort_tmp, bytes, reinterpret_cast<const uint32_t*>(gs.depths),
                                              gs.depth_keys_sorted, rocprim::counting_iterator<uint32_t>(0), gs.order,
                                              (size_t)P, 0u, 32u, stream);
     if (e != hipSuccess) return e;

@@ -37,7 +37,7 @@ namespace gsr {
 
 constexpr int kResident = 384;
 constexpr int kMaskWords = kResident / 32;
-constexpr int kMaskStride = kMaskWords + 1;  // odd row stride: conflict-free LDS rows
+constexpr int kRecSlots = 3 * kResident > 4 * kTilePixels ? 3 * kResident : 4 * kTilePixels;
 
 struct RenderFwdArgs {
     const uint2* ranges;
@@ -131,9 +131,13 @@ __device__ unsigned long long g_render_stats[8];
 template <bool GEOM, bool SKIP, bool STATS = false>
 __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 256 x 16 B = 16 KB) aliased with the
-    // bisection cache (3 x 512 x 16 B = 24 KB).
-    __shared__ float4 s_rec[3 * kResident];
-    __shared__ uint32_t s_mask[GEOM ? kTilePixels * kMaskStride : 1];  // blended contributors per pixel
+    // bisection cache (3 x 384 x 16 B = 18 KB), plus the 12 KB of masks:
+    // 30 KB per block, 5 blocks (20 waves) per CU.  (A 320-record cache
+    // reaches 6 blocks per CU but sends C3's longest tiles to the
+    // wave-uniform walk: measured slower.)
+    __shared__ float4 s_rec[kRecSlots];
+    // blended contributors per pixel, word-major (word w of lane t at w * 256 + t: conflict-free)
+    __shared__ uint32_t s_mask[GEOM ? kTilePixels * kMaskWords : 1];
     __shared__ int s_alive[2][4];
     __shared__ uint32_t s_max[4];
 
@@ -152,16 +156,15 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     float4* s_w0 = s_rec;
     float4* s_w1 = s_rec + kTilePixels;
     float4* s_w2 = s_rec + 2 * kTilePixels;
-    float4* s_w3 = s_rec + 3 * kTilePixels;  // within the 18 KB (3*384 float4 >= 4*256)
-    static_assert(3 * kResident >= 4 * kTilePixels, "composite staging must fit in the bisection cache");
+    float4* s_w3 = s_rec + 3 * kTilePixels;
 
-    // each lane owns one mask row: no barrier needed between init, writes and reads
-    uint32_t* my_mask = s_mask + (GEOM ? tid * kMaskStride : 0);
+    // each lane owns one mask column: no barrier needed between init, writes and reads
+    uint32_t* my_mask = s_mask + (GEOM ? tid : 0);
     uint32_t mask_cur = 0;
     int mask_w = 0;
     if constexpr (GEOM) {
 #pragma unroll
-        for (int q = 0; q < kMaskWords; q++) my_mask[q] = 0u;
+        for (int q = 0; q < kMaskWords; q++) my_mask[q * kTilePixels] = 0u;
     }
 
     float T = 1.0f;
@@ -216,7 +219,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 const int g = i * kTilePixels + j;
                 if (g < kResident) {
                     if ((g >> 5) != mask_w) {
-                        my_mask[mask_w] = mask_cur;
+                        my_mask[mask_w * kTilePixels] = mask_cur;
                         mask_cur = 0u;
                         mask_w = g >> 5;
                     }
@@ -228,7 +231,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         }
     }
 
-    if constexpr (GEOM) my_mask[mask_w] = mask_cur;
+    if constexpr (GEOM) my_mask[mask_w * kTilePixels] = mask_cur;
 
     // block max of last contributor (cub BlockReduce in the reference)
     const uint32_t wmax = wave_max_u(last);
@@ -281,7 +284,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 int w = 0;
                 uint32_t bits = nwords ? my_mask[0] : 0u;
                 while (true) {
-                    while (bits == 0u && w + 1 < nwords) bits = my_mask[++w];
+                    while (bits == 0u && w + 1 < nwords) bits = my_mask[++w * kTilePixels];
                     if (bits == 0u) break;
                     const int j = (w << 5) + __builtin_ctz(bits);
                     bits &= bits - 1u;

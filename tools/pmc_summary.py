@@ -39,8 +39,10 @@ def stage_of(name: str) -> str | None:
         return "render_bwd"
     if "gather_counts_kernel" in n:
         return "depth_order"
-    if "radix_sort" in n or "onesweep" in n:
-        return "sort"  # (depth sort of P and tile sort of K share rocPRIM kernels)
+    if "radix_sort" in n or "onesweep" in n or "merge_sort" in n:
+        # rocPRIM kernels are named by key/value types: the tile sort has
+        # 16-bit keys (grids <= 65536 tiles), the depth sort 32-bit keys
+        return "sort" if "unsigned short" in n else "depth_order"
     if "scan" in n:
         return "scan"
     return None
@@ -93,6 +95,14 @@ def main():
     nw = launches(write_csv, "WRITE_SIZE")
     fetch = per_stage_counter(fetch_csv, "FETCH_SIZE", nf)
     write = per_stage_counter(write_csv, "WRITE_SIZE", nw)
+    sq_csv = os.path.join(src, "sq", "run_counter_collection.csv")
+    sq = {}
+    if os.path.exists(sq_csv):
+        ns = launches(sq_csv, "GRBM_GUI_ACTIVE")
+        for cn in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+                   "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE"):
+            for st, v in per_stage_counter(sq_csv, cn, ns).items():
+                sq.setdefault(st, {})[cn] = v
     stages = {}
     ncalls_trace = defaultdict(int)
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
@@ -113,13 +123,23 @@ def main():
         stages[st] = {"avg_call_ms": round(avg_ns / 1e6, 4), "max_call_ms": round(calls[-1] / 1e6, 4),
                       "calls": len(calls), "dispatches_per_call": per_call,
                       "fetch_kib_per_call": f, "write_kib_per_call": w, "hbm_bytes_per_launch": hbm}
+        if st in sq:
+            c = sq[st]
+            stages[st]["sq_per_call"] = c
+            # VALU busy (estimate): each wave64 VALU instruction holds its SIMD
+            # >= 4 cycles (MI355X_MICROARCH.md issue costs; transcendentals 8),
+            # over the SIMD-cycles of the call: 256 CUs x 4 SIMDs x
+            # GRBM_GUI_ACTIVE / 8 (GRBM_GUI_ACTIVE is summed over the 8 XCDs).
+            if c.get("GRBM_GUI_ACTIVE"):
+                simd_cycles = 256 * 4 * c["GRBM_GUI_ACTIVE"] / 8.0
+                stages[st]["valu_busy"] = round(4.0 * c.get("SQ_INSTS_VALU", 0.0) / simd_cycles, 4)
     out = {"tag": tag, "source": src, "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950)",
            "stages": stages}
     for name in (f"{tag}_stages.json", "pmc_summary.json"):
         with open(os.path.join(dst, name), "w") as fh:
             json.dump(out, fh, indent=1)
     for st, v in sorted(stages.items(), key=lambda kv: -kv[1]["avg_call_ms"]):
-        print(f"{st:16s} {v['avg_call_ms']:8.3f} ms  hbm/call={v['hbm_bytes_per_launch']}")
+        print(f"{st:16s} {v['avg_call_ms']:8.3f} ms  hbm/call={v['hbm_bytes_per_launch']}  valu_busy={v.get('valu_busy')}")
 
 
 if __name__ == "__main__":
