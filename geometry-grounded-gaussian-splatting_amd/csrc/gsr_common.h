@@ -204,6 +204,15 @@ __device__ inline uint32_t xcd_remap(uint32_t b, uint32_t n) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
+// Division as the reference compiles it: CR is built with --use_fast_math
+// (DGR/setup.py), where a / b is the approximate div.approx.f32, i.e.
+// a * rcp(b).  Here: v_rcp_f32 (1 ulp) and one multiply, instead of the
+// ~10-instruction IEEE division sequence.  Used in the per-(pixel, splat)
+// backward loops; per-Gaussian code keeps IEEE division (its integer
+// outputs are checked bit-exactly against the oracle).
+__device__ __forceinline__ float fast_rcp(float b) { return __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ float fast_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+
 // Footprint of a splat record at a pixel offset (dx, dy) = (mean - pixel):
 //   power  = -0.5 (a dx^2 + c dy^2) - b dx dy   (render_forward.cu:486-487)
 //   t_peak = plane.x dx + plane.y dy + |t|      (render_forward.cu:513, 603)

@@ -8,9 +8,9 @@
 // summed over the 64 pixels of a wave with one transposed butterfly
 // (wave_transpose_reduce16: v_permlane32_swap / v_permlane16_swap, then DPP
 // mirrors and quad perms, all VALU), after which lanes 0, 4, ..., 60 hold the
-// 16 field totals and issue ONE 16-lane global_atomic_add_f32 that covers the Gaussian's 64-B
-// accumulator record (a single 64-B atomic request), plus one lane for the
-// |dmean2D| channel.  The reference (32-lane cg::reduce per field, then 17
+// 16 field totals and issue ONE global_atomic_add_f32 whose 16 field lanes
+// cover the Gaussian's 64-B accumulator record (a single 64-B atomic request)
+// and whose 17th lane adds the |dmean2D| channel.  The reference (32-lane cg::reduce per field, then 17
 // scalar atomics from lane 0) issues 17 single-lane atomic requests per warp
 // and Gaussian.  Waves with no valid pixel for a Gaussian skip it (ballot),
 // as the reference's warp.any does.
@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
                 const float t_delta = (mDepth - t_peak) * rsig;
                 const float G_exp = __expf(-0.5f * t_delta * t_delta);
                 const float Gt = alpha * G_exp;
-                dT_dtm += -0.25f * Gt / (1.f - Gt) * fabsf(t_delta) * rsig;
+                dT_dtm += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * rsig;
             }
         }
         kappa = dL_dmt / fmaxf(-dT_dtm, 1e-7f);
@@ -163,7 +163,8 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
             if (valid) {
                 const float4 w2 = s_w2[j];
                 const float4 w3 = s_w3[j];
-                T = T / (1.f - alpha);
+                const float r1a = fast_rcp(1.f - alpha);
+                T = T * r1a;
                 const float bw = alpha * T;
                 float dL_dopa = 0.f;
                 ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0;
@@ -197,10 +198,10 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
                     const float t_delta = (mDepth - t_peak) * rsig;
                     const float G_exp = __expf(-0.5f * t_delta * t_delta);
                     const float Gt = alpha * G_exp;
-                    float dL_dGt = kappa * 0.25f / (1.f - Gt);
+                    float dL_dGt = fast_div(kappa * 0.25f, 1.f - Gt);
                     dL_dGt = mDepth > t_peak ? dL_dGt : -dL_dGt;
                     dL_dGt = rsig > 0.f ? dL_dGt : 0.f;
-                    dL_dopa_sigma = dL_dGt * G_exp - kappa * (t_delta > 0.f ? 0.5f / (1.f - alpha) : 0.f);
+                    dL_dopa_sigma = dL_dGt * G_exp - kappa * (t_delta > 0.f ? 0.5f * r1a : 0.f);
                     const float dL_ddelta = -dL_dGt * Gt * t_delta;
                     dL_dt = -dL_ddelta * rsig;
                     f[kAccPlane + 0] = dL_dt * dx;
@@ -210,7 +211,7 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
                 }
                 dL_dopa *= T;
                 if constexpr (GEOM) dL_dopa += dL_dopa_sigma;
-                dL_dopa += -T_final / (1.f - alpha) * dL_dfinalT;
+                dL_dopa += -T_final * r1a * dL_dfinalT;
                 last_alpha = alpha;
                 const float dL_dG = w1.y * dL_dopa;
                 const float gdx = G * dx, gdy = G * dy;
@@ -233,11 +234,13 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
             const float red = wave_transpose_reduce16(f);
             const float abs_red = wave_sum_dpp(fabs_sum);
             const uint32_t g = s_id[j];
-            if ((lane & 3) == 0) {
-                const int field = lane >> 2;
-                if (GEOM || field < kAccNormal) atomicAdd(a.acc + (size_t)g * kAccFields + field, red);
+            // one atomic instruction: lanes 0, 4, .., 60 add the 16 fields of
+            // the record (one 64-B line), lane 1 adds |dmean2D|
+            const bool field_lane = (lane & 3) == 0 && (GEOM || (lane >> 2) < kAccNormal);
+            if (field_lane || lane == 1) {
+                float* dst = field_lane ? a.acc + (size_t)g * kAccFields + (lane >> 2) : a.acc_abs + g;
+                atomicAdd(dst, field_lane ? red : abs_red);
             }
-            if (lane == 0) atomicAdd(a.acc_abs + g, abs_red);
         }
     }
 }
