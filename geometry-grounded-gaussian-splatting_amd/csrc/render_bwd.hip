@@ -39,197 +39,267 @@ struct RenderBwdArgs {
     float* acc_abs;  // [P]
 };
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr int kBwdThreads = 128;  // 2 wave64 per tile, two pixels per lane
+constexpr int kBwdBatch = 256;    // splat records staged per LDS batch
+
+__device__ __forceinline__ f2 sel2(bool ca, bool cb, f2 x, f2 y) { return f2{ca ? x.x : y.x, cb ? x.y : y.y}; }
+__device__ __forceinline__ f2 splat2(float v) { return f2{v, v}; }
+__device__ __forceinline__ float hsum(f2 v) { return v.x + v.y; }
+
+// splat_power / splat_tpeak (gsr_common.h) for the two pixels of a lane,
+// which share the column (dx) and differ in the row (dy.x, dy.y); the
+// packed operations round exactly as the scalar helpers, so alpha and the
+// contribute decision stay bit-identical to the forward.
+__device__ __forceinline__ f2 splat_power2(const float4& w0, const float4& w1, float dx, f2 dy) {
+#pragma clang fp contract(off)
+    const float ax = (w0.z * dx) * dx;
+    const f2 q = __builtin_elementwise_fma(splat2(w1.x) * dy, dy, splat2(ax));
+    return __builtin_elementwise_fma(splat2(-0.5f), q, -(splat2(w0.w * dx) * dy));
+}
+__device__ __forceinline__ f2 splat_tpeak2(const float4& w1, const float4& w2, float dx, f2 dy) {
+#pragma clang fp contract(off)
+    return __builtin_elementwise_fma(splat2(w1.w), dy, splat2(w1.z * dx)) + splat2(w2.x);
+}
+
+// Per-pixel inputs of the backward (render_backward.cu:771-833).
+struct PixIn {
+    bool inside;
+    uint32_t last;
+    float T_final, dLp0, dLp1, dLp2, dL_dfinalT, dLn0, dLn1, dLn2, mDepth, dL_dmt;
+};
+
 template <bool GEOM>
-__global__ void __launch_bounds__(256) render_bwd_kernel(RenderBwdArgs a) {
-    __shared__ float4 s_w0[kTilePixels], s_w1[kTilePixels], s_w2[kTilePixels], s_w3[kTilePixels];
-    __shared__ uint32_t s_id[kTilePixels];
+__device__ __forceinline__ PixIn load_pixel(const RenderBwdArgs& a, int px, int py) {
+    PixIn r{};
+    r.inside = px < a.W && py < a.H;
+    r.T_final = 1.f;
+    if (!r.inside) return r;
+    const int HW = a.W * a.H;
+    const int pix = a.W * py + px;
+    const float w_final = a.alphas[pix];
+    r.T_final = 1.f - w_final;
+    r.last = a.n_contrib[pix];
+    if (r.last == 0) return r;  // blended nothing: no gradient terms (and 1/alpha would be inf)
+    r.dLp0 = a.dL_dpix[pix];
+    r.dLp1 = a.dL_dpix[HW + pix];
+    r.dLp2 = a.dL_dpix[2 * HW + pix];
+    r.dL_dfinalT = -a.dL_dalpha[pix] + a.bg[0] * r.dLp0 + a.bg[1] * r.dLp1 + a.bg[2] * r.dLp2;
+    if constexpr (GEOM) {
+        const float inv_w = 1.f / w_final;
+        const float pnx = ((float)px - (float)(a.W - 1) / 2.f) / a.focal_x;
+        const float pny = ((float)py - (float)(a.H - 1) / 2.f) / a.focal_y;
+        const float nrm = sqrtf(pnx * pnx + pny * pny + 1.f);
+        r.dL_dmt = a.dL_dmdepth[pix] * (1.0f / nrm);
+        r.dLn0 = a.dL_dnormal[pix] * inv_w;
+        r.dLn1 = a.dL_dnormal[HW + pix] * inv_w;
+        r.dLn2 = a.dL_dnormal[2 * HW + pix] * inv_w;
+        r.dL_dfinalT += r.dLn0 * a.normalmap[pix] + r.dLn1 * a.normalmap[HW + pix] + r.dLn2 * a.normalmap[2 * HW + pix];
+        r.mDepth = a.mdepth[pix] * nrm;
+    }
+    return r;
+}
+
+// One workgroup of 128 lanes (2 wave64) per 16x16 tile; lane l of wave w
+// owns the pixel pair (x, y) and (x, y + 4) with x = l % 16,
+// y = 8 w + l / 16.  The two pixels' state lives in the halves of packed
+// fp32 registers (v_pk_{add,mul,fma}_f32), so one instruction stream serves
+// two pixels, and the per-(wave, Gaussian) reduction and atomic cover 128
+// pixels instead of 64.  Per-pixel validity is a select, not a branch.
+template <bool GEOM>
+__global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a) {
+    __shared__ float4 s_w0[kBwdBatch], s_w1[kBwdBatch], s_w2[kBwdBatch], s_w3[kBwdBatch];
+    __shared__ uint32_t s_id[kBwdBatch];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const int wave = tid >> 6;
     const uint32_t tile = xcd_remap(blockIdx.x, a.num_tiles);
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
-    const int px = tx * kTile + (tid & 15), py = ty * kTile + (tid >> 4);
-    const bool inside = px < a.W && py < a.H;
-    const float pixx = (float)px, pixy = (float)py;
     const uint2 range = a.ranges[tile];
     const int max_contrib = (int)a.max_contrib[tile];
     if (max_contrib == 0) return;  // uniform over the block
-    const int HW = a.W * a.H;
-    const int pix = a.W * py + px;
 
-    const float w_final = inside ? a.alphas[pix] : 0.f;
-    const float T_final = 1.f - w_final;
-    float T = T_final;
-    const uint32_t last = inside ? a.n_contrib[pix] : 0u;
+    const int px = tx * kTile + (lane & 15);
+    const int pya = ty * kTile + wave * 8 + (lane >> 4), pyb = pya + 4;
+    const PixIn pa = load_pixel<GEOM>(a, px, pya);
+    const PixIn pb = load_pixel<GEOM>(a, px, pyb);
+    const float pixx = (float)px;
+    const f2 pixy = {(float)pya, (float)pyb};
+    const bool ina = pa.inside, inb = pb.inside;
+    const uint32_t last_a = pa.last, last_b = pb.last;
+    const f2 T_final = {pa.T_final, pb.T_final};
+    const f2 dLp0 = {pa.dLp0, pb.dLp0}, dLp1 = {pa.dLp1, pb.dLp1}, dLp2 = {pa.dLp2, pb.dLp2};
+    const f2 dL_dfinalT = {pa.dL_dfinalT, pb.dL_dfinalT};
+    const f2 dLn0 = {pa.dLn0, pb.dLn0}, dLn1 = {pa.dLn1, pb.dLn1}, dLn2 = {pa.dLn2, pb.dLn2};
+    const f2 mDepth = {pa.mDepth, pb.mDepth};
+    const int rounds = (max_contrib + kBwdBatch - 1) / kBwdBatch;
 
-    float dLp0 = 0.f, dLp1 = 0.f, dLp2 = 0.f, dL_dfinalT = 0.f;
-    float dLn0 = 0.f, dLn1 = 0.f, dLn2 = 0.f, mDepth = 0.f, dL_dmt = 0.f;
-    if (inside) {
-        dLp0 = a.dL_dpix[pix];
-        dLp1 = a.dL_dpix[HW + pix];
-        dLp2 = a.dL_dpix[2 * HW + pix];
-        dL_dfinalT = -a.dL_dalpha[pix] + a.bg[0] * dLp0 + a.bg[1] * dLp1 + a.bg[2] * dLp2;
-        if constexpr (GEOM) {
-            const float inv_w = 1.f / w_final;
-            const float pnx = (pixx - (float)(a.W - 1) / 2.f) / a.focal_x;
-            const float pny = (pixy - (float)(a.H - 1) / 2.f) / a.focal_y;
-            const float nrm = sqrtf(pnx * pnx + pny * pny + 1.f);
-            dL_dmt = a.dL_dmdepth[pix] * (1.0f / nrm);
-            dLn0 = a.dL_dnormal[pix] * inv_w;
-            dLn1 = a.dL_dnormal[HW + pix] * inv_w;
-            dLn2 = a.dL_dnormal[2 * HW + pix] * inv_w;
-            dL_dfinalT += dLn0 * a.normalmap[pix] + dLn1 * a.normalmap[HW + pix] + dLn2 * a.normalmap[2 * HW + pix];
-            mDepth = a.mdepth[pix] * nrm;
+    auto stage_fwd = [&](int i) {
+        for (int k = tid; k < kBwdBatch; k += kBwdThreads) {
+            const int c = i * kBwdBatch + k;
+            if (c < max_contrib) {
+                const Splat* sp = a.splats + a.point_list[range.x + c];
+                s_w0[k] = sp->w0;
+                s_w1[k] = sp->w1;
+                s_w2[k] = sp->w2;
+            }
         }
-    }
-    const int rounds = (max_contrib + kTilePixels - 1) / kTilePixels;
+    };
 
     // ---- median-depth implicit gradient pre-pass (render_backward.cu:835-880)
-    float kappa = 0.f;
+    f2 kappa = {0.f, 0.f};
     if constexpr (GEOM) {
-        float dT_dtm = 0.f;
+        f2 dT_dtm = {0.f, 0.f};
+        const bool on_a = ina && pa.mDepth != 0.f && last_a != 0;
+        const bool on_b = inb && pb.mDepth != 0.f && last_b != 0;
+        const uint32_t wave_last = wave_max_u(max(on_a ? last_a : 0u, on_b ? last_b : 0u));
         uint32_t c = 0;
-        bool pdone = (mDepth == 0.f) || (last == 0) || !inside;
         int toDo = max_contrib;
-        for (int i = 0; i < rounds; i++, toDo -= kTilePixels) {
+        for (int i = 0; i < rounds; i++, toDo -= kBwdBatch) {
             __syncthreads();
-            const int k = i * kTilePixels + tid;
-            if (k < max_contrib) {
-                const Splat* sp = a.splats + a.point_list[range.x + k];
-                s_w0[tid] = sp->w0;
-                s_w1[tid] = sp->w1;
-                s_w2[tid] = sp->w2;
-            }
+            stage_fwd(i);
             __syncthreads();
-            const int n = min(kTilePixels, toDo);
-            for (int j = 0; !pdone && j < n; j++) {
+            const int n = min(kBwdBatch, toDo);
+            for (int j = 0; j < n && c < wave_last; j++) {
                 c++;
-                pdone = c >= last;
                 const float4 w0 = s_w0[j];
-                const float dx = w0.x - pixx, dy = w0.y - pixy;
                 const float4 w1 = s_w1[j];
-                const float power = splat_power(w0, w1, dx, dy);
-                if (power > 0.0f) continue;
-                const float alpha = fminf(0.99f, w1.y * __expf(power));
-                if (alpha < 1.0f / 255.0f) continue;
+                const float dx = w0.x - pixx;
+                const f2 dy = splat2(w0.y) - pixy;
+                const f2 power = splat_power2(w0, w1, dx, dy);
+                const f2 alpha = {fminf(0.99f, w1.y * __expf(power.x)), fminf(0.99f, w1.y * __expf(power.y))};
+                const bool va = on_a && c <= last_a && !(power.x > 0.f) && !(alpha.x < 1.0f / 255.0f);
+                const bool vb = on_b && c <= last_b && !(power.y > 0.f) && !(alpha.y < 1.0f / 255.0f);
                 const float4 w2 = s_w2[j];
-                const float t_peak = splat_tpeak(w1, w2, dx, dy);
+                const f2 t_peak = splat_tpeak2(w1, w2, dx, dy);
                 const float rsig = w2.y;
-                const float t_delta = (mDepth - t_peak) * rsig;
-                const float G_exp = __expf(-0.5f * t_delta * t_delta);
-                const float Gt = alpha * G_exp;
-                dT_dtm += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * rsig;
+                const f2 t_delta = (mDepth - t_peak) * rsig;
+                const f2 G_exp = {__expf(-0.5f * t_delta.x * t_delta.x), __expf(-0.5f * t_delta.y * t_delta.y)};
+                const f2 Gt = alpha * G_exp;
+                const f2 term = f2{fast_div(-0.25f * Gt.x, 1.f - Gt.x), fast_div(-0.25f * Gt.y, 1.f - Gt.y)} *
+                                f2{fabsf(t_delta.x), fabsf(t_delta.y)} * rsig;
+                dT_dtm += sel2(va, vb, term, splat2(0.f));
             }
         }
-        kappa = dL_dmt / fmaxf(-dT_dtm, 1e-7f);
+        kappa = f2{pa.dL_dmt / fmaxf(-dT_dtm.x, 1e-7f), pb.dL_dmt / fmaxf(-dT_dtm.y, 1e-7f)};
     }
 
     // ---- main back-to-front pass (render_backward.cu:882-1068)
+    // The reference carries (last_alpha, last_colour) one step and folds them
+    // into accum_rec at the NEXT valid contributor; here a contributor is
+    // folded in right after its own terms (same values, same operations).  A
+    // pixel for which the splat is not valid runs with alpha = 0, which leaves
+    // T (x rcp(1) = 1), accum_rec (x 1 + 0) and the plane terms unchanged
+    // exactly, so only dL/dopacity and G need a select.
     uint32_t contributor = (uint32_t)max_contrib;
-    float last_alpha = 0.f;
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, ar0 = 0.f, ar1 = 0.f, ar2 = 0.f;
-    float ln0 = 0.f, ln1 = 0.f, ln2 = 0.f, an0 = 0.f, an1 = 0.f, an2 = 0.f;
+    f2 T = T_final;
+    f2 ar0 = {0.f, 0.f}, ar1 = {0.f, 0.f}, ar2 = {0.f, 0.f};
+    f2 an0 = {0.f, 0.f}, an1 = {0.f, 0.f}, an2 = {0.f, 0.f};
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
+    const f2 zero = {0.f, 0.f}, one = {1.f, 1.f};
     int toDo = max_contrib;
-    for (int i = 0; i < rounds; i++, toDo -= kTilePixels) {
+    for (int i = 0; i < rounds; i++, toDo -= kBwdBatch) {
         __syncthreads();
-        const int k = i * kTilePixels + tid;
-        if (k < max_contrib) {
-            const uint32_t g = a.point_list[range.x + max_contrib - k - 1];
-            const Splat sp = a.splats[g];
-            s_id[tid] = g;
-            s_w0[tid] = sp.w0;
-            s_w1[tid] = sp.w1;
-            s_w2[tid] = sp.w2;
-            s_w3[tid] = sp.w3;
+        for (int k = tid; k < kBwdBatch; k += kBwdThreads) {
+            const int c = i * kBwdBatch + k;
+            if (c < max_contrib) {
+                const uint32_t g = a.point_list[range.x + max_contrib - c - 1];
+                const Splat* sp = a.splats + g;
+                s_id[k] = g;
+                s_w0[k] = sp->w0;
+                s_w1[k] = sp->w1;
+                s_w2[k] = sp->w2;
+                s_w3[k] = sp->w3;
+            }
         }
         __syncthreads();
-        const int n = min(kTilePixels, toDo);
+        const int n = min(kBwdBatch, toDo);
         for (int j = 0; j < n; j++) {
             contributor--;
             const float4 w0 = s_w0[j];
-            const float dx = w0.x - pixx, dy = w0.y - pixy;
             const float4 w1 = s_w1[j];
-            const float power = splat_power(w0, w1, dx, dy);
-            const float G = __expf(power);
-            const float alpha = fminf(0.99f, w1.y * G);
-            const bool valid = inside && !(contributor >= last || power > 0.0f || alpha < 1.0f / 255.0f);
-            if (__ballot(valid) == 0ull) continue;  // wave-uniform skip (warp.any)
+            const float dx = w0.x - pixx;
+            const f2 dy = splat2(w0.y) - pixy;
+            const f2 power = splat_power2(w0, w1, dx, dy);
+            const f2 G = {__expf(power.x), __expf(power.y)};
+            const f2 alpha_raw = {fminf(0.99f, w1.y * G.x), fminf(0.99f, w1.y * G.y)};
+            const bool va = ina && !(contributor >= last_a || power.x > 0.0f || alpha_raw.x < 1.0f / 255.0f);
+            const bool vb = inb && !(contributor >= last_b || power.y > 0.0f || alpha_raw.y < 1.0f / 255.0f);
+            if (__ballot(va || vb) == 0ull) continue;  // wave-uniform skip (warp.any)
 
+            const float4 w2 = s_w2[j];
+            const float4 w3 = s_w3[j];
+            const f2 alpha = sel2(va, vb, alpha_raw, zero);
+            const f2 one_m_alpha = one - alpha;
+            const f2 r1a = {fast_rcp(one_m_alpha.x), fast_rcp(one_m_alpha.y)};
+            T = T * r1a;
+            const f2 bw = alpha * T;
+            const f2 c0 = splat2(w2.z), c1 = splat2(w2.w), c2 = splat2(w3.x);
+            f2 dL_dopa = (c0 - ar0) * dLp0 + (c1 - ar1) * dLp1 + (c2 - ar2) * dLp2;
+            ar0 = alpha * c0 + one_m_alpha * ar0;
+            ar1 = alpha * c1 + one_m_alpha * ar1;
+            ar2 = alpha * c2 + one_m_alpha * ar2;
             float f[16];
+            f[kAccColor + 0] = hsum(bw * dLp0);
+            f[kAccColor + 1] = hsum(bw * dLp1);
+            f[kAccColor + 2] = hsum(bw * dLp2);
+            f2 dL_dt = zero;
+            if constexpr (GEOM) {
+                const f2 n0 = splat2(w3.y), n1 = splat2(w3.z), n2 = splat2(w3.w);
+                dL_dopa += (n0 - an0) * dLn0 + (n1 - an1) * dLn1 + (n2 - an2) * dLn2;
+                an0 = alpha * n0 + one_m_alpha * an0;
+                an1 = alpha * n1 + one_m_alpha * an1;
+                an2 = alpha * n2 + one_m_alpha * an2;
+                f[kAccNormal + 0] = hsum(bw * dLn0);
+                f[kAccNormal + 1] = hsum(bw * dLn1);
+                f[kAccNormal + 2] = hsum(bw * dLn2);
+                const f2 t_peak = splat_tpeak2(w1, w2, dx, dy);
+                const float rsig = w2.y;
+                const f2 dmt = mDepth - t_peak;
+                const f2 t_delta = dmt * rsig;
+                const f2 G_exp = {__expf(-0.5f * t_delta.x * t_delta.x), __expf(-0.5f * t_delta.y * t_delta.y)};
+                const f2 Gt = alpha * G_exp;  // 0 for a non-valid pixel -> no plane terms
+                const f2 omGt = one - Gt;
+                f2 dL_dGt = kappa * 0.25f * f2{fast_rcp(omGt.x), fast_rcp(omGt.y)};
+                dL_dGt = sel2(mDepth.x > t_peak.x, mDepth.y > t_peak.y, dL_dGt, -dL_dGt);
+                dL_dGt = rsig > 0.f ? dL_dGt : zero;
+                const f2 half_r = sel2(t_delta.x > 0.f, t_delta.y > 0.f, 0.5f * r1a, zero);
+                const f2 dL_dopa_sigma = dL_dGt * G_exp - kappa * half_r;
+                const f2 dL_ddelta = -dL_dGt * Gt * t_delta;
+                dL_dt = -dL_ddelta * rsig;
+                f[kAccPlane + 0] = hsum(dL_dt) * dx;
+                f[kAccPlane + 1] = hsum(dL_dt * dy);
+                f[kAccPlane + 2] = hsum(dL_dt);
+                f[kAccPlane + 3] = hsum(dL_ddelta * dmt);
+                dL_dopa = dL_dopa * T + dL_dopa_sigma;
+            } else {
+                dL_dopa = dL_dopa * T;
+            }
+            dL_dopa += -T_final * r1a * dL_dfinalT;
+            dL_dopa = sel2(va, vb, dL_dopa, zero);
+            const f2 Gc = sel2(va, vb, G, zero);
+            const f2 dL_dG = w1.y * dL_dopa;
+            const f2 gdx = Gc * dx, gdy = Gc * dy;
+            const f2 dG_ddelx = -gdx * w0.z - gdy * w0.w;
+            const f2 dG_ddely = -gdy * w1.x - gdx * w0.w;
+            f2 dL_ddelx = dL_dG * dG_ddelx;
+            f2 dL_ddely = dL_dG * dG_ddely;
+            if constexpr (GEOM) {
+                dL_ddelx += dL_dt * w1.z;
+                dL_ddely += dL_dt * w1.w;
+            }
+            const f2 mx = dL_ddelx * ddelx_dx, my = dL_ddely * ddely_dy;
+            f[kAccMean2D + 0] = hsum(mx);
+            f[kAccMean2D + 1] = hsum(my);
+            const float fabs_sum = (fabsf(mx.x) + fabsf(my.x)) + (fabsf(mx.y) + fabsf(my.y));
+            f[kAccConic + 0] = hsum(-0.5f * gdx * dx * dL_dG);
+            f[kAccConic + 1] = hsum(-0.5f * gdx * dy * dL_dG);
+            f[kAccConic + 2] = hsum(-0.5f * gdy * dy * dL_dG);
+            f[kAccConic + 3] = hsum(Gc * dL_dopa);
+            if constexpr (!GEOM) {
 #pragma unroll
-            for (int q = 0; q < 16; q++) f[q] = 0.f;
-            float fabs_sum = 0.f;
-            if (valid) {
-                const float4 w2 = s_w2[j];
-                const float4 w3 = s_w3[j];
-                const float r1a = fast_rcp(1.f - alpha);
-                T = T * r1a;
-                const float bw = alpha * T;
-                float dL_dopa = 0.f;
-                ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0;
-                ar1 = last_alpha * lc1 + (1.f - last_alpha) * ar1;
-                ar2 = last_alpha * lc2 + (1.f - last_alpha) * ar2;
-                lc0 = w2.z;
-                lc1 = w2.w;
-                lc2 = w3.x;
-                dL_dopa += (lc0 - ar0) * dLp0;
-                dL_dopa += (lc1 - ar1) * dLp1;
-                dL_dopa += (lc2 - ar2) * dLp2;
-                f[kAccColor + 0] = bw * dLp0;
-                f[kAccColor + 1] = bw * dLp1;
-                f[kAccColor + 2] = bw * dLp2;
-                float dL_dt = 0.f, dL_dopa_sigma = 0.f;
-                if constexpr (GEOM) {
-                    an0 = last_alpha * ln0 + (1.f - last_alpha) * an0;
-                    an1 = last_alpha * ln1 + (1.f - last_alpha) * an1;
-                    an2 = last_alpha * ln2 + (1.f - last_alpha) * an2;
-                    ln0 = w3.y;
-                    ln1 = w3.z;
-                    ln2 = w3.w;
-                    dL_dopa += (ln0 - an0) * dLn0;
-                    dL_dopa += (ln1 - an1) * dLn1;
-                    dL_dopa += (ln2 - an2) * dLn2;
-                    f[kAccNormal + 0] = bw * dLn0;
-                    f[kAccNormal + 1] = bw * dLn1;
-                    f[kAccNormal + 2] = bw * dLn2;
-                    const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                    const float rsig = w2.y;
-                    const float t_delta = (mDepth - t_peak) * rsig;
-                    const float G_exp = __expf(-0.5f * t_delta * t_delta);
-                    const float Gt = alpha * G_exp;
-                    float dL_dGt = fast_div(kappa * 0.25f, 1.f - Gt);
-                    dL_dGt = mDepth > t_peak ? dL_dGt : -dL_dGt;
-                    dL_dGt = rsig > 0.f ? dL_dGt : 0.f;
-                    dL_dopa_sigma = dL_dGt * G_exp - kappa * (t_delta > 0.f ? 0.5f * r1a : 0.f);
-                    const float dL_ddelta = -dL_dGt * Gt * t_delta;
-                    dL_dt = -dL_ddelta * rsig;
-                    f[kAccPlane + 0] = dL_dt * dx;
-                    f[kAccPlane + 1] = dL_dt * dy;
-                    f[kAccPlane + 2] = dL_dt;
-                    f[kAccPlane + 3] = dL_ddelta * (mDepth - t_peak);
-                }
-                dL_dopa *= T;
-                if constexpr (GEOM) dL_dopa += dL_dopa_sigma;
-                dL_dopa += -T_final * r1a * dL_dfinalT;
-                last_alpha = alpha;
-                const float dL_dG = w1.y * dL_dopa;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * w0.z - gdy * w0.w;
-                const float dG_ddely = -gdy * w1.x - gdx * w0.w;
-                float dL_ddelx = dL_dG * dG_ddelx;
-                float dL_ddely = dL_dG * dG_ddely;
-                if constexpr (GEOM) {
-                    dL_ddelx += dL_dt * w1.z;
-                    dL_ddely += dL_dt * w1.w;
-                }
-                f[kAccMean2D + 0] = dL_ddelx * ddelx_dx;
-                f[kAccMean2D + 1] = dL_ddely * ddely_dy;
-                fabs_sum = fabsf(f[kAccMean2D + 0]) + fabsf(f[kAccMean2D + 1]);
-                f[kAccConic + 0] = -0.5f * gdx * dx * dL_dG;
-                f[kAccConic + 1] = -0.5f * gdx * dy * dL_dG;
-                f[kAccConic + 2] = -0.5f * gdy * dy * dL_dG;
-                f[kAccConic + 3] = G * dL_dopa;
+                for (int q = kAccNormal; q < kAccFields; q++) f[q] = 0.f;
             }
             const float red = wave_transpose_reduce16(f);
             const float abs_red = wave_sum_dpp(fabs_sum);
@@ -272,9 +342,9 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.acc_abs = ws.acc_abs;
     if (a.num_tiles == 0) return hipSuccess;
     if (p.require_depth)
-        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(a.num_tiles), dim3(kBwdThreads), 0, stream, a);
     else
-        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(a.num_tiles), dim3(kBwdThreads), 0, stream, a);
     return hipGetLastError();
 }
 

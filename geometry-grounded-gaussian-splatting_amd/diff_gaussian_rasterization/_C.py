@@ -67,6 +67,10 @@ def loaded_library_path() -> str:
 
 
 NUM_STAGES = 10
+# debugging aid: keep the last backward's accumulator buffer (gsr_api.hip
+# carve_bwd layout: 256-B aligned base, float acc[P][16], then float acc_abs[P])
+KEEP_BWD_SCRATCH = False
+last_bwd_scratch = None
 OPT_BISECT_SKIP = 0
 OPT_RENDER_STATS = 1
 
@@ -243,6 +247,9 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
                 _ptr(outs["dcov3D"]), _ptr(outs["dsh"]), _ptr(outs["dsg_axis"]), _ptr(outs["dsg_sharpness"]),
                 _ptr(outs["dsg_color"]), int(bool(require_depth)), int(bool(debug)), _stream(dev))
         _check(rc)
+        if KEEP_BWD_SCRATCH:
+            global last_bwd_scratch
+            last_bwd_scratch = scratch.tensor
     return (outs["dmeans2D"], outs["dcolors"], outs["dopacity"], outs["dmeans3D"], outs["dcov3D"], outs["dsh"],
             outs["dsg_axis"], outs["dsg_sharpness"], outs["dsg_color"], outs["dscales"], outs["drotations"])
 
