@@ -125,7 +125,8 @@ __device__ __forceinline__ void bisect_step(float (&A)[kSplit + 1], float (&B)[k
 
 // Diagnostic counters (STATS builds only, option GSR_OPT_RENDER_STATS):
 // [0] bisection wave-steps and [1] active lanes on the per-lane (resident)
-// walk; [2] wave-steps and [3] active lanes on the wave-uniform walk.
+// walk; [2] active lanes in passes 2-5 and [3] those whose whole window is
+// more than 7 sigma from the splat's peak (exact-constant factors).
 __device__ unsigned long long g_render_stats[8];
 
 template <bool GEOM, bool SKIP, bool STATS = false>
@@ -302,6 +303,17 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                     const float alpha = fminf(0.99f, w1.y * __expf(power));
                     const float4 w2 = c_w2[j];
                     const float t_peak = splat_tpeak(w1, w2, dx, dy);
+                    if constexpr (STATS && !FIRST) {
+                        // lanes whose whole window is > 7 sigma from the peak
+                        const float d_lo = (ts[1] - t_peak) * w2.y, d_hi = (ts[kSplit - 1] - t_peak) * w2.y;
+                        const bool far = w2.y > 0.f && (d_lo > 7.f || d_hi < -7.f);
+                        const unsigned long long m = __ballot(1);
+                        const unsigned long long fm = __ballot(far);
+                        if ((tid & 63) == __builtin_ctzll(m)) {
+                            st[2] += __popcll(m);
+                            st[3] += __popcll(fm);
+                        }
+                    }
                     bisect_step<FIRST, SKIP>(A, B, ts, alpha, t_peak, w2.y);
                 }
             } else {
@@ -324,13 +336,6 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                         if (alpha < 1.0f / 255.0f) continue;
                         const float4 w2 = c_w2[j];
                         const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                        if constexpr (STATS) {
-                            const unsigned long long m = __ballot(1);
-                            if ((tid & 63) == __builtin_ctzll(m)) {
-                                st[2] += 1;
-                                st[3] += __popcll(m);
-                            }
-                        }
                         bisect_step<FIRST, SKIP>(A, B, ts, alpha, t_peak, w2.y);
                     }
                 }

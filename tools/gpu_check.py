@@ -59,7 +59,7 @@ if __name__ == "__main__":
     st = _C.debug_render_stats(True)
     _C.set_option(_C.OPT_RENDER_STATS, 0)
     print("stats per forward (4 calls):", [v / 4 for v in st[:4]],
-          "lanes/step per-lane walk=%.1f uniform walk=%.1f" % (st[1] / max(st[0], 1), st[3] / max(st[2], 1)))
+          "lanes/step=%.1f far-frac passes2-5=%.3f" % (st[1] / max(st[0], 1), st[3] / max(st[2], 1)))
     run(20000, 320, 240)
     for opt in (0, 1):
         _C.set_option(_C.OPT_BISECT_SKIP, opt)
