@@ -52,8 +52,8 @@ size_t carve_geom(void* base, int P, GeomState& g) {
     g.tiles_touched = c.take<uint32_t>(P);
     g.order = c.take<uint32_t>(P);
     g.depth_keys_sorted = c.take<uint32_t>(P);
-    g.counts = c.take<uint32_t>(P);
-    g.offsets = c.take<uint32_t>(P);
+    g.counts = c.take<uint2>(P);
+    g.offsets = c.take<uint2>(P);
     g.radii = c.take<int>(P);
     g.clamped = c.take<uint8_t>(P);
     g.scan_tmp_bytes = scan_temp_bytes(P);
@@ -343,22 +343,26 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     }
 
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, radii, stream), "preprocess");
-    GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_order(gs, P, stream), "depth order");
+    GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_order(p, gs, radii, stream), "depth order");
     GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
-    uint32_t K = 0;
-    GSR_TRY(hipMemcpyAsync(&K, gs.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
+    // K = the reference's instance count (rect tiles, returned as num_rendered
+    // and sizing the binning buffer); K_live = instances that survive the
+    // tile test and are actually sorted and rendered (binning.hip)
+    uint2 Ks = make_uint2(0u, 0u);
+    GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
     {
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
     }
+    const uint32_t K = Ks.x, K_live = Ks.y;
     const int tile_bits = (int)higher_msb((uint32_t)tiles);
     BinningState bs;
     void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, tile_bits, bs));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
     carve_binning(aligned_base(bbuf), (int)K, tile_bits, bs);
     GSR_STAGE(GSR_STAGE_EMIT_KEYS, launch_emit_keys(p, gs, radii, bs, stream), "emit keys");
-    GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K, tile_bits, stream), "sort");
-    GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K, ts, tiles, stream), "tile ranges");
+    GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K_live, tile_bits, stream), "sort");
+    GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K_live, ts, tiles, stream), "tile ranges");
     GSR_STAGE(GSR_STAGE_RENDER_FWD,
               launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
     if (num_rendered) *num_rendered = (int)K;

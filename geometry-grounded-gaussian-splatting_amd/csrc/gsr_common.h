@@ -67,8 +67,8 @@ struct GeomState {
     uint32_t* tiles_touched;
     uint32_t* order;              // Gaussian indices in (depth bits, index) order
     uint32_t* depth_keys_sorted;  // sorted depth bit patterns (sort output, unused after)
-    uint32_t* counts;             // tiles_touched in depth order
-    uint32_t* offsets;            // inclusive scan of counts
+    uint2* counts;                // per Gaussian in depth order: (tiles_touched, live tiles)
+    uint2* offsets;               // inclusive scan of counts: .x -> K (reference count), .y -> live instances
     int* radii;                   // internal copy when the caller passes radii == NULL
     uint8_t* clamped;             // bit c set: colour channel c was clamped at 0
     void* scan_tmp;

@@ -65,7 +65,7 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
 size_t scan_temp_bytes(int P);
 size_t depth_sort_temp_bytes(int P);
 size_t sort_temp_bytes(int K, int tile_bits);
-hipError_t launch_depth_order(const GeomState& gs, int P, hipStream_t stream);
+hipError_t launch_depth_order(const FwdParams& p, const GeomState& gs, const int* radii, hipStream_t stream);
 hipError_t launch_scan(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_emit_keys(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
                             hipStream_t stream);

@@ -46,15 +46,50 @@ def _fwd_args(c, colors_precomp=None, cov3D=None, scale_modifier=1.0):
     return a
 
 
-def _check_binning(out, o, H, W):
-    """Per-tile Gaussian lists and tile ranges equal the oracle's (the
-    reference's stable (tile, depth) sort order), element for element."""
+def _check_binning(out, o, H, W, dead_sample=None):
+    """Per-tile Gaussian lists against the oracle's (the reference's stable
+    (tile, depth) sort order): ours is the oracle's list with the instances
+    the tile test culls removed, in the same order, and every removed
+    instance is dead — power > 0 or alpha < 1/255 at every pixel of its tile
+    (checked for all of them, or for `dead_sample` random ones)."""
     from diff_gaussian_rasterization import _C
 
     plist, ranges = _C.debug_binning(out[7], out[9], out[0], H, W)
-    ob = o["state"].binning()
-    assert np.array_equal(plist, ob["point_list"])
-    assert np.array_equal(ranges, o["state"].tile_state()["ranges"])
+    ob = o["state"].binning()["point_list"].astype(np.int64)
+    oranges = o["state"].tile_state()["ranges"].astype(np.int64)
+    tiles = ranges.shape[0]
+
+    def keys(pl, rg):
+        tile = np.repeat(np.arange(tiles, dtype=np.int64), rg[:, 1] - rg[:, 0])
+        ent = np.concatenate([pl[a:b] for a, b in rg]) if len(pl) else np.zeros(0, np.int64)
+        return (tile << 32) | ent.astype(np.int64)
+
+    ours = keys(plist.astype(np.int64), ranges.astype(np.int64))
+    ref = keys(ob, oranges)
+    assert len(ours) <= len(ref) == out[0]
+    srt = np.argsort(ref, kind="stable")
+    at = np.searchsorted(ref[srt], ours)
+    assert np.all(at < len(ref)) and np.array_equal(ref[srt][np.minimum(at, len(ref) - 1)], ours)
+    pos = srt[at]
+    assert np.all(np.diff(pos) > 0)  # same relative order in every tile
+    dropped = ref[~np.isin(ref, ours)]
+    if dead_sample is not None and len(dropped) > dead_sample:
+        dropped = np.random.default_rng(0).choice(dropped, dead_sample, replace=False)
+    geo = o["state"].geometry()
+    gx = (W + 15) // 16
+    py, px = np.mgrid[0:16, 0:16]
+    for k in dropped:
+        t, g = int(k >> 32), int(k & 0xFFFFFFFF)
+        ty, tx = divmod(t, gx)
+        x = (tx * 16 + px).ravel().astype(np.float64)
+        y = (ty * 16 + py).ravel().astype(np.float64)
+        keep = (x < W) & (y < H)
+        mx, my = geo["means2D"][g].astype(np.float64)
+        a, b, c, op = geo["conic_opacity"][g].astype(np.float64)
+        dx, dy = mx - x[keep], my - y[keep]
+        power = -0.5 * (a * dx * dx + c * dy * dy) - b * dx * dy
+        alpha = np.minimum(0.99, op * np.exp(np.minimum(power, 0.0)))
+        assert np.all((power > 0) | (alpha < 1.0 / 255.0)), (t, g)
 
 
 def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True):
@@ -252,7 +287,7 @@ def test_c3_full_size_properties(c3):
         O.set_tile_stride(1)
     assert K == o["num_rendered"]
     assert np.array_equal(radii.cpu().numpy(), o["radii"])
-    _check_binning(out1, o, 1080, 1920)  # binning is computed in full for every tile
+    _check_binning(out1, o, 1080, 1920, dead_sample=20000)  # binning is computed in full for every tile
     gx = (1920 + 15) // 16
     mask = np.zeros((1080, 1920), bool)
     for t in range(0, gx * ((1080 + 15) // 16), stride):
