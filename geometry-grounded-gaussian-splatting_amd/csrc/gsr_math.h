@@ -104,6 +104,49 @@ __device__ inline void sh_basis(int D, float x, float y, float z, float* Y) {
 
 __device__ inline int sh_count(int D) { return (D + 1) * (D + 1); }
 
+// One Gaussian's SH row ([SHM][3] floats, coefficient-major) in registers.
+// The training layout (SHM = 16, 16-B aligned rows of 192 B) moves as 12
+// dwordx4 per lane; other layouts element by element (entries >= 3 n read 0).
+__device__ __forceinline__ bool sh_rows_vec4(const void* base, int SHM) {
+    return SHM == 16 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+}
+__device__ __forceinline__ void load_sh(const float* row, int SHM, int n, float (&v)[48]) {
+    if (sh_rows_vec4(row, SHM)) {
+        const float4* q = reinterpret_cast<const float4*>(row);
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            const float4 t = q[i];
+            v[4 * i] = t.x;
+            v[4 * i + 1] = t.y;
+            v[4 * i + 2] = t.z;
+            v[4 * i + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 48; k++) v[k] = k < 3 * n ? row[k] : 0.f;
+    }
+}
+// dL/dsh row: entry 3k + c = Y_k dL/dRGB_c for k < n, 0 beyond (all 3 * SHM
+// entries written), generated straight into the stores.
+__device__ __forceinline__ void store_sh_grad(float* row, int SHM, int n, const float (&Y)[16], float d0, float d1,
+                                              float d2) {
+    auto val = [&](int e) {
+        const int k = e / 3, c = e - 3 * (e / 3);
+        const float d = c == 0 ? d0 : (c == 1 ? d1 : d2);
+        return k < n ? Y[k] * d : 0.f;
+    };
+    if (sh_rows_vec4(row, SHM)) {
+        float4* q = reinterpret_cast<float4*>(row);
+#pragma unroll
+        for (int i = 0; i < 12; i++) q[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
+    } else {
+#pragma unroll
+        for (int e = 0; e < 48; e++)
+            if (e < 3 * SHM) row[e] = val(e);
+        for (int e = 48; e < 3 * SHM; e++) row[e] = 0.f;
+    }
+}
+
 // ---- symmetric 3x3 eigen-decomposition (cov3D_precomp path) --------------
 // The reference runs glm's Householder + QL solver (auxiliary.h:155-340); any
 // solver that returns the same eigen-pairs up to sign gives the same results,

@@ -420,14 +420,9 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         float Y[16];
         sh_basis(a.D, x, y, z, Y);
         const int n = sh_count(a.D);
-        const float* sh = a.shs + (size_t)idx * a.SHM * 3;
-        float* dsh = a.dL_dsh + (size_t)idx * a.SHM * 3;
-        for (int k = 0; k < n; k++) {
-            dsh[3 * k] = Y[k] * dR0;
-            dsh[3 * k + 1] = Y[k] * dR1;
-            dsh[3 * k + 2] = Y[k] * dR2;
-        }
-        for (int k = 3 * n; k < 3 * a.SHM; k++) dsh[k] = 0.f;
+        float sh[48];
+        load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
+        store_sh_grad(a.dL_dsh + (size_t)idx * a.SHM * 3, a.SHM, n, Y, dR0, dR1, dR2);
         // d(colour)/d(dir) per channel: dx/dy/dz (render_backward.cu:94-153)
         float gdx[3] = {0.f, 0.f, 0.f}, gdy[3] = {0.f, 0.f, 0.f}, gdz[3] = {0.f, 0.f, 0.f};
         if (a.D > 0) {

@@ -204,14 +204,18 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
         float Y[16];
         sh_basis(a.D, dx, dy, dz, Y);
         const int n = sh_count(a.D);
-        const float* sh = a.shs + (size_t)idx * a.SHM * 3;
+        float sh[48];
+        load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
         col[0] = Y[0] * sh[0];
         col[1] = Y[0] * sh[1];
         col[2] = Y[0] * sh[2];
-        for (int kk = 1; kk < n; kk++) {
-            col[0] += Y[kk] * sh[3 * kk];
-            col[1] += Y[kk] * sh[3 * kk + 1];
-            col[2] += Y[kk] * sh[3 * kk + 2];
+#pragma unroll
+        for (int kk = 1; kk < 16; kk++) {
+            if (kk < n) {
+                col[0] += Y[kk] * sh[3 * kk];
+                col[1] += Y[kk] * sh[3 * kk + 1];
+                col[2] += Y[kk] * sh[3 * kk + 2];
+            }
         }
         for (int sg = 0; sg < a.SGD; sg++) {
             const size_t o = (size_t)idx * a.SGM + sg;
