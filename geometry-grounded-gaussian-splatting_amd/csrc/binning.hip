@@ -23,12 +23,16 @@
 // Tile culling: a (Gaussian, tile) instance is emitted only when some pixel
 // centre of the tile can reach alpha >= 1/255, i.e. the opacity-aware
 // ellipse a dx^2 + 2 b dx dy + c dy^2 <= 2 ln(255 o) meets the tile's pixel
-// rectangle (tile_live; exact minimum of the quadratic over the rectangle,
-// with a margin above every rounding of the per-pixel test).  The dropped
+// rectangle (row_span: the exact span of the ellipse per tile row, with a
+// margin above every rounding of the per-pixel test).  The dropped
 // instances fail the power/alpha test at every pixel of the tile in the
 // forward and the backward, so images and gradients are unchanged; the point
 // list is the reference's with those instances removed (tested against the
 // oracle), and num_rendered stays the reference's K (the rect count).
+// No FMA contraction in this file: the live-tile spans are computed twice
+// (count, then emission) and must agree bit for bit.
+#pragma clang fp contract(off)
+
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -90,112 +94,107 @@ __device__ __forceinline__ TileRect tile_rect(float mx, float my, int r, uint32_
     return t;
 }
 
-// Per-Gaussian constants of the tile test: Q(d) = a dx^2 + 2 b dx dy + c dy^2
-// (power = -Q/2, render_forward.cu:486-487) and the threshold tau: a pixel
-// can pass alpha = min(0.99, o e^power) >= 1/255 only if Q <= tau = 2 ln(255 o).
-struct LiveTest {
-    float mx, my, a, b, c, tau, b_over_a, b_over_c;
-    bool none, all;  // no tile can pass / keep every tile (not positive definite, NaN)
+// Tile culling.  A pixel passes the reference's test alpha = min(0.99,
+// o e^power) >= 1/255 only if Q(u, v) = a u^2 + 2 b u v + c v^2 <= tau =
+// 2 ln(255 o), with (u, v) = mean - pixel centre and (a, b, c) the conic
+// (power = -Q/2, render_forward.cu:486-487).  For a tile row (pixel centres
+// v in [v_lo, v_hi]) the ellipse Q <= tau covers one interval of u: its ends
+// are the concave/convex branches u = (-b v +- sqrt(a tau - det v^2)) / a,
+// extremal at v = -+ b sqrt(tau / (c det)), so clamping that point into the
+// band gives the exact interval; the row's live tiles are those whose pixel
+// centres meet it — the same set as "the minimum of Q over the tile's pixel
+// rectangle is <= tau", with tau raised by a margin (x1.001 + 0.01) far above
+// the rounding of the per-pixel power and exp.  Non-positive-definite conics
+// keep their whole rect; o < 1/255 keeps nothing.
+struct Ellipse {
+    float mx, my, a, b, c, det, tau, vmax, kst;
+    int mode;  // 0 = interval test, 1 = whole rect, 2 = nothing
 };
-__device__ __forceinline__ LiveTest live_test(const Splat& sp) {
-    LiveTest L;
-    L.mx = sp.w0.x;
-    L.my = sp.w0.y;
-    L.a = sp.w0.z;
-    L.b = sp.w0.w;
-    L.c = sp.w1.x;
-    const float o = sp.w1.y;
-    L.none = !(255.f * o >= 1.f) && o == o;  // o < 1/255: o e^power < 1/255 everywhere
-    L.tau = 2.f * logf(fmaxf(255.f * o, 1.f));
-    L.all = !(L.a > 0.f && L.c > 0.f && L.a * L.c - L.b * L.b > 0.f) || !(L.tau == L.tau);
-    L.b_over_a = L.b / L.a;
-    L.b_over_c = L.b / L.c;
-    return L;
+__device__ __forceinline__ Ellipse make_ellipse(const float4& w0, const float4& w1) {
+    Ellipse E;
+    E.mx = w0.x;
+    E.my = w0.y;
+    E.a = w0.z;
+    E.b = w0.w;
+    E.c = w1.x;
+    const float o = w1.y;
+    E.det = E.a * E.c - E.b * E.b;
+    E.tau = 2.f * logf(fmaxf(255.f * o, 1.f)) * 1.001f + 0.01f;
+    E.vmax = sqrtf(E.a * E.tau / E.det);
+    E.kst = sqrtf(E.tau / (E.c * E.det));
+    const bool pd = E.a > 0.f && E.c > 0.f && E.det > 0.f && E.vmax == E.vmax && E.kst == E.kst;
+    E.mode = !(255.f * o >= 1.f) && o == o ? 2 : (pd ? 0 : 1);
+    return E;
 }
-// Exact minimum of the positive-definite Q over the tile's pixel-centre
-// rectangle (on an edge when the mean lies outside), compared with tau plus
-// a margin far above the rounding of the per-pixel power and exp.
-__device__ __forceinline__ bool tile_live(const LiveTest& L, uint32_t tx, uint32_t ty) {
-    if (L.all) return true;
-    if (L.none) return false;
-    const float dx_lo = L.mx - (float)(tx * kTile + kTile - 1), dx_hi = L.mx - (float)(tx * kTile);
-    const float dy_lo = L.my - (float)(ty * kTile + kTile - 1), dy_hi = L.my - (float)(ty * kTile);
-    if (dx_lo <= 0.f && dx_hi >= 0.f && dy_lo <= 0.f && dy_hi >= 0.f) return true;
-    auto q = [&](float dx, float dy) { return (L.a * dx + 2.f * L.b * dy) * dx + L.c * dy * dy; };
-    const float y0 = fminf(fmaxf(-L.b_over_c * dx_lo, dy_lo), dy_hi);
-    const float y1 = fminf(fmaxf(-L.b_over_c * dx_hi, dy_lo), dy_hi);
-    const float x0 = fminf(fmaxf(-L.b_over_a * dy_lo, dx_lo), dx_hi);
-    const float x1 = fminf(fmaxf(-L.b_over_a * dy_hi, dx_lo), dx_hi);
-    const float qmin = fminf(fminf(q(dx_lo, y0), q(dx_hi, y1)), fminf(q(x0, dy_lo), q(x1, dy_hi)));
-    const float mxd = fmaxf(fabsf(dx_lo), fabsf(dx_hi)), myd = fmaxf(fabsf(dy_lo), fabsf(dy_hi));
-    const float scale = L.a * mxd * mxd + 2.f * fabsf(L.b) * mxd * myd + L.c * myd * myd;
-    return qmin <= L.tau * 1.001f + 1e-3f + 1e-4f * scale;
+// Live tiles [*lo, *hi] of tile row ty inside rect R (false: none).
+__device__ __forceinline__ bool row_span(const Ellipse& E, const TileRect& R, uint32_t ty, uint32_t* lo,
+                                         uint32_t* hi) {
+    if (E.mode == 2) return false;
+    if (E.mode == 1) {
+        *lo = R.x0;
+        *hi = R.x1 - 1;
+        return R.x1 > R.x0;
+    }
+    const float vlo = fmaxf(E.my - (float)(ty * kTile + kTile - 1), -E.vmax);
+    const float vhi = fminf(E.my - (float)(ty * kTile), E.vmax);
+    if (vlo > vhi) return false;
+    const float vu = fminf(fmaxf(-E.b * E.kst, vlo), vhi);  // maximiser of the upper branch
+    const float vl = fminf(fmaxf(E.b * E.kst, vlo), vhi);   // minimiser of the lower branch
+    const float ia = 1.f / E.a;
+    const float umax = (-E.b * vu + sqrtf(fmaxf(E.a * E.tau - E.det * vu * vu, 0.f))) * ia;
+    const float umin = (-E.b * vl - sqrtf(fmaxf(E.a * E.tau - E.det * vl * vl, 0.f))) * ia;
+    // pixel centres x in [mx - umax, mx - umin]; tile tx holds x in [16 tx, 16 tx + 15]
+    const float xlo = E.mx - umax, xhi = E.mx - umin;
+    const int t0 = (int)ceilf((xlo - (float)(kTile - 1)) * (1.f / kTile));
+    const int t1 = (int)floorf(xhi * (1.f / kTile));
+    const int l = max(t0, (int)R.x0), h = min(t1, (int)R.x1 - 1);
+    if (l > h) return false;
+    *lo = (uint32_t)l;
+    *hi = (uint32_t)h;
+    return true;
+}
+__device__ __forceinline__ uint32_t live_count(const Ellipse& E, const TileRect& R) {
+    uint32_t n = 0, lo, hi;
+    for (uint32_t ty = R.y0; ty < R.y1; ty++)
+        if (row_span(E, R, ty, &lo, &hi)) n += hi - lo + 1;
+    return n;
 }
 
-// Splats touching more than this many tiles are tested by the whole wave
-// (one tile per lane) instead of by their own lane.
-constexpr uint32_t kCoopArea = 16;
-
-__device__ __forceinline__ float bcast(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+// Live tiles per Gaussian, in index order (coalesced reads).
+__global__ void __launch_bounds__(256)
+    live_tiles_kernel(int P, const uint32_t* __restrict__ tiles_touched, const Splat* __restrict__ splats,
+                      const int* __restrict__ radii, uint32_t gx, uint32_t gy, uint32_t* __restrict__ tiles_live) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    uint32_t live = 0;
+    if (tiles_touched[idx]) {
+        const float4 w0 = splats[idx].w0, w1 = splats[idx].w1;
+        live = live_count(make_ellipse(w0, w1), tile_rect(w0.x, w0.y, radii[idx], gx, gy));
+    }
+    tiles_live[idx] = live;
 }
-__device__ __forceinline__ uint32_t bcast(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
-// Live-tile count of each Gaussian in depth order (and its rect count).
 __global__ void __launch_bounds__(256)
     gather_counts_kernel(int P, const uint32_t* __restrict__ order, const uint32_t* __restrict__ tiles_touched,
-                         const Splat* __restrict__ splats, const int* __restrict__ radii, uint32_t gx, uint32_t gy,
-                         uint2* __restrict__ counts) {
+                         const uint32_t* __restrict__ tiles_live, uint2* __restrict__ counts) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    const bool in = q < P;
-    const uint32_t idx = in ? order[q] : 0u;
-    const uint32_t touched = in ? tiles_touched[idx] : 0u;
-    LiveTest L{};
-    TileRect R{0, 0, 0, 0};
-    if (touched) {
-        const Splat sp = splats[idx];
-        L = live_test(sp);
-        R = tile_rect(sp.w0.x, sp.w0.y, radii[idx], gx, gy);
-    }
-    uint32_t live = 0;
-    const bool big = touched > kCoopArea;
-    if (touched && !big) {
-        for (uint32_t y = R.y0; y < R.y1; y++)
-            for (uint32_t x = R.x0; x < R.x1; x++) live += tile_live(L, x, y);
-    }
-    // large footprints: the wave takes them one at a time, a tile per lane
-    unsigned long long pending = __ballot(big);
-    while (pending) {
-        const int l = __builtin_ctzll(pending);
-        pending &= pending - 1ull;
-        LiveTest B;
-        B.mx = bcast(L.mx, l), B.my = bcast(L.my, l), B.a = bcast(L.a, l), B.b = bcast(L.b, l);
-        B.c = bcast(L.c, l), B.tau = bcast(L.tau, l), B.b_over_a = bcast(L.b_over_a, l);
-        B.b_over_c = bcast(L.b_over_c, l);
-        B.none = bcast((uint32_t)L.none, l) != 0u, B.all = bcast((uint32_t)L.all, l) != 0u;
-        const uint32_t x0 = bcast(R.x0, l), y0 = bcast(R.y0, l), w = bcast(R.x1, l) - x0;
-        const uint32_t n = bcast(touched, l);
-        uint32_t tot = 0;
-        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            tot += (uint32_t)__popcll(__ballot(i < n && tile_live(B, x0 + i % w, y0 + i / w)));
-        }
-        if (lane == l) live = tot;
-    }
-    if (in) counts[q] = make_uint2(touched, live);
+    if (q >= P) return;
+    const uint32_t idx = order[q];
+    counts[q] = make_uint2(tiles_touched[idx], tiles_live[idx]);
 }
 
 hipError_t launch_depth_order(const FwdParams& p, const GeomState& gs, const int* radii, hipStream_t stream) {
     const int P = p.P;
     if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(live_tiles_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, P, gs.tiles_touched,
+                       gs.splats, radii, p.grid_x, p.grid_y, gs.tiles_live);
     size_t bytes = gs.dsort_tmp_bytes;
-    hipError_t e = rocprim::radix_sort_pairs<DepthSortConfig>(gs.dsort_tmp, bytes, reinterpret_cast<const uint32_t*>(gs.depths),
-                                             gs.depth_keys_sorted, rocprim::counting_iterator<uint32_t>(0), gs.order,
-                                             (size_t)P, 0u, 32u, stream);
+    hipError_t e = rocprim::radix_sort_pairs<DepthSortConfig>(
+        gs.dsort_tmp, bytes, reinterpret_cast<const uint32_t*>(gs.depths), gs.depth_keys_sorted,
+        rocprim::counting_iterator<uint32_t>(0), gs.order, (size_t)P, 0u, 32u, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gather_counts_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, P, gs.order,
-                       gs.tiles_touched, gs.splats, radii, p.grid_x, p.grid_y, gs.counts);
+                       gs.tiles_touched, gs.tiles_live, gs.counts);
     return hipGetLastError();
 }
 
@@ -205,9 +204,17 @@ hipError_t launch_scan(const GeomState& gs, int P, hipStream_t stream) {
     return rocprim::inclusive_scan(gs.scan_tmp, bytes, gs.counts, gs.offsets, (size_t)P, Uint2Plus(), stream);
 }
 
-// One thread per Gaussian in depth order; writes its live tiles row-major
-// (the reference's emission order within one Gaussian is irrelevant here:
-// a Gaussian lands once in each tile).
+// Gaussians with more live tiles than this are emitted by the whole wave,
+// one tile row per lane.
+constexpr uint32_t kCoopLive = 32;
+
+__device__ __forceinline__ float bcast(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ uint32_t bcast(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+
+// One thread per Gaussian in depth order writes its live tiles, row by row
+// (the order within one Gaussian is irrelevant: it lands once per tile).
 template <typename KeyT>
 __global__ void __launch_bounds__(256)
     emit_keys_kernel(int P, const uint32_t* __restrict__ order, const Splat* __restrict__ splats,
@@ -217,53 +224,62 @@ __global__ void __launch_bounds__(256)
     const int lane = threadIdx.x & 63;
     const bool in = q < P;
     const uint32_t idx = in ? order[q] : 0u;
-    const int r = in ? radii[idx] : 0;
-    uint32_t off = (!in || q == 0) ? 0u : offsets[q - 1].y;
-    LiveTest L{};
+    const uint2 o1 = in ? offsets[q] : make_uint2(0u, 0u);
+    const uint32_t off0 = (!in || q == 0) ? 0u : offsets[q - 1].y;
+    const uint32_t n = o1.y - off0;  // live tiles of this Gaussian
+    Ellipse E{};
     TileRect R{0, 0, 0, 0};
-    uint32_t area = 0;
-    if (r > 0) {
-        const Splat sp = splats[idx];
-        L = live_test(sp);
-        R = tile_rect(sp.w0.x, sp.w0.y, r, grid_x, grid_y);
-        area = (R.x1 - R.x0) * (R.y1 - R.y0);
+    if (n) {
+        const float4 w0 = splats[idx].w0, w1 = splats[idx].w1;
+        E = make_ellipse(w0, w1);
+        R = tile_rect(w0.x, w0.y, radii[idx], grid_x, grid_y);
     }
-    const bool big = area > kCoopArea;
-    if (area && !big) {
-        for (uint32_t y = R.y0; y < R.y1; y++)
-            for (uint32_t x = R.x0; x < R.x1; x++) {
-                if (!tile_live(L, x, y)) continue;
-                keys[off] = (KeyT)(y * grid_x + x);
+    const bool big = n > kCoopLive;
+    if (n && !big) {
+        uint32_t off = off0, lo, hi;
+        const uint32_t end = off0 + n;  // spans are recomputed bit-identically; never write past the count
+        for (uint32_t ty = R.y0; ty < R.y1; ty++) {
+            if (!row_span(E, R, ty, &lo, &hi)) continue;
+            for (uint32_t tx = lo; tx <= hi && off < end; tx++) {
+                keys[off] = (KeyT)(ty * grid_x + tx);
                 values[off] = idx;
                 off++;
             }
+        }
     }
-    // large footprints: the wave emits them one at a time, a tile per lane,
-    // live tiles compacted in row-major order by ballot prefix counts
+    // large footprints: one Gaussian at a time, a tile row per lane, rows
+    // placed by a wave prefix sum of their lengths
     unsigned long long pending = __ballot(big);
     while (pending) {
         const int l = __builtin_ctzll(pending);
         pending &= pending - 1ull;
-        LiveTest B;
-        B.mx = bcast(L.mx, l), B.my = bcast(L.my, l), B.a = bcast(L.a, l), B.b = bcast(L.b, l);
-        B.c = bcast(L.c, l), B.tau = bcast(L.tau, l), B.b_over_a = bcast(L.b_over_a, l);
-        B.b_over_c = bcast(L.b_over_c, l);
-        B.none = bcast((uint32_t)L.none, l) != 0u, B.all = bcast((uint32_t)L.all, l) != 0u;
-        const uint32_t x0 = bcast(R.x0, l), y0 = bcast(R.y0, l), w = bcast(R.x1, l) - x0;
-        const uint32_t n = bcast(area, l), g = bcast(idx, l);
-        uint32_t base = bcast(off, l);
-        const unsigned long long below = (1ull << lane) - 1ull;
-        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const uint32_t ty = y0 + i / w, tx = x0 + i % w;
-            const bool live = i < n && tile_live(B, tx, ty);
-            const unsigned long long m = __ballot(live);
-            if (live) {
-                const uint32_t o = base + (uint32_t)__popcll(m & below);
-                keys[o] = (KeyT)(ty * grid_x + tx);
-                values[o] = g;
+        Ellipse B;
+        B.mx = bcast(E.mx, l), B.my = bcast(E.my, l), B.a = bcast(E.a, l), B.b = bcast(E.b, l);
+        B.c = bcast(E.c, l), B.det = bcast(E.det, l), B.tau = bcast(E.tau, l), B.vmax = bcast(E.vmax, l);
+        B.kst = bcast(E.kst, l), B.mode = (int)bcast((uint32_t)E.mode, l);
+        TileRect RB;
+        RB.x0 = bcast(R.x0, l), RB.x1 = bcast(R.x1, l), RB.y0 = bcast(R.y0, l), RB.y1 = bcast(R.y1, l);
+        const uint32_t g = bcast(idx, l);
+        uint32_t base = bcast(off0, l);
+        const uint32_t end = base + bcast(n, l);
+        for (uint32_t ty0 = RB.y0; ty0 < RB.y1; ty0 += 64) {
+            const uint32_t ty = ty0 + lane;
+            uint32_t lo = 0, hi = 0, len = 0;
+            if (ty < RB.y1 && row_span(B, RB, ty, &lo, &hi)) len = hi - lo + 1;
+            // exclusive prefix of len over the wave
+            uint32_t incl = len;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += v;
             }
-            base += (uint32_t)__popcll(m);
+            uint32_t off = base + incl - len;
+            for (uint32_t tx = lo; tx < lo + len && off < end; tx++) {
+                keys[off] = (KeyT)(ty * grid_x + tx);
+                values[off] = g;
+                off++;
+            }
+            base += (uint32_t)__shfl(incl, 63, 64);
         }
     }
 }

@@ -52,6 +52,7 @@ size_t carve_geom(void* base, int P, GeomState& g) {
     g.tiles_touched = c.take<uint32_t>(P);
     g.order = c.take<uint32_t>(P);
     g.depth_keys_sorted = c.take<uint32_t>(P);
+    g.tiles_live = c.take<uint32_t>(P);
     g.counts = c.take<uint2>(P);
     g.offsets = c.take<uint2>(P);
     g.radii = c.take<int>(P);

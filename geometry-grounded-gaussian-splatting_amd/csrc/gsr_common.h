@@ -67,6 +67,7 @@ struct GeomState {
     uint32_t* tiles_touched;
     uint32_t* order;              // Gaussian indices in (depth bits, index) order
     uint32_t* depth_keys_sorted;  // sorted depth bit patterns (sort output, unused after)
+    uint32_t* tiles_live;         // tiles of the rect that pass the tile test (binning.hip)
     uint2* counts;                // per Gaussian in depth order: (tiles_touched, live tiles)
     uint2* offsets;               // inclusive scan of counts: .x -> K (reference count), .y -> live instances
     int* radii;                   // internal copy when the caller passes radii == NULL
