@@ -61,26 +61,26 @@ def parse():
     return ap.parse_args()
 
 
-def stage_bytes(P, K, HW, shm, sgm, geom, tiles):
+def stage_bytes(P, K, K_live, HW, shm, sgm, geom):
     """Algorithmic (compulsory) HBM bytes per launch of each stage, from the
-    per-unit figures of SURVEY.md §8(d), with the binning terms of this
-    build's pipeline (depth order of P, 16-bit tile keys)."""
+    per-unit figures of SURVEY.md §8(d).  K is the reference's instance count
+    (rect tiles); the stages after binning process the K_live instances that
+    survive tile culling, so their unit count is K_live."""
     Bp = 44 + 12 * shm + 28 * sgm
     G = 64 if geom else 36
     Opx = 36 if geom else 20
     Ipx = 56 if geom else 24
     A = 68 if geom else 40
-    kb = 2 if tiles <= 65536 else 4
     return {
         "preprocess": P * (Bp + 80),
-        "depth_order": P * 28,  # depth bits in, (key, index) out, tiles_touched gathered into depth order
-        "scan": P * 8,
-        "emit_keys": P * 28 + K * (kb + 4),
-        "sort": K * (kb + 4) * 2,
-        "tile_ranges": K * kb + tiles * 8,
-        "render_fwd": K * (4 + G) + HW * Opx,
+        "depth_order": P * 36,  # splat rect/conic read, depth sort (key, index) in and out, counts gathered
+        "scan": P * 16,
+        "emit_keys": P * 36 + K_live * 6,
+        "sort": K_live * 12,
+        "tile_ranges": K_live * 2,
+        "render_fwd": K_live * (4 + G) + HW * Opx,
         "bwd_clear": P * A,
-        "render_bwd": HW * Ipx + K * (4 + G),
+        "render_bwd": HW * Ipx + K_live * (4 + G),
         "preprocess_bwd": P * (A + Bp + 8 + Bp),
     }
 
@@ -223,6 +223,14 @@ def main():
                                    params["sg_axis"], params["sg_sharpness"], params["sg_color"], args.sh_degree,
                                    args.sg_degree, 1.0, cam.world_view_transform, cam.full_proj_transform, tanx,
                                    tany, 0.0, H, W, cam.camera_center, False, geom, False)[0]
+    # instances that survive tile culling (the units the raster kernels process)
+    with torch.no_grad():
+        fo = _C.rasterize_gaussians(settings.bg, params["means3D"], torch.Tensor([]), params["opacities"],
+                                    params["scales"], params["rotations"], torch.Tensor([]), params["shs"],
+                                    params["sg_axis"], params["sg_sharpness"], params["sg_color"], args.sh_degree,
+                                    args.sg_degree, 1.0, cam.world_view_transform, cam.full_proj_transform, tanx,
+                                    tany, 0.0, H, W, cam.camera_center, False, geom, False)
+        K_live = int(_C.debug_binning(fo[7], fo[9], fo[0], H, W, with_list=False)[1][:, 1].max())
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.steps / elapsed
     shm = (args.sh_degree + 1) ** 2
@@ -251,7 +259,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": workload, "P": P, "width": W, "height": H, "sh_degree": args.sh_degree,
-                       "sg_degree": args.sg_degree, "require_depth": geom, "num_rendered": int(K),
+                       "sg_degree": args.sg_degree, "require_depth": geom, "num_rendered": int(K), "instances_after_tile_culling": K_live,
                        "parallelism": f"view-parallel dp{world}" if world > 1 else "single",
                        "step_algorithmic_GBps": round(total_algo / (ms_per_step * 1e-3) / 1e9, 2)},
             "roofline": roofline,

@@ -82,18 +82,20 @@ def debug_render_stats(reset: bool = True) -> list:
     return list(out)
 
 
-def debug_binning(binningBuffer, tileBuffer, R: int, image_height: int, image_width: int):
+def debug_binning(binningBuffer, tileBuffer, R: int, image_height: int, image_width: int, with_list: bool = True):
     """(point_list [R] uint32, ranges [tiles, 2] uint32) of a forward's buffers
-    (gsr_debug_binning), as numpy arrays."""
+    (gsr_debug_binning), as numpy arrays.  The per-tile lists hold only the
+    instances that survive tile culling: their count is ranges[:, 1].max(),
+    R (= num_rendered, the reference's K) is the capacity."""
     import numpy as np
 
     tiles = ((image_width + 15) // 16) * ((image_height + 15) // 16)
-    plist = np.zeros(max(R, 0), np.uint32)
+    plist = np.zeros(max(R, 0) if with_list else 0, np.uint32)
     ranges = np.zeros((tiles, 2), np.uint32)
     stream = torch.cuda.current_stream(binningBuffer.device).cuda_stream
     _check(_load().gsr_debug_binning(ctypes.c_void_p(binningBuffer.data_ptr()),
                                      ctypes.c_void_p(tileBuffer.data_ptr()), int(R), int(image_width),
-                                     int(image_height), plist.ctypes.data_as(ctypes.c_void_p),
+                                     int(image_height), plist.ctypes.data_as(ctypes.c_void_p) if with_list else None,
                                      ranges.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream)))
     return plist, ranges
 

@@ -37,7 +37,7 @@ def stage_of(name: str) -> str | None:
         return "render_fwd"
     if "render_bwd_kernel" in n:
         return "render_bwd"
-    if "gather_counts_kernel" in n:
+    if "gather_counts_kernel" in n or "live_tiles_kernel" in n:
         return "depth_order"
     if "radix_sort" in n or "onesweep" in n or "merge_sort" in n:
         # rocPRIM kernels are named by key/value types: the tile sort has
