@@ -53,6 +53,7 @@ struct RenderFwdArgs {
     float* out_alpha;
     float* out_normal;
     float* out_mdepth;
+    int passes;  // bisection passes (kSplitIterations; fewer only for GSR_OPT_BISECT_PASSES timing runs)
 };
 
 // One contributor's factor on the bisection samples (render_forward.cu:610-621):
@@ -64,9 +65,9 @@ struct RenderFwdArgs {
 // ulp; both products stay >= the pixel's final transmittance >= 1e-4, so
 // nothing underflows).  Samples are evaluated two at a time with packed
 // fp32 (v_pk_{add,mul,fma}_f32), and
-//  * exp(-delta^2/2) = exp2(round(delta*delta) * (-0.5 * log2e)): __expf is
-//    v_exp_f32(x * log2e) and scaling by -0.5 is exact, so the product folds
-//    into one constant;
+//  * exp(-delta^2/2) = exp2((d d) k) with d = ts - t_peak and
+//    k = (rsigma rsigma)(-0.5 log2e) per contributor: one packed multiply
+//    less per sample pair than ((d rsigma)^2)(-0.5 log2e) (a few ulp apart);
 //  * a non-ball splat (rsigma <= 0, g = 0 in the reference) runs with
 //    alpha_g = 0 and rsigma = 0: delta = 0, g = 1, 1 - 0*g = 1 exactly.
 // Exact shortcut (SKIP): when every sample of the window has |delta| > 7,
@@ -76,50 +77,41 @@ struct RenderFwdArgs {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float kHalfNegLog2e = -0.5f * 1.44269502162933349609375f;  // -0.5 * (float)log2(e), exact
 
-template <bool FIRST, bool SKIP>
-__device__ __forceinline__ void bisect_step(float (&A)[kSplit + 1], float (&B)[kSplit + 1],
-                                            const float (&ts)[kSplit + 1], float alpha, float t_peak, float rsig) {
-    constexpr int START = FIRST ? 0 : 1;
-    constexpr int END = FIRST ? kSplit + 1 : kSplit;
+// Samples live in packed register pairs: pair k holds samples START + 2k and
+// START + 2k + 1 (an odd count repeats the last sample in the spare half), so
+// every v_pk_* operand is already an aligned pair and no lane-moves are
+// needed to feed them.
+template <int NP, bool SKIP>
+__device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], const f32x2 (&TS)[NP], float alpha,
+                                            float t_peak, float rsig) {
     const bool ball = rsig > 0.f;
     const float om = 1.f - alpha;
+    const f32x2 om2 = {om, om};
     if constexpr (SKIP) {
-        const float d_lo = (ts[START] - t_peak) * rsig;
-        const float d_hi = (ts[END - 1] - t_peak) * rsig;
+        const float d_lo = (TS[0].x - t_peak) * rsig;
+        const float d_hi = (TS[NP - 1].y - t_peak) * rsig;
         if (ball && d_lo > 7.f) {
 #pragma unroll
-            for (int s = START; s < END; s++) A[s] *= om;
+            for (int k = 0; k < NP; k++) A[k] *= om2;
             return;
         }
         if (ball && d_hi < -7.f) return;
     }
     const float ag = ball ? alpha : 0.f;
     const float rg = ball ? rsig : 0.f;
-    const f32x2 ag2 = {ag, ag}, rg2 = {rg, rg}, tp2 = {t_peak, t_peak};
-    const f32x2 c2 = {kHalfNegLog2e, kHalfNegLog2e}, one2 = {1.f, 1.f};
+    const float kk = (rg * rg) * kHalfNegLog2e;
+    const f32x2 ag2 = {ag, ag}, kk2 = {kk, kk}, tp2 = {t_peak, t_peak};
+    const f32x2 one2 = {1.f, 1.f};
 #pragma unroll
-    for (int s = START; s + 1 < END; s += 2) {
-        const f32x2 t = {ts[s], ts[s + 1]};
-        const f32x2 delta = (t - tp2) * rg2;
-        const f32x2 e = (delta * delta) * c2;
+    for (int k = 0; k < NP; k++) {
+        const f32x2 t = TS[k];
+        const f32x2 d = t - tp2;
+        const f32x2 e = (d * d) * kk2;
         const f32x2 g = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
         const f32x2 omg = __builtin_elementwise_fma(-ag2, g, one2);
         const f32x2 sel = {t.x > t_peak ? om : omg.x, t.y > t_peak ? om : omg.y};
-        f32x2 A2 = {A[s], A[s + 1]}, B2 = {B[s], B[s + 1]};
-        A2 *= sel;
-        B2 *= omg;
-        A[s] = A2.x;
-        A[s + 1] = A2.y;
-        B[s] = B2.x;
-        B[s + 1] = B2.y;
-    }
-    if constexpr (((END - START) & 1) != 0) {
-        constexpr int s = END - 1;
-        const float delta = (ts[s] - t_peak) * rg;
-        const float g = __builtin_amdgcn_exp2f((delta * delta) * kHalfNegLog2e);
-        const float omg = __builtin_fmaf(-ag, g, 1.f);
-        A[s] *= ts[s] > t_peak ? om : omg;
-        B[s] *= omg;
+        A[k] *= sel;
+        B[k] *= omg;
     }
 }
 
@@ -243,7 +235,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     float mDepth = 0.f;
     if constexpr (GEOM) {
         unsigned long long st[4] = {0, 0, 0, 0};
-        float Tp[kSplit + 1], A[kSplit + 1], B[kSplit + 1];
+        float Tp[kSplit + 1];
         float dmin = fmaxf(m_init - kSampleRange, 0.f);
         float dmax = fmaxf(m_init + kSampleRange, 0.f);
         bool in_range = T <= kMinTransmittance;
@@ -268,26 +260,48 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         }
         // one bisection pass; FIRST evaluates all 9 samples, later passes
         // reuse the bracketing ends (render_forward.cu:560-645)
-        auto pass = [&](auto first_c) {
+        // Contributors whose whole pass-2 window lies more than 7 sigma from
+        // their peak have exactly constant factors in passes 3-5 (their
+        // windows nest inside it; see bisect_step SKIP): pass 2 drops them
+        // from the lane's mask and folds the (1 - a) of those behind the
+        // window into far_A, the starting value of A in passes 3-5.
+        float far_A = 1.f;
+        auto pass = [&](auto first_c, bool prune) {
             constexpr bool FIRST = decltype(first_c)::value;
             constexpr int START = FIRST ? 0 : 1;
             constexpr int END = FIRST ? kSplit + 1 : kSplit;
-#pragma unroll
-            for (int s = START; s < END; s++) A[s] = B[s] = 1.f;
+            constexpr int NP = (END - START + 1) / 2;
+            const float a0 = FIRST || prune ? 1.f : far_A;
             const float interval = (dmax - dmin) * (1.f / (float)kSplit);
             float ts[kSplit + 1];
 #pragma unroll
             for (int s = 0; s <= kSplit; s++) ts[s] = __builtin_fmaf(interval, (float)s, dmin);
+            f32x2 A[NP], B[NP], TS[NP];
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                const int s0 = START + 2 * k, s1 = s0 + 1 < END ? s0 + 1 : s0;
+                TS[k] = f32x2{ts[s0], ts[s1]};
+                A[k] = f32x2{a0, a0};
+                B[k] = f32x2{1.f, 1.f};
+            }
             if (resident) {
                 // per-lane walk over the blended contributors, increasing index
                 // (same multiplication order as the reference's c = 1..last loop)
                 const int nwords = in_range ? (int)((last + 31) >> 5) : 0;
                 int w = 0;
                 uint32_t bits = nwords ? my_mask[0] : 0u;
+                uint32_t keep = 0u;  // (prune) near contributors of word w
                 while (true) {
-                    while (bits == 0u && w + 1 < nwords) bits = my_mask[++w * kTilePixels];
+                    while (bits == 0u && w + 1 < nwords) {
+                        if (prune) {
+                            my_mask[w * kTilePixels] = keep;
+                            keep = 0u;
+                        }
+                        bits = my_mask[++w * kTilePixels];
+                    }
                     if (bits == 0u) break;
                     const int j = (w << 5) + __builtin_ctz(bits);
+                    const uint32_t jbit = bits & (0u - bits);
                     bits &= bits - 1u;
                     if constexpr (STATS) {
                         const unsigned long long m = __ballot(1);
@@ -314,8 +328,16 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                             st[3] += __popcll(fm);
                         }
                     }
-                    bisect_step<FIRST, SKIP>(A, B, ts, alpha, t_peak, w2.y);
+                    if (!FIRST && prune) {
+                        const bool ball = w2.y > 0.f;
+                        const bool behind = ball && (ts[0] - t_peak) * w2.y > 7.f;
+                        const bool front = ball && (ts[kSplit] - t_peak) * w2.y < -7.f;
+                        far_A *= behind ? 1.f - alpha : 1.f;
+                        keep |= (behind || front) ? 0u : jbit;
+                    }
+                    bisect_step<NP, SKIP>(A, B, TS, alpha, t_peak, w2.y);
                 }
+                if (prune && nwords) my_mask[w * kTilePixels] = keep;
             } else {
                 bool bdone = !in_range;
                 uint32_t c = 0;
@@ -336,12 +358,15 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                         if (alpha < 1.0f / 255.0f) continue;
                         const float4 w2 = c_w2[j];
                         const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                        bisect_step<FIRST, SKIP>(A, B, ts, alpha, t_peak, w2.y);
+                        bisect_step<NP, SKIP>(A, B, TS, alpha, t_peak, w2.y);
                     }
                 }
             }
 #pragma unroll
-            for (int s = START; s < END; s++) Tp[s] = A[s] * __builtin_amdgcn_rsqf(B[s]);
+            for (int k = 0; k < NP; k++) {
+                Tp[START + 2 * k] = A[k].x * __builtin_amdgcn_rsqf(B[k].x);
+                if (START + 2 * k + 1 < END) Tp[START + 2 * k + 1] = A[k].y * __builtin_amdgcn_rsqf(B[k].y);
+            }
             if (FIRST) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
             int start_id = 0;
 #pragma unroll
@@ -358,9 +383,9 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             Tp[0] = lo;
             Tp[kSplit] = hi;
         };
-        pass(std::true_type{});
+        if (a.passes > 0) pass(std::true_type{}, false);
 #pragma unroll 1
-        for (int it = 1; it < kSplitIterations; it++) pass(std::false_type{});
+        for (int it = 1; it < a.passes; it++) pass(std::false_type{}, it == 1);
         if constexpr (STATS) {
             for (int q = 0; q < 4; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
@@ -418,6 +443,11 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.out_alpha = out_alpha;
     a.out_normal = out_normal;
     a.out_mdepth = out_mdepth;
+    {
+        const int np = option(kOptBisectPasses);
+        a.passes = (np > 0 && np < kSplitIterations) ? np : kSplitIterations;
+        if (np < 0) a.passes = 0;
+    }
     if (a.num_tiles == 0) return hipSuccess;
     if (p.require_depth) {
         if (option(kOptRenderStats))

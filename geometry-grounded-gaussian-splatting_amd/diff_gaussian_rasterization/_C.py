@@ -73,6 +73,7 @@ KEEP_BWD_SCRATCH = False
 last_bwd_scratch = None
 OPT_BISECT_SKIP = 0
 OPT_RENDER_STATS = 1
+OPT_BISECT_PASSES = 2
 
 
 def debug_render_stats(reset: bool = True) -> list:

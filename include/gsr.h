@@ -131,7 +131,9 @@ const char* gsr_stage_name(int stage);
  * samples far from a Gaussian's ray peak (render_fwd.hip; slower on the
  * fog-like benchmark scene, where most samples are near a peak).
  */
-enum gsr_option { GSR_OPT_BISECT_SKIP = 0, GSR_OPT_RENDER_STATS = 1 };
+/* GSR_OPT_BISECT_PASSES (diagnostic, default 0 = all 5): run only n median-depth
+ * bisection passes (n < 0: none) to time them; median depth is then wrong. */
+enum gsr_option { GSR_OPT_BISECT_SKIP = 0, GSR_OPT_RENDER_STATS = 1, GSR_OPT_BISECT_PASSES = 2 };
 int gsr_set_option(int opt, int value);
 /* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (8 values, see render_fwd.hip). */
 int gsr_debug_render_stats(unsigned long long* out8, int reset);

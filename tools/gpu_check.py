@@ -61,17 +61,11 @@ if __name__ == "__main__":
     print("stats per forward (4 calls):", [v / 4 for v in st[:4]],
           "lanes/step=%.1f far-frac passes2-5=%.3f" % (st[1] / max(st[0], 1), st[3] / max(st[2], 1)))
     run(20000, 320, 240)
-    for opt in (0, 1):
-        _C.set_option(_C.OPT_BISECT_SKIP, opt)
-        print("bisect skip", opt)
-        bench(require_depth=True)
+    for npass in (-1, 1, 2, 3, 4, 0):
+        _C.set_option(_C.OPT_BISECT_PASSES, npass)
         _C.timing_enable(True)
         bench(require_depth=True, iters=5)
         _C.timing_enable(False)
-        print({k: round(v[0] / max(v[1], 1), 3) for k, v in _C.timing_collect().items()})
-    _C.set_option(_C.OPT_BISECT_SKIP, 0)
-    bench(require_depth=False)
-    _C.timing_enable(True)
-    bench(require_depth=False, iters=5)
-    _C.timing_enable(False)
-    print({k: round(v[0] / max(v[1], 1), 3) for k, v in _C.timing_collect().items()})
+        st = _C.timing_collect()
+        print("bisection passes", npass, "render_fwd ms", round(st["render_fwd"][0] / max(st["render_fwd"][1], 1), 3))
+    _C.set_option(_C.OPT_BISECT_PASSES, 0)
