@@ -77,29 +77,30 @@ struct RenderFwdArgs {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float kHalfNegLog2e = -0.5f * 1.44269502162933349609375f;  // -0.5 * (float)log2(e), exact
 
-// Samples live in packed register pairs: pair k holds samples START + 2k and
-// START + 2k + 1 (an odd count repeats the last sample in the spare half), so
-// every v_pk_* operand is already an aligned pair and no lane-moves are
-// needed to feed them.
-template <int NP, bool SKIP>
-__device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], const f32x2 (&TS)[NP], float alpha,
-                                            float t_peak, float rsig) {
-    const bool ball = rsig > 0.f;
+// Samples live in packed register pairs (pair k holds samples START + 2k and
+// START + 2k + 1, so every v_pk_* operand is an aligned pair and no lane
+// moves feed them); an odd count leaves one scalar sample (A1, B1 at T1).
+// Per contributor the staged record supplies k = rsigma^2 (-0.5 log2e) and
+// the ball flag bm (1 or 0), so a_g = alpha bm and e = (d d) k.
+template <int NP, bool HAS1, bool SKIP>
+__device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], const f32x2 (&TS)[NP], float& A1,
+                                            float& B1, float T1, float alpha, float t_peak, float rsig, float kk,
+                                            float bm) {
     const float om = 1.f - alpha;
     const f32x2 om2 = {om, om};
     if constexpr (SKIP) {
+        const bool ball = rsig > 0.f;
         const float d_lo = (TS[0].x - t_peak) * rsig;
-        const float d_hi = (TS[NP - 1].y - t_peak) * rsig;
+        const float d_hi = ((HAS1 ? T1 : TS[NP - 1].y) - t_peak) * rsig;
         if (ball && d_lo > 7.f) {
 #pragma unroll
             for (int k = 0; k < NP; k++) A[k] *= om2;
+            if constexpr (HAS1) A1 *= om;
             return;
         }
         if (ball && d_hi < -7.f) return;
     }
-    const float ag = ball ? alpha : 0.f;
-    const float rg = ball ? rsig : 0.f;
-    const float kk = (rg * rg) * kHalfNegLog2e;
+    const float ag = alpha * bm;
     const f32x2 ag2 = {ag, ag}, kk2 = {kk, kk}, tp2 = {t_peak, t_peak};
     const f32x2 one2 = {1.f, 1.f};
 #pragma unroll
@@ -112,6 +113,13 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
         const f32x2 sel = {t.x > t_peak ? om : omg.x, t.y > t_peak ? om : omg.y};
         A[k] *= sel;
         B[k] *= omg;
+    }
+    if constexpr (HAS1) {
+        const float d = T1 - t_peak;
+        const float g = __builtin_amdgcn_exp2f((d * d) * kk);
+        const float omg = __builtin_fmaf(-ag, g, 1.f);
+        A1 *= T1 > t_peak ? om : omg;
+        B1 *= omg;
     }
 }
 
@@ -250,7 +258,9 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 const Splat* sp = a.splats + a.point_list[range.x + c0 + k];
                 c_w0[k] = sp->w0;
                 c_w1[k] = sp->w1;
-                c_w2[k] = sp->w2;
+                const float4 w2 = sp->w2;
+                const bool ball = w2.y > 0.f;  // non-ball splats: g = 0 (bisect_step)
+                c_w2[k] = make_float4(w2.x, w2.y, ball ? (w2.y * w2.y) * kHalfNegLog2e : 0.f, ball ? 1.f : 0.f);
             }
         };
         if (resident && max_contrib > 0) {
@@ -266,11 +276,13 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         // from the lane's mask and folds the (1 - a) of those behind the
         // window into far_A, the starting value of A in passes 3-5.
         float far_A = 1.f;
-        auto pass = [&](auto first_c, bool prune) {
+        auto pass = [&](auto first_c, auto prune_c) {
             constexpr bool FIRST = decltype(first_c)::value;
+            constexpr bool prune = decltype(prune_c)::value;
             constexpr int START = FIRST ? 0 : 1;
             constexpr int END = FIRST ? kSplit + 1 : kSplit;
-            constexpr int NP = (END - START + 1) / 2;
+            constexpr int NP = (END - START) / 2;
+            constexpr bool HAS1 = ((END - START) & 1) != 0;
             const float a0 = FIRST || prune ? 1.f : far_A;
             const float interval = (dmax - dmin) * (1.f / (float)kSplit);
             float ts[kSplit + 1];
@@ -279,11 +291,12 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             f32x2 A[NP], B[NP], TS[NP];
 #pragma unroll
             for (int k = 0; k < NP; k++) {
-                const int s0 = START + 2 * k, s1 = s0 + 1 < END ? s0 + 1 : s0;
-                TS[k] = f32x2{ts[s0], ts[s1]};
+                TS[k] = f32x2{ts[START + 2 * k], ts[START + 2 * k + 1]};
                 A[k] = f32x2{a0, a0};
                 B[k] = f32x2{1.f, 1.f};
             }
+            float A1 = a0, B1 = 1.f;
+            const float T1 = ts[END - 1];
             if (resident) {
                 // per-lane walk over the blended contributors, increasing index
                 // (same multiplication order as the reference's c = 1..last loop)
@@ -293,7 +306,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 uint32_t keep = 0u;  // (prune) near contributors of word w
                 while (true) {
                     while (bits == 0u && w + 1 < nwords) {
-                        if (prune) {
+                        if constexpr (prune) {
                             my_mask[w * kTilePixels] = keep;
                             keep = 0u;
                         }
@@ -328,16 +341,18 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                             st[3] += __popcll(fm);
                         }
                     }
-                    if (!FIRST && prune) {
+                    if constexpr (!FIRST && prune) {
                         const bool ball = w2.y > 0.f;
                         const bool behind = ball && (ts[0] - t_peak) * w2.y > 7.f;
                         const bool front = ball && (ts[kSplit] - t_peak) * w2.y < -7.f;
                         far_A *= behind ? 1.f - alpha : 1.f;
                         keep |= (behind || front) ? 0u : jbit;
                     }
-                    bisect_step<NP, SKIP>(A, B, TS, alpha, t_peak, w2.y);
+                    bisect_step<NP, HAS1, SKIP>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
                 }
-                if (prune && nwords) my_mask[w * kTilePixels] = keep;
+                if constexpr (prune) {
+                    if (nwords) my_mask[w * kTilePixels] = keep;
+                }
             } else {
                 bool bdone = !in_range;
                 uint32_t c = 0;
@@ -358,15 +373,16 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                         if (alpha < 1.0f / 255.0f) continue;
                         const float4 w2 = c_w2[j];
                         const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                        bisect_step<NP, SKIP>(A, B, TS, alpha, t_peak, w2.y);
+                        bisect_step<NP, HAS1, SKIP>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
                     }
                 }
             }
 #pragma unroll
             for (int k = 0; k < NP; k++) {
                 Tp[START + 2 * k] = A[k].x * __builtin_amdgcn_rsqf(B[k].x);
-                if (START + 2 * k + 1 < END) Tp[START + 2 * k + 1] = A[k].y * __builtin_amdgcn_rsqf(B[k].y);
+                Tp[START + 2 * k + 1] = A[k].y * __builtin_amdgcn_rsqf(B[k].y);
             }
+            if constexpr (HAS1) Tp[END - 1] = A1 * __builtin_amdgcn_rsqf(B1);
             if (FIRST) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
             int start_id = 0;
 #pragma unroll
@@ -383,9 +399,10 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             Tp[0] = lo;
             Tp[kSplit] = hi;
         };
-        if (a.passes > 0) pass(std::true_type{}, false);
+        if (a.passes > 0) pass(std::true_type{}, std::false_type{});
+        if (a.passes > 1) pass(std::false_type{}, std::true_type{});
 #pragma unroll 1
-        for (int it = 1; it < a.passes; it++) pass(std::false_type{}, it == 1);
+        for (int it = 2; it < a.passes; it++) pass(std::false_type{}, std::false_type{});
         if constexpr (STATS) {
             for (int q = 0; q < 4; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
