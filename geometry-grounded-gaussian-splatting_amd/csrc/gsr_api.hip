@@ -79,6 +79,8 @@ size_t carve_binning(void* base, int K, int tile_bits, BinningState& b) {
 size_t carve_image(void* base, int HW, ImageState& s) {
     Carver c(base);
     s.n_contrib = c.take<uint32_t>(HW);
+    s.dT_dtm = c.take<float>(HW);
+    s.md_check = c.take<uint32_t>(HW);
     return c.off + 256;
 }
 

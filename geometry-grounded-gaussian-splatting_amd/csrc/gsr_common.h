@@ -92,7 +92,10 @@ struct BinningState {
 // ---- per-pixel / per-tile state (ImageState, TileState<false>) ----
 struct ImageState {
     uint32_t* n_contrib;
+    float* dT_dtm;       // GEOM: median-depth implicit derivative, computed by the forward
+    uint32_t* md_check;  // bits of the mdepth output it belongs to (NaN pattern: not cached)
 };
+constexpr uint32_t kNoCache = 0x7fffffffu;
 struct TileState {
     uint2* ranges;
     uint32_t* max_contrib;
@@ -213,6 +216,16 @@ __device__ inline uint32_t xcd_remap(uint32_t b, uint32_t n) {
 // outputs are checked bit-exactly against the oracle).
 __device__ __forceinline__ float fast_rcp(float b) { return __builtin_amdgcn_rcpf(b); }
 __device__ __forceinline__ float fast_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+
+// Length of the ray (pnx, pny, 1) through pixel (px, py): the median depth
+// is stored divided by it (render_forward.cu:651-653) and multiplied back in
+// the backward (render_backward.cu:813-816); one rounding sequence for both.
+__device__ __forceinline__ float pixel_ray_norm(float px, float py, int W, int H, float fx, float fy) {
+#pragma clang fp contract(off)
+    const float pnx = (px - (float)(W - 1) / 2.f) / fx;
+    const float pny = (py - (float)(H - 1) / 2.f) / fy;
+    return sqrtf(pnx * pnx + pny * pny + 1.f);
+}
 
 // Footprint of a splat record at a pixel offset (dx, dy) = (mean - pixel):
 //   power  = -0.5 (a dx^2 + c dy^2) - b dx dy   (render_forward.cu:486-487)

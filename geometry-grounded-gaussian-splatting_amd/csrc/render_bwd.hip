@@ -23,6 +23,8 @@ struct RenderBwdArgs {
     const uint32_t* point_list;
     const Splat* splats;
     const uint32_t* n_contrib;
+    const float* dT_dtm;
+    const uint32_t* md_check;
     const uint32_t* max_contrib;
     int W, H;
     uint32_t grid_x, num_tiles;
@@ -37,6 +39,7 @@ struct RenderBwdArgs {
     const float* dL_dnormal;
     float* acc;      // [P][16]
     float* acc_abs;  // [P]
+    int skip_prepass;  // diagnostic (GSR_OPT_BWD_NO_PREPASS): time the kernel without the pre-pass
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -64,9 +67,9 @@ __device__ __forceinline__ f2 splat_tpeak2(const float4& w1, const float4& w2, f
 
 // Per-pixel inputs of the backward (render_backward.cu:771-833).
 struct PixIn {
-    bool inside;
+    bool inside, cached;
     uint32_t last;
-    float T_final, dLp0, dLp1, dLp2, dL_dfinalT, dLn0, dLn1, dLn2, mDepth, dL_dmt;
+    float T_final, dLp0, dLp1, dLp2, dL_dfinalT, dLn0, dLn1, dLn2, mDepth, dL_dmt, dT_dtm;
 };
 
 template <bool GEOM>
@@ -87,15 +90,17 @@ __device__ __forceinline__ PixIn load_pixel(const RenderBwdArgs& a, int px, int 
     r.dL_dfinalT = -a.dL_dalpha[pix] + a.bg[0] * r.dLp0 + a.bg[1] * r.dLp1 + a.bg[2] * r.dLp2;
     if constexpr (GEOM) {
         const float inv_w = 1.f / w_final;
-        const float pnx = ((float)px - (float)(a.W - 1) / 2.f) / a.focal_x;
-        const float pny = ((float)py - (float)(a.H - 1) / 2.f) / a.focal_y;
-        const float nrm = sqrtf(pnx * pnx + pny * pny + 1.f);
+        const float nrm = pixel_ray_norm((float)px, (float)py, a.W, a.H, a.focal_x, a.focal_y);
         r.dL_dmt = a.dL_dmdepth[pix] * (1.0f / nrm);
         r.dLn0 = a.dL_dnormal[pix] * inv_w;
         r.dLn1 = a.dL_dnormal[HW + pix] * inv_w;
         r.dLn2 = a.dL_dnormal[2 * HW + pix] * inv_w;
         r.dL_dfinalT += r.dLn0 * a.normalmap[pix] + r.dLn1 * a.normalmap[HW + pix] + r.dLn2 * a.normalmap[2 * HW + pix];
-        r.mDepth = a.mdepth[pix] * nrm;
+        const float md = a.mdepth[pix];
+        r.mDepth = md * nrm;
+        // the forward computed dT/dt_m for exactly this mdepth value
+        r.cached = a.md_check[pix] == __float_as_uint(md);
+        r.dT_dtm = a.dT_dtm[pix];
     }
     return r;
 }
@@ -148,15 +153,19 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
     };
 
     // ---- median-depth implicit gradient pre-pass (render_backward.cu:835-880)
+    // Pixels whose mdepth is the forward's own output take dT/dt_m from the
+    // forward (render_fwd.hip); the others (an mdepth the caller changed, a
+    // tile too long for the forward's LDS cache) recompute it here.
     f2 kappa = {0.f, 0.f};
-    if constexpr (GEOM) {
-        f2 dT_dtm = {0.f, 0.f};
-        const bool on_a = ina && pa.mDepth != 0.f && last_a != 0;
-        const bool on_b = inb && pb.mDepth != 0.f && last_b != 0;
+    if (GEOM && !a.skip_prepass) {
+        f2 dT_dtm = {pa.cached ? pa.dT_dtm : 0.f, pb.cached ? pb.dT_dtm : 0.f};
+        const bool on_a = ina && pa.mDepth != 0.f && last_a != 0 && !pa.cached;
+        const bool on_b = inb && pb.mDepth != 0.f && last_b != 0 && !pb.cached;
         const uint32_t wave_last = wave_max_u(max(on_a ? last_a : 0u, on_b ? last_b : 0u));
+        const bool block_needs = __syncthreads_or(wave_last != 0u);
         uint32_t c = 0;
         int toDo = max_contrib;
-        for (int i = 0; i < rounds; i++, toDo -= kBwdBatch) {
+        for (int i = 0; block_needs && i < rounds; i++, toDo -= kBwdBatch) {
             __syncthreads();
             stage_fwd(i);
             __syncthreads();
@@ -323,6 +332,8 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.point_list = bs.point_list;
     a.splats = gs.splats;
     a.n_contrib = is.n_contrib;
+    a.dT_dtm = is.dT_dtm;
+    a.md_check = is.md_check;
     a.max_contrib = ts.max_contrib;
     a.W = p.W;
     a.H = p.H;
@@ -340,6 +351,7 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.dL_dnormal = b.dL_dnormal;
     a.acc = ws.acc;
     a.acc_abs = ws.acc_abs;
+    a.skip_prepass = option(kOptBwdNoPrepass);
     if (a.num_tiles == 0) return hipSuccess;
     if (p.require_depth)
         hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(a.num_tiles), dim3(kBwdThreads), 0, stream, a);

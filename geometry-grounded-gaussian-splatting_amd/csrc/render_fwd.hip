@@ -36,6 +36,7 @@
 namespace gsr {
 
 constexpr int kResident = 384;
+constexpr bool kPruneAfterPass2 = true;  // measured: 1.98 vs 2.18 ms render_fwd at C3
 constexpr int kMaskWords = kResident / 32;
 constexpr int kRecSlots = 3 * kResident > 4 * kTilePixels ? 3 * kResident : 4 * kTilePixels;
 
@@ -48,6 +49,8 @@ struct RenderFwdArgs {
     float focal_x, focal_y;
     const float* bg;
     uint32_t* n_contrib;
+    float* dT_dtm;
+    uint32_t* md_check;
     uint32_t* max_contrib;
     float* out_color;
     float* out_alpha;
@@ -240,7 +243,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     __syncthreads();
     const uint32_t max_contrib = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
 
-    float mDepth = 0.f;
+    float mDepth = 0.f, md_out = 0.f, md_dT = 0.f;
+    bool md_ok = false;
     if constexpr (GEOM) {
         unsigned long long st[4] = {0, 0, 0, 0};
         float Tp[kSplit + 1];
@@ -400,7 +404,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             Tp[kSplit] = hi;
         };
         if (a.passes > 0) pass(std::true_type{}, std::false_type{});
-        if (a.passes > 1) pass(std::false_type{}, std::true_type{});
+        if (a.passes > 1) pass(std::false_type{}, std::integral_constant<bool, kPruneAfterPass2>{});
 #pragma unroll 1
         for (int it = 2; it < a.passes; it++) pass(std::false_type{}, std::false_type{});
         if constexpr (STATS) {
@@ -411,6 +415,39 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         w_max = fminf(fmaxf(w_max, 0.f), 1.f);  // __saturatef (NaN -> 0)
         const float w_min = 1.f - w_max;
         mDepth = in_range ? __builtin_fmaf(w_max, dmax, w_min * dmin) : 0.f;
+
+        // The backward's median-depth pre-pass (render_backward.cu:835-880),
+        // done here while the blended set is still in LDS: dT/dt_m at the
+        // depth the backward will reconstruct from the mdepth output.  The
+        // backward uses it when it receives that same mdepth (md_check) and
+        // recomputes it otherwise.  Contributors dropped after pass 2 are
+        // > 7 sigma from every depth of the final window: their terms are
+        // below 1e-10 of the sum.
+        const float nrm = pixel_ray_norm(pixx, pixy, a.W, a.H, a.focal_x, a.focal_y);
+        md_out = mDepth * (1.0f / nrm);
+        const float mDepth_b = md_out * nrm;
+        float dT_dtm = 0.f;
+        if (resident && inside && mDepth_b != 0.f && last != 0) {
+            const int nwords = (int)((last + 31) >> 5);
+            for (int w = 0; w < nwords; w++) {
+                uint32_t bits = my_mask[w * kTilePixels];
+                while (bits) {
+                    const int j = (w << 5) + __builtin_ctz(bits);
+                    bits &= bits - 1u;
+                    const float4 w0 = c_w0[j];
+                    const float dx = w0.x - pixx, dy = w0.y - pixy;
+                    const float4 w1 = c_w1[j];
+                    const float alpha = fminf(0.99f, w1.y * __expf(splat_power(w0, w1, dx, dy)));
+                    const float4 w2 = c_w2[j];
+                    const float t_peak = splat_tpeak(w1, w2, dx, dy);
+                    const float t_delta = (mDepth_b - t_peak) * w2.y;
+                    const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
+                    dT_dtm += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
+                }
+            }
+        }
+        md_dT = dT_dtm;
+        md_ok = resident;
     }
 
     if (inside) {
@@ -422,15 +459,15 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2);
         a.out_alpha[pix] = 1.f - T;
         if constexpr (GEOM) {
-            const float pnx = (pixx - (float)(a.W - 1) / 2.f) / a.focal_x;
-            const float pny = (pixy - (float)(a.H - 1) / 2.f) / a.focal_y;
-            const float rln = 1.0f / sqrtf(pnx * pnx + pny * pny + 1.f);
-            a.out_mdepth[pix] = mDepth * rln;
+            a.out_mdepth[pix] = md_out;
+            a.dT_dtm[pix] = md_dT;
+            a.md_check[pix] = md_ok ? __float_as_uint(md_out) : kNoCache;
             const float len = 1.f - T;
             a.out_normal[pix] = last ? N0 / len : 0.f;
             a.out_normal[HW + pix] = last ? N1 / len : 0.f;
             a.out_normal[2 * HW + pix] = last ? N2 / len : 0.f;
         } else {
+            a.md_check[pix] = kNoCache;
             a.out_mdepth[pix] = 0.f;
             a.out_normal[pix] = 0.f;
             a.out_normal[HW + pix] = 0.f;
@@ -455,6 +492,8 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.focal_y = p.focal_y;
     a.bg = p.background;
     a.n_contrib = is.n_contrib;
+    a.dT_dtm = is.dT_dtm;
+    a.md_check = is.md_check;
     a.max_contrib = ts.max_contrib;
     a.out_color = out_color;
     a.out_alpha = out_alpha;

@@ -74,6 +74,7 @@ last_bwd_scratch = None
 OPT_BISECT_SKIP = 0
 OPT_RENDER_STATS = 1
 OPT_BISECT_PASSES = 2
+OPT_BWD_NO_PREPASS = 3
 
 
 def debug_render_stats(reset: bool = True) -> list:

@@ -152,6 +152,33 @@ def test_parity_small(case):
     _run(Hh.small_case(kernel_size=ks, **case))
 
 
+def test_backward_with_foreign_mdepth():
+    """The forward caches the median-depth derivative for its own mdepth
+    output; a backward handed a different mdepth (bitwise) recomputes it, as
+    the reference always does (render_backward.cu:835-880)."""
+    from diff_gaussian_rasterization import _C
+
+    c = Hh.small_case(P=400, W=64, H=48, seed=21)
+    a = _fwd_args(c)
+    o = O.forward(*a)
+    ga = [_gpu(x) for x in a] + [False]
+    out = _C.rasterize_gaussians(*ga)
+    K, color, alpha, normal, mdepth, radii = out[:6]
+    md2 = mdepth * (1.0 + 1e-3)  # not the forward's output any more
+    g = S.upstream_grads(c["H"], c["W"])
+    b = O.backward(o["state"], *a[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], alpha.cpu(),
+                   normal.cpu(), md2.cpu(), c["cam"].camera_center, o["radii"])
+    gb = _C.rasterize_gaussians_backward(*ga[:19], _gpu(g["color"]), _gpu(g["mdepth"]), _gpu(g["alpha"]),
+                                         _gpu(g["normal"]), alpha, normal, md2, _gpu(c["cam"].camera_center),
+                                         radii, out[6], K, out[7], out[8], out[9], True, False)
+    for name, t in zip(GRAD_NAMES, gb):
+        mine, ref = t.cpu().numpy().astype(np.float64), b[name]
+        if ref.size == 0 or not np.any(ref):
+            continue
+        l2 = np.linalg.norm(mine - ref) / np.linalg.norm(ref)
+        assert l2 <= 1e-4, (name, l2)
+
+
 def test_parity_colors_precomp():
     c = Hh.small_case(P=400, W=64, H=48, seed=12)
     cols = torch.rand(400, 3, generator=torch.Generator().manual_seed(3))

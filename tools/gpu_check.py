@@ -69,3 +69,10 @@ if __name__ == "__main__":
         st = _C.timing_collect()
         print("bisection passes", npass, "render_fwd ms", round(st["render_fwd"][0] / max(st["render_fwd"][1], 1), 3))
     _C.set_option(_C.OPT_BISECT_PASSES, 0)
+    for nopre in (1, 0):
+        _C.set_option(_C.OPT_BWD_NO_PREPASS, nopre)
+        _C.timing_enable(True)
+        bench(require_depth=True, iters=5)
+        _C.timing_enable(False)
+        st = _C.timing_collect()
+        print("bwd no-prepass", nopre, "render_bwd ms", round(st["render_bwd"][0] / max(st["render_bwd"][1], 1), 3))
