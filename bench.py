@@ -78,6 +78,8 @@ def stage_bytes(P, K, K_live, HW, shm, sgm, geom):
         "emit_keys": P * 36 + K_live * 6,
         "sort": K_live * 12,
         "tile_ranges": K_live * 2,
+        # q-ordered Gaussians (index + splat rect/conic + radius) in, per-tile lists out
+        "tile_lists": P * 40 + K_live * 4,
         "render_fwd": K_live * (4 + G) + HW * Opx,
         "bwd_clear": P * A,
         "render_bwd": HW * Ipx + K_live * (4 + G),
@@ -234,7 +236,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.steps / elapsed
     shm = (args.sh_degree + 1) ** 2
-    algo = stage_bytes(P, K, W * H, shm, args.sg_degree, geom, ((W + 15) // 16) * ((H + 15) // 16))
+    algo = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom)
     per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in stages.items()}
     dom = max(per_launch, key=lambda k: per_launch[k])
     achieved = algo[dom] / (per_launch[dom] * 1e-3) / 1e9

@@ -57,22 +57,44 @@ size_t carve_geom(void* base, int P, GeomState& g) {
     g.offsets = c.take<uint2>(P);
     g.radii = c.take<int>(P);
     g.clamped = c.take<uint8_t>(P);
-    g.scan_tmp_bytes = scan_temp_bytes(P);
+    g.offsets_K = c.take<uint32_t>(1);
+    g.scan_tmp_bytes = scan_temp_bytes(P) > reduce_temp_bytes(P) ? scan_temp_bytes(P) : reduce_temp_bytes(P);
     g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
     g.dsort_tmp_bytes = depth_sort_temp_bytes(P);
     g.dsort_tmp = c.take<char>(g.dsort_tmp_bytes);
     return c.off + 256;
 }
 
-size_t carve_binning(void* base, int K, int tile_bits, BinningState& b) {
+// Binning buffer.  The point list comes first, so its offset depends only on
+// the base (gsr_debug_binning carves it knowing K alone); the rest depends
+// on the path: tile lists (tilelists.hip) or emit + tile-id sort.
+size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, BinningState& b) {
     Carver c(base);
-    b.key_bytes = tile_key_bytes(tile_bits);
-    b.keys_unsorted = c.take<char>((size_t)K * b.key_bytes);
-    b.keys = c.take<char>((size_t)K * b.key_bytes);
-    b.values_unsorted = c.take<uint32_t>(K);
     b.point_list = c.take<uint32_t>(K);
-    b.sort_tmp_bytes = sort_temp_bytes(K, tile_bits);
-    b.sort_tmp = c.take<char>(b.sort_tmp_bytes);
+    const int tiles = (int)(gx * gy);
+    const int tile_bits = (int)higher_msb((uint32_t)tiles);
+    b.use_lists = list_binning(gx, gy);
+    b.key_bytes = tile_key_bytes(tile_bits);
+    if (b.use_lists) {
+        b.lists = list_layout(P, K, gx, gy);
+        b.rows = c.take<uint2>(K);
+        b.rows_count = c.take<uint32_t>((size_t)gy * b.lists.nseg_rows);
+        b.rows_off = c.take<uint32_t>((size_t)gy * b.lists.nseg_rows);
+        b.segbase = c.take<uint32_t>(gy + 1);
+        b.tiles_count = c.take<uint32_t>((size_t)gx * b.lists.nseg_tiles_max + 1);
+        b.tiles_off = c.take<uint32_t>((size_t)gx * b.lists.nseg_tiles_max + 1);
+        b.list_tmp = c.take<char>(b.lists.tmp_bytes);
+        b.keys_unsorted = b.keys = nullptr;
+        b.values_unsorted = nullptr;
+        b.sort_tmp = nullptr;
+        b.sort_tmp_bytes = 0;
+    } else {
+        b.keys_unsorted = c.take<char>((size_t)K * b.key_bytes);
+        b.keys = c.take<char>((size_t)K * b.key_bytes);
+        b.values_unsorted = c.take<uint32_t>(K);
+        b.sort_tmp_bytes = sort_temp_bytes(K, tile_bits);
+        b.sort_tmp = c.take<char>(b.sort_tmp_bytes);
+    }
     return c.off + 256;
 }
 
@@ -237,7 +259,10 @@ int gsr_debug_binning(const void* binning_buffer, const void* tile_buffer, int R
     const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
     const int tiles = (int)(gx * gy);
     BinningState bs;
-    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, (int)higher_msb((uint32_t)tiles), bs);
+    {
+        Carver c(aligned_base(const_cast<void*>(binning_buffer)));
+        bs.point_list = c.take<uint32_t>(R);  // first in every layout (carve_binning)
+    }
     TileState ts;
     carve_tiles(aligned_base(const_cast<void*>(tile_buffer)), tiles, ts);
     hipStream_t stream = (hipStream_t)stream_ptr;
@@ -257,7 +282,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 3; }
+int gsr_abi_version(void) { return 4; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -290,7 +315,7 @@ int gsr_timing_collect(double* ms, int* launches) {
 
 const char* gsr_stage_name(int stage) {
     static const char* names[GSR_NUM_STAGES] = {"preprocess", "scan", "emit_keys", "sort", "tile_ranges",
-                                                 "render_fwd", "bwd_clear", "render_bwd", "preprocess_bwd", "depth_order"};
+                                                 "render_fwd", "bwd_clear", "render_bwd", "preprocess_bwd", "depth_order", "tile_lists"};
     return (stage >= 0 && stage < GSR_NUM_STAGES) ? names[stage] : "?";
 }
 
@@ -338,34 +363,46 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
         if (e == hipSuccess) e = hipMemsetAsync(ts.max_contrib, 0, sizeof(uint32_t) * tiles, stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "memset", e);
         BinningState bs;
-        void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, 0, 16, bs));
+        void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, 0, 0, p.grid_x, p.grid_y, bs));
         if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-        carve_binning(aligned_base(bbuf), 0, 16, bs);
+        carve_binning(aligned_base(bbuf), 0, 0, p.grid_x, p.grid_y, bs);
         GSR_TRY(launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
         return GSR_OK;
     }
 
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, radii, stream), "preprocess");
-    GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_order(p, gs, radii, stream), "depth order");
-    GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
-    // K = the reference's instance count (rect tiles, returned as num_rendered
-    // and sizing the binning buffer); K_live = instances that survive the
-    // tile test and are actually sorted and rendered (binning.hip)
+    const bool lists = list_binning(p.grid_x, p.grid_y);
+    // K = the reference's instance count (rect tiles): returned as
+    // num_rendered and the capacity of the binning buffer.  The sort path
+    // also needs K_live, the instances that survive tile culling.
     uint2 Ks = make_uint2(0u, 0u);
-    GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
+    if (lists) {
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
+        GSR_TRY(hipMemcpyAsync(&Ks.x, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
+    } else {
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_live_counts(p, gs, radii, stream), "live counts");
+        GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
+        GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
+    }
     {
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
     }
     const uint32_t K = Ks.x, K_live = Ks.y;
-    const int tile_bits = (int)higher_msb((uint32_t)tiles);
     BinningState bs;
-    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, tile_bits, bs));
+    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, bs));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-    carve_binning(aligned_base(bbuf), (int)K, tile_bits, bs);
-    GSR_STAGE(GSR_STAGE_EMIT_KEYS, launch_emit_keys(p, gs, radii, bs, stream), "emit keys");
-    GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K_live, tile_bits, stream), "sort");
-    GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K_live, ts, tiles, stream), "tile ranges");
+    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, bs);
+    if (lists) {
+        GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_list_binning(p, gs, radii, bs, ts, (int)K, stream), "tile lists");
+    } else {
+        const int tile_bits = (int)higher_msb((uint32_t)tiles);
+        GSR_STAGE(GSR_STAGE_EMIT_KEYS, launch_emit_keys(p, gs, radii, bs, stream), "emit keys");
+        GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K_live, tile_bits, stream), "sort");
+        GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K_live, ts, tiles, stream), "tile ranges");
+    }
     GSR_STAGE(GSR_STAGE_RENDER_FWD,
               launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
     if (num_rendered) *num_rendered = (int)K;
@@ -426,11 +463,10 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
     b.dL_dsg_color = dL_dsg_color;
 
     const int tiles = (int)(b.f.grid_x * b.f.grid_y);
-    const int tile_bits = (int)higher_msb((uint32_t)tiles);
     GeomState gs;
     carve_geom(aligned_base(const_cast<void*>(geom_buffer)), P, gs);
     BinningState bs;
-    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, tile_bits, bs);
+    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, P, b.f.grid_x, b.f.grid_y, bs);
     ImageState is;
     carve_image(aligned_base(const_cast<void*>(image_buffer)), width * height, is);
     TileState ts;

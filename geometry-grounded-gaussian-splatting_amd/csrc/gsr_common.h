@@ -70,6 +70,7 @@ struct GeomState {
     uint32_t* tiles_live;         // tiles of the rect that pass the tile test (binning.hip)
     uint2* counts;                // per Gaussian in depth order: (tiles_touched, live tiles)
     uint2* offsets;               // inclusive scan of counts: .x -> K (reference count), .y -> live instances
+    uint32_t* offsets_K;          // (tile-list path) K = sum of tiles_touched
     int* radii;                   // internal copy when the caller passes radii == NULL
     uint8_t* clamped;             // bit c set: colour channel c was clamped at 0
     void* scan_tmp;
@@ -80,12 +81,23 @@ struct GeomState {
 // ---- per-instance state (replaces BinningState) ----
 // tile ids as 16-bit sort keys when the grid allows (<= 65536 tiles)
 inline int tile_key_bytes(int tile_bits) { return tile_bits <= 16 ? 2 : 4; }
+// Tile-list binning (tilelists.hip): grids up to kMaxGrid x kMaxGrid tiles.
+constexpr int kMaxGrid = 1024;
+struct ListLayout {
+    int nseg_rows = 0, nseg_tiles_max = 0;
+    size_t tmp_bytes = 0;
+};
 struct BinningState {
+    uint32_t* point_list;  // first in the buffer: its offset depends on nothing else
+    bool use_lists;        // tilelists.hip path (else emit + tile-id sort)
+    ListLayout lists;
+    uint2* rows;           // (Gaussian, column span) per tile row, q order
+    uint32_t *rows_count, *rows_off, *segbase, *tiles_count, *tiles_off;
+    void* list_tmp;
     int key_bytes;        // 2 or 4 (tile_key_bytes)
     void* keys_unsorted;  // tile id per instance, emission (depth) order
     void* keys;           // tile ids sorted
     uint32_t* values_unsorted;
-    uint32_t* point_list;
     void* sort_tmp;
     size_t sort_tmp_bytes;
 };

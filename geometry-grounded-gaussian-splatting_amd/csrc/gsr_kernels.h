@@ -65,12 +65,21 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
 size_t scan_temp_bytes(int P);
 size_t depth_sort_temp_bytes(int P);
 size_t sort_temp_bytes(int K, int tile_bits);
-hipError_t launch_depth_order(const FwdParams& p, const GeomState& gs, const int* radii, hipStream_t stream);
+hipError_t launch_depth_sort(const GeomState& gs, int P, hipStream_t stream);
+hipError_t launch_live_counts(const FwdParams& p, const GeomState& gs, const int* radii, hipStream_t stream);
 hipError_t launch_scan(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_emit_keys(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
                             hipStream_t stream);
 hipError_t launch_sort(const BinningState& bs, int K, int tile_bits, hipStream_t stream);
 hipError_t launch_tile_ranges(const BinningState& bs, int K, const TileState& ts, int tiles, hipStream_t stream);
+
+// tilelists.hip
+bool list_binning(uint32_t gx, uint32_t gy);
+ListLayout list_layout(int P, int K, uint32_t gx, uint32_t gy);
+size_t reduce_temp_bytes(int P);
+hipError_t launch_count_K(const GeomState& gs, int P, hipStream_t stream);
+hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
+                               const TileState& ts, int K, hipStream_t stream);
 
 // render_fwd.hip
 hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const ImageState& is,

@@ -1,0 +1,327 @@
+// tilelists.hip — per-tile Gaussian lists without sorting the instances.
+//
+// Replaces duplicateWithKeys + cub::DeviceRadixSort::SortPairs +
+// identifyTileRanges (CR/rasterizer_impl.cu:70-161, 392-421) for grids of
+// up to kMaxGrid x kMaxGrid tiles (binning.hip keeps the sort path for larger
+// ones).  Input: the Gaussians in q order = (depth bits, index), the stable
+// depth sort of binning.hip.  Output: for every tile, the Gaussians whose
+// live tile set (tiles.h: rect + opacity-aware ellipse culling) contains it,
+// in q order — exactly the reference's per-tile (depth, index) order with
+// the culled instances removed — and the tile ranges.
+//
+// Two stable counting passes, each a deterministic rank-and-scatter:
+//   rows:  q order -> per tile row, the (Gaussian, column span) entries in
+//          q order;
+//   tiles: per row -> per tile of the row, the Gaussians in q order.
+// Each pass: (1) one wave per segment counts its entries per bucket (LDS
+// histogram); (2) an exclusive scan of the [bucket][segment] counts gives
+// every (bucket, segment) its first output slot; (3) the same wave walks its
+// segment again 64 entries at a time: every entry ORs its lane bit into a
+// 64-bit LDS mask per bucket it lands in, its rank among the 64 is the
+// popcount of the lower lanes' bits, and the bucket's first entry advances
+// the bucket's running slot.  One wave per segment and in-order LDS make
+// this barrier-free; rows and tile columns are few (<= kMaxGrid), so the
+// LDS per wave is small and many segments run per CU.
+#pragma clang fp contract(off)
+
+#include <rocprim/device/device_reduce.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "gsr_kernels.h"
+#include "tiles.h"
+
+namespace gsr {
+
+constexpr int kRowSeg = 256;   // Gaussians per row-pass segment
+constexpr int kTileSeg = 512;  // row entries per tile-pass segment
+
+bool list_binning(uint32_t gx, uint32_t gy) { return gx <= (uint32_t)kMaxGrid && gy <= (uint32_t)kMaxGrid; }
+
+ListLayout list_layout(int P, int K, uint32_t gx, uint32_t gy) {
+    ListLayout L;
+    L.nseg_rows = (P + kRowSeg - 1) / kRowSeg;
+    L.nseg_tiles_max = (K + kTileSeg - 1) / kTileSeg + (int)gy;
+    size_t a = 0, b = 0, c = 0;
+    (void)rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                  (size_t)gy * L.nseg_rows, rocprim::plus<uint32_t>());
+    (void)rocprim::exclusive_scan(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                  (size_t)gx * L.nseg_tiles_max + 1, rocprim::plus<uint32_t>());
+    (void)rocprim::reduce(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)P,
+                          rocprim::plus<uint32_t>());
+    L.tmp_bytes = a > b ? a : b;
+    L.tmp_bytes = L.tmp_bytes > c ? L.tmp_bytes : c;
+    return L;
+}
+
+size_t reduce_temp_bytes(int P) {
+    size_t c = 0;
+    (void)rocprim::reduce(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)P,
+                          rocprim::plus<uint32_t>());
+    return c;
+}
+
+hipError_t launch_count_K(const GeomState& gs, int P, hipStream_t stream) {
+    size_t bytes = gs.scan_tmp_bytes;
+    return rocprim::reduce(gs.scan_tmp, bytes, gs.tiles_touched, gs.offsets_K, 0u, (size_t)P,
+                           rocprim::plus<uint32_t>(), stream);
+}
+
+// --------------------------------------------------------------- rows pass
+struct QGauss {  // one Gaussian in q order, as the row kernels need it
+    bool on;
+    uint32_t g;
+    Ellipse E;
+    TileRect R;
+};
+__device__ __forceinline__ QGauss load_q(int q, int q1, const uint32_t* order, const Splat* splats,
+                                         const int* radii, uint32_t gx, uint32_t gy) {
+    QGauss G{};
+    if (q >= q1) return G;
+    G.g = order[q];
+    const int r = radii[G.g];
+    if (r <= 0) return G;
+    const float4 w0 = splats[G.g].w0, w1 = splats[G.g].w1;
+    G.E = make_ellipse(w0, w1);
+    G.R = tile_rect(w0.x, w0.y, r, gx, gy);
+    G.on = G.E.mode != 2 && G.R.x1 > G.R.x0 && G.R.y1 > G.R.y0;
+    return G;
+}
+
+__global__ void __launch_bounds__(64)
+    rows_count_kernel(int P, int nseg, uint32_t gx, uint32_t gy, const uint32_t* __restrict__ order,
+                      const Splat* __restrict__ splats, const int* __restrict__ radii, uint32_t* __restrict__ M) {
+    extern __shared__ unsigned long long s_dyn[];
+    uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
+    const int seg = blockIdx.x, lane = threadIdx.x;
+    for (uint32_t y = lane; y < gy; y += 64) s_cnt[y] = 0u;
+    __syncthreads();
+    const int q0 = seg * kRowSeg, q1 = min(P, q0 + kRowSeg);
+    for (int q = q0 + lane; q < q1; q += 64) {
+        const QGauss G = load_q(q, q1, order, splats, radii, gx, gy);
+        if (!G.on) continue;
+        uint32_t lo, hi;
+        for (uint32_t y = G.R.y0; y < G.R.y1; y++)
+            if (row_span(G.E, G.R, y, &lo, &hi)) atomicAdd(&s_cnt[y], 1u);
+    }
+    __syncthreads();
+    for (uint32_t y = lane; y < gy; y += 64) M[(size_t)y * nseg + seg] = s_cnt[y];
+}
+
+__global__ void __launch_bounds__(64)
+    rows_emit_kernel(int P, int nseg, uint32_t gx, uint32_t gy, const uint32_t* __restrict__ order,
+                     const Splat* __restrict__ splats, const int* __restrict__ radii, const uint32_t* __restrict__ O,
+                     uint2* __restrict__ rows) {
+    extern __shared__ unsigned long long s_dyn[];  // [gy] masks, then [gy] running slots
+    unsigned long long* s_cov = s_dyn;
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + gy);
+    const int seg = blockIdx.x, lane = threadIdx.x;
+    for (uint32_t y = lane; y < gy; y += 64) {
+        s_run[y] = O[(size_t)y * nseg + seg];
+        s_cov[y] = 0ull;
+    }
+    __syncthreads();
+    const unsigned long long bit = 1ull << lane, below = bit - 1ull;
+    const int q0 = seg * kRowSeg, q1 = min(P, q0 + kRowSeg);
+    for (int c0 = q0; c0 < q1; c0 += 64) {
+        const QGauss G = load_q(c0 + lane, q1, order, splats, radii, gx, gy);
+        uint32_t lo, hi;
+        if (G.on)
+            for (uint32_t y = G.R.y0; y < G.R.y1; y++)
+                if (row_span(G.E, G.R, y, &lo, &hi)) atomicOr(&s_cov[y], bit);
+        __syncthreads();  // one wave: orders the LDS phases for the compiler
+        if (G.on)
+            for (uint32_t y = G.R.y0; y < G.R.y1; y++)
+                if (row_span(G.E, G.R, y, &lo, &hi)) {
+                    const uint32_t rank = (uint32_t)__popcll(s_cov[y] & below);
+                    rows[s_run[y] + rank] = make_uint2(G.g, lo | (hi << 16));
+                }
+        __syncthreads();
+        if (G.on)
+            for (uint32_t y = G.R.y0; y < G.R.y1; y++)
+                if (row_span(G.E, G.R, y, &lo, &hi)) {
+                    const unsigned long long m = s_cov[y];
+                    if ((m & below) == 0ull) s_run[y] += (uint32_t)__popcll(m);  // the row's first entry here
+                }
+        __syncthreads();
+        if (G.on)
+            for (uint32_t y = G.R.y0; y < G.R.y1; y++)
+                if (row_span(G.E, G.R, y, &lo, &hi)) s_cov[y] = 0ull;
+        __syncthreads();
+    }
+}
+
+// --------------------------------------------------------------- tiles pass
+// Row y's entries are [O_rows[y * nseg_rows], O_rows[(y + 1) * nseg_rows]);
+// it is cut into ceil(len / kTileSeg) segments; segbase[y] is the exclusive
+// prefix of the segment counts (segbase[gy] = total).  The tile-pass counts
+// of row y live at [gx * segbase[y], gx * segbase[y + 1]), column-major
+// (x * nk + k), so one exclusive scan orders them (row, column, segment).
+__device__ __forceinline__ uint32_t row_begin(const uint32_t* O_rows, int nseg_rows, uint32_t y, uint32_t gy,
+                                              uint32_t total) {
+    return y < gy ? O_rows[(size_t)y * nseg_rows] : total;
+}
+
+__global__ void __launch_bounds__(1024)
+    tiles_setup_kernel(uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
+                       const uint32_t* __restrict__ M_rows_last, uint32_t* __restrict__ segbase) {
+    __shared__ uint32_t s[kMaxGrid];
+    const uint32_t y = threadIdx.x;
+    // total row entries = last exclusive offset + last count
+    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
+    uint32_t nk = 0;
+    if (y < gy) {
+        const uint32_t len = row_begin(O_rows, nseg_rows, y + 1, gy, total) - row_begin(O_rows, nseg_rows, y, gy, total);
+        nk = (len + kTileSeg - 1) / kTileSeg;
+    }
+    s[y] = nk;
+    __syncthreads();
+    // inclusive Hillis-Steele scan over <= 1024 rows
+    for (uint32_t o = 1; o < blockDim.x; o <<= 1) {
+        const uint32_t v = y >= o ? s[y - o] : 0u;
+        __syncthreads();
+        s[y] += v;
+        __syncthreads();
+    }
+    if (y < gy) segbase[y + 1] = s[y];
+    if (y == 0) segbase[0] = 0u;
+}
+
+struct TileSeg {
+    bool on;
+    uint32_t y, k, nk, e0, e1;
+};
+__device__ __forceinline__ TileSeg find_seg(uint32_t b, uint32_t gy, const uint32_t* segbase, const uint32_t* O_rows,
+                                            int nseg_rows, uint32_t total) {
+    TileSeg S{};
+    if (b >= segbase[gy]) return S;
+    uint32_t lo = 0, hi = gy;  // largest y with segbase[y] <= b
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segbase[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    S.on = true;
+    S.y = lo;
+    S.k = b - segbase[lo];
+    S.nk = segbase[lo + 1] - segbase[lo];
+    const uint32_t rb = row_begin(O_rows, nseg_rows, lo, gy, total), re = row_begin(O_rows, nseg_rows, lo + 1, gy, total);
+    S.e0 = rb + S.k * kTileSeg;
+    S.e1 = min(re, S.e0 + kTileSeg);
+    return S;
+}
+
+__global__ void __launch_bounds__(64)
+    tiles_count_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
+                       const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
+                       const uint2* __restrict__ rows, uint32_t* __restrict__ M) {
+    extern __shared__ unsigned long long s_dyn[];
+    uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
+    const int lane = threadIdx.x;
+    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
+    const TileSeg S = find_seg(blockIdx.x, gy, segbase, O_rows, nseg_rows, total);
+    if (!S.on) return;  // uniform over the (single-wave) block
+    for (uint32_t x = lane; x < gx; x += 64) s_cnt[x] = 0u;
+    __syncthreads();
+    for (uint32_t e = S.e0 + lane; e < S.e1; e += 64) {
+        const uint32_t sp = rows[e].y;
+        for (uint32_t x = sp & 0xffffu; x <= (sp >> 16); x++) atomicAdd(&s_cnt[x], 1u);
+    }
+    __syncthreads();
+    const size_t base = (size_t)gx * segbase[S.y];
+    for (uint32_t x = lane; x < gx; x += 64) M[base + (size_t)x * S.nk + S.k] = s_cnt[x];
+}
+
+__global__ void __launch_bounds__(64)
+    tiles_emit_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
+                      const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
+                      const uint2* __restrict__ rows, const uint32_t* __restrict__ O, uint32_t* __restrict__ point_list) {
+    extern __shared__ unsigned long long s_dyn[];  // [gx] masks, then [gx] running slots
+    unsigned long long* s_cov = s_dyn;
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + gx);
+    const int lane = threadIdx.x;
+    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
+    const TileSeg S = find_seg(blockIdx.x, gy, segbase, O_rows, nseg_rows, total);
+    if (!S.on) return;
+    const size_t base = (size_t)gx * segbase[S.y];
+    for (uint32_t x = lane; x < gx; x += 64) {
+        s_run[x] = O[base + (size_t)x * S.nk + S.k];
+        s_cov[x] = 0ull;
+    }
+    __syncthreads();
+    const unsigned long long bit = 1ull << lane, below = bit - 1ull;
+    for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64) {
+        const uint32_t e = c0 + lane;
+        const bool on = e < S.e1;
+        const uint2 ent = on ? rows[e] : make_uint2(0u, 1u);  // empty span when off
+        const uint32_t lo = ent.y & 0xffffu, hi = on ? (ent.y >> 16) : 0u;
+        for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&s_cov[x], bit);
+        __syncthreads();
+        for (uint32_t x = lo; on && x <= hi; x++)
+            point_list[s_run[x] + (uint32_t)__popcll(s_cov[x] & below)] = ent.x;
+        __syncthreads();
+        for (uint32_t x = lo; on && x <= hi; x++) {
+            const unsigned long long m = s_cov[x];
+            if ((m & below) == 0ull) s_run[x] += (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        for (uint32_t x = lo; on && x <= hi; x++) s_cov[x] = 0ull;
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256)
+    list_ranges_kernel(uint32_t gx, uint32_t gy, const uint32_t* __restrict__ segbase, const uint32_t* __restrict__ O,
+                       uint2* __restrict__ ranges) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= gx * gy) return;
+    const uint32_t y = t / gx, x = t - y * gx;
+    const uint32_t nk = segbase[y + 1] - segbase[y];
+    uint2 r = make_uint2(0u, 0u);
+    if (nk) {
+        const size_t base = (size_t)gx * segbase[y];
+        const uint32_t b = O[base + (size_t)x * nk], e = O[base + (size_t)(x + 1) * nk];
+        if (e > b) r = make_uint2(b, e);  // empty tiles stay (0, 0) as in the reference
+    }
+    ranges[t] = r;
+}
+
+hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
+                               const TileState& ts, int K, hipStream_t stream) {
+    const uint32_t gx = p.grid_x, gy = p.grid_y;
+    const ListLayout& L = bs.lists;
+    hipError_t e;
+    // rows pass
+    hipLaunchKernelGGL(rows_count_kernel, dim3(L.nseg_rows), dim3(64), 4 * gy, stream, p.P, L.nseg_rows, gx, gy, gs.order,
+                       gs.splats, radii, bs.rows_count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t bytes = L.tmp_bytes;
+    e = rocprim::exclusive_scan(bs.list_tmp, bytes, bs.rows_count, bs.rows_off, 0u, (size_t)gy * L.nseg_rows,
+                                rocprim::plus<uint32_t>(), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 12 * gy, stream, p.P, L.nseg_rows, gx, gy, gs.order,
+                       gs.splats, radii, bs.rows_off, bs.rows);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // tiles pass
+    const uint32_t* last = bs.rows_count + (size_t)gy * L.nseg_rows - 1;
+    hipLaunchKernelGGL(tiles_setup_kernel, dim3(1), dim3(1024), 0, stream, gy, L.nseg_rows, bs.rows_off, last,
+                       bs.segbase);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const size_t mt = (size_t)gx * L.nseg_tiles_max + 1;
+    if ((e = hipMemsetAsync(bs.tiles_count, 0, sizeof(uint32_t) * mt, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(tiles_count_kernel, dim3(L.nseg_tiles_max), dim3(64), 4 * gx, stream, gx, gy, L.nseg_rows,
+                       bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    bytes = L.tmp_bytes;
+    e = rocprim::exclusive_scan(bs.list_tmp, bytes, bs.tiles_count, bs.tiles_off, 0u, mt, rocprim::plus<uint32_t>(),
+                                stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tiles_emit_kernel, dim3(L.nseg_tiles_max), dim3(64), 12 * gx, stream, gx, gy, L.nseg_rows,
+                       bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(list_ranges_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, stream, gx, gy, bs.segbase,
+                       bs.tiles_off, ts.ranges);
+    (void)K;
+    return hipGetLastError();
+}
+
+}  // namespace gsr

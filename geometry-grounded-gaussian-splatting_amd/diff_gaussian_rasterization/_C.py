@@ -66,7 +66,7 @@ def loaded_library_path() -> str:
     return LIB_PATH
 
 
-NUM_STAGES = 10
+NUM_STAGES = 11
 # debugging aid: keep the last backward's accumulator buffer (gsr_api.hip
 # carve_bwd layout: 256-B aligned base, float acc[P][16], then float acc_abs[P])
 KEEP_BWD_SCRATCH = False

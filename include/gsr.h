@@ -110,14 +110,15 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
 enum gsr_stage {
     GSR_STAGE_PREPROCESS = 0,
     GSR_STAGE_SCAN,
-    GSR_STAGE_EMIT_KEYS,
-    GSR_STAGE_SORT,
-    GSR_STAGE_TILE_RANGES,
+    GSR_STAGE_EMIT_KEYS, /* (grids > 1024 tiles a side) instance emission for the tile-id sort */
+    GSR_STAGE_SORT,      /* (grids > 1024 tiles a side) stable tile-id sort */
+    GSR_STAGE_TILE_RANGES, /* (grids > 1024 tiles a side) */
     GSR_STAGE_RENDER_FWD,
     GSR_STAGE_BWD_CLEAR,
     GSR_STAGE_RENDER_BWD,
     GSR_STAGE_PREPROCESS_BWD,
-    GSR_STAGE_DEPTH_ORDER, /* stable depth sort of the Gaussians feeding the tile sort (binning.hip) */
+    GSR_STAGE_DEPTH_ORDER, /* stable depth sort of the Gaussians (binning.hip) */
+    GSR_STAGE_TILE_LISTS,  /* per-tile lists without an instance sort (tilelists.hip; grids <= 1024^2 tiles) */
     GSR_NUM_STAGES
 };
 int gsr_timing_enable(int on);

@@ -33,6 +33,9 @@ def stage_of(name: str) -> str | None:
         return "emit_keys"
     if "tile_ranges_kernel" in n:
         return "tile_ranges"
+    if any(k in n for k in ("rows_count_kernel", "rows_emit_kernel", "tiles_setup_kernel", "tiles_count_kernel",
+                            "tiles_emit_kernel", "list_ranges_kernel")):
+        return "tile_lists"
     if "render_fwd_kernel" in n:
         return "render_fwd"
     if "render_bwd_kernel" in n:
@@ -43,7 +46,7 @@ def stage_of(name: str) -> str | None:
         # rocPRIM kernels are named by key/value types: the tile sort has
         # 16-bit keys (grids <= 65536 tiles), the depth sort 32-bit keys
         return "sort" if "unsigned short" in n else "depth_order"
-    if "scan" in n:
+    if "scan" in n or "reduce" in n:
         return "scan"
     return None
 
