@@ -144,6 +144,18 @@ __device__ __forceinline__ float bcast(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 __device__ __forceinline__ uint32_t bcast(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+// every field of lane l's ellipse (word by word, so a new field cannot be missed)
+__device__ __forceinline__ Ellipse bcast(const Ellipse& E, int l) {
+    static_assert(sizeof(Ellipse) % 4 == 0, "Ellipse is broadcast as 32-bit words");
+    constexpr int kWords = sizeof(Ellipse) / 4;
+    int w[kWords];
+    __builtin_memcpy(w, &E, sizeof(Ellipse));
+#pragma unroll
+    for (int i = 0; i < kWords; i++) w[i] = __builtin_amdgcn_readlane(w[i], l);
+    Ellipse B;
+    __builtin_memcpy(&B, w, sizeof(Ellipse));
+    return B;
+}
 
 // One thread per Gaussian in depth order writes its live tiles, row by row
 // (the order within one Gaussian is irrelevant: it lands once per tile).
@@ -185,10 +197,7 @@ __global__ void __launch_bounds__(256)
     while (pending) {
         const int l = __builtin_ctzll(pending);
         pending &= pending - 1ull;
-        Ellipse B;
-        B.mx = bcast(E.mx, l), B.my = bcast(E.my, l), B.a = bcast(E.a, l), B.b = bcast(E.b, l);
-        B.c = bcast(E.c, l), B.det = bcast(E.det, l), B.tau = bcast(E.tau, l), B.vmax = bcast(E.vmax, l);
-        B.kst = bcast(E.kst, l), B.mode = (int)bcast((uint32_t)E.mode, l);
+        const Ellipse B = bcast(E, l);
         TileRect RB;
         RB.x0 = bcast(R.x0, l), RB.x1 = bcast(R.x1, l), RB.y0 = bcast(R.y0, l), RB.y1 = bcast(R.y1, l);
         const uint32_t g = bcast(idx, l);

@@ -107,13 +107,19 @@ __global__ void __launch_bounds__(64)
     for (uint32_t y = lane; y < gy; y += 64) M[(size_t)y * nseg + seg] = s_cnt[y];
 }
 
+// Ranking within a 64-entry chunk: every entry ORs its lane bit into its
+// bucket's mask; its slot is the bucket's running slot plus the popcount of
+// the lower lanes' bits, and the bucket's lowest lane advances the running
+// slot into the other half of a ping-pong pair, so one walk over the
+// entries does rank, write and advance.  The row-wide prologue of each chunk
+// carries the untouched running slots over and clears the next chunk's masks.
 __global__ void __launch_bounds__(64)
     rows_emit_kernel(int P, int nseg, uint32_t gx, uint32_t gy, const uint32_t* __restrict__ order,
                      const Splat* __restrict__ splats, const int* __restrict__ radii, const uint32_t* __restrict__ O,
                      uint2* __restrict__ rows) {
-    extern __shared__ unsigned long long s_dyn[];  // [gy] masks, then [gy] running slots
+    extern __shared__ unsigned long long s_dyn[];  // 2 x [gy] masks, then 2 x [gy] running slots
     unsigned long long* s_cov = s_dyn;
-    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + gy);
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * gy);
     const int seg = blockIdx.x, lane = threadIdx.x;
     for (uint32_t y = lane; y < gy; y += 64) {
         s_run[y] = O[(size_t)y * nseg + seg];
@@ -122,30 +128,29 @@ __global__ void __launch_bounds__(64)
     __syncthreads();
     const unsigned long long bit = 1ull << lane, below = bit - 1ull;
     const int q0 = seg * kRowSeg, q1 = min(P, q0 + kRowSeg);
-    for (int c0 = q0; c0 < q1; c0 += 64) {
+    uint32_t cur = 0;
+    for (int c0 = q0; c0 < q1; c0 += 64, cur ^= 1u) {
+        unsigned long long* cov = s_cov + cur * gy;
+        const uint32_t* run = s_run + cur * gy;
+        uint32_t* run_next = s_run + (cur ^ 1u) * gy;
+        for (uint32_t y = lane; y < gy; y += 64) {
+            run_next[y] = run[y];
+            s_cov[(cur ^ 1u) * gy + y] = 0ull;
+        }
         const QGauss G = load_q(c0 + lane, q1, order, splats, radii, gx, gy);
         uint32_t lo, hi;
         if (G.on)
             for (uint32_t y = G.R.y0; y < G.R.y1; y++)
-                if (row_span(G.E, G.R, y, &lo, &hi)) atomicOr(&s_cov[y], bit);
+                if (row_span(G.E, G.R, y, &lo, &hi)) atomicOr(&cov[y], bit);
         __syncthreads();  // one wave: orders the LDS phases for the compiler
         if (G.on)
             for (uint32_t y = G.R.y0; y < G.R.y1; y++)
                 if (row_span(G.E, G.R, y, &lo, &hi)) {
-                    const uint32_t rank = (uint32_t)__popcll(s_cov[y] & below);
-                    rows[s_run[y] + rank] = make_uint2(G.g, lo | (hi << 16));
+                    const unsigned long long m = cov[y];
+                    const uint32_t r0 = run[y];
+                    rows[r0 + (uint32_t)__popcll(m & below)] = make_uint2(G.g, lo | (hi << 16));
+                    if ((m & below) == 0ull) run_next[y] = r0 + (uint32_t)__popcll(m);
                 }
-        __syncthreads();
-        if (G.on)
-            for (uint32_t y = G.R.y0; y < G.R.y1; y++)
-                if (row_span(G.E, G.R, y, &lo, &hi)) {
-                    const unsigned long long m = s_cov[y];
-                    if ((m & below) == 0ull) s_run[y] += (uint32_t)__popcll(m);  // the row's first entry here
-                }
-        __syncthreads();
-        if (G.on)
-            for (uint32_t y = G.R.y0; y < G.R.y1; y++)
-                if (row_span(G.E, G.R, y, &lo, &hi)) s_cov[y] = 0ull;
         __syncthreads();
     }
 }
@@ -235,9 +240,9 @@ __global__ void __launch_bounds__(64)
     tiles_emit_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
                       const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
                       const uint2* __restrict__ rows, const uint32_t* __restrict__ O, uint32_t* __restrict__ point_list) {
-    extern __shared__ unsigned long long s_dyn[];  // [gx] masks, then [gx] running slots
+    extern __shared__ unsigned long long s_dyn[];  // 2 x [gx] masks, then 2 x [gx] running slots (rows_emit_kernel)
     unsigned long long* s_cov = s_dyn;
-    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + gx);
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * gx);
     const int lane = threadIdx.x;
     const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
     const TileSeg S = find_seg(blockIdx.x, gy, segbase, O_rows, nseg_rows, total);
@@ -249,22 +254,27 @@ __global__ void __launch_bounds__(64)
     }
     __syncthreads();
     const unsigned long long bit = 1ull << lane, below = bit - 1ull;
-    for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64) {
+    uint32_t cur = 0;
+    for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64, cur ^= 1u) {
+        unsigned long long* cov = s_cov + cur * gx;
+        const uint32_t* run = s_run + cur * gx;
+        uint32_t* run_next = s_run + (cur ^ 1u) * gx;
+        for (uint32_t x = lane; x < gx; x += 64) {
+            run_next[x] = run[x];
+            s_cov[(cur ^ 1u) * gx + x] = 0ull;
+        }
         const uint32_t e = c0 + lane;
         const bool on = e < S.e1;
         const uint2 ent = on ? rows[e] : make_uint2(0u, 1u);  // empty span when off
         const uint32_t lo = ent.y & 0xffffu, hi = on ? (ent.y >> 16) : 0u;
-        for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&s_cov[x], bit);
-        __syncthreads();
-        for (uint32_t x = lo; on && x <= hi; x++)
-            point_list[s_run[x] + (uint32_t)__popcll(s_cov[x] & below)] = ent.x;
+        for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&cov[x], bit);
         __syncthreads();
         for (uint32_t x = lo; on && x <= hi; x++) {
-            const unsigned long long m = s_cov[x];
-            if ((m & below) == 0ull) s_run[x] += (uint32_t)__popcll(m);
+            const unsigned long long m = cov[x];
+            const uint32_t r0 = run[x];
+            point_list[r0 + (uint32_t)__popcll(m & below)] = ent.x;
+            if ((m & below) == 0ull) run_next[x] = r0 + (uint32_t)__popcll(m);
         }
-        __syncthreads();
-        for (uint32_t x = lo; on && x <= hi; x++) s_cov[x] = 0ull;
         __syncthreads();
     }
 }
@@ -298,7 +308,7 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     e = rocprim::exclusive_scan(bs.list_tmp, bytes, bs.rows_count, bs.rows_off, 0u, (size_t)gy * L.nseg_rows,
                                 rocprim::plus<uint32_t>(), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 12 * gy, stream, p.P, L.nseg_rows, gx, gy, gs.order,
+    hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, gx, gy, gs.order,
                        gs.splats, radii, bs.rows_off, bs.rows);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // tiles pass
@@ -315,7 +325,7 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     e = rocprim::exclusive_scan(bs.list_tmp, bytes, bs.tiles_count, bs.tiles_off, 0u, mt, rocprim::plus<uint32_t>(),
                                 stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tiles_emit_kernel, dim3(L.nseg_tiles_max), dim3(64), 12 * gx, stream, gx, gy, L.nseg_rows,
+    hipLaunchKernelGGL(tiles_emit_kernel, dim3(L.nseg_tiles_max), dim3(64), 24 * gx, stream, gx, gy, L.nseg_rows,
                        bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(list_ranges_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, stream, gx, gy, bs.segbase,

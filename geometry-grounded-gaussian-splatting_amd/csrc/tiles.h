@@ -35,7 +35,7 @@ __device__ __forceinline__ TileRect tile_rect(float mx, float my, int r, uint32_
 // the rounding of the per-pixel power and exp.  Non-positive-definite conics
 // keep their whole rect; o < 1/255 keeps nothing.
 struct Ellipse {
-    float mx, my, a, b, c, det, tau, vmax, kst;
+    float mx, my, a, b, c, det, tau, vmax, kst, ia;
     int mode;  // 0 = interval test, 1 = whole rect, 2 = nothing
 };
 __device__ __forceinline__ Ellipse make_ellipse(const float4& w0, const float4& w1) {
@@ -50,6 +50,7 @@ __device__ __forceinline__ Ellipse make_ellipse(const float4& w0, const float4& 
     E.tau = 2.f * logf(fmaxf(255.f * o, 1.f)) * 1.001f + 0.01f;
     E.vmax = sqrtf(E.a * E.tau / E.det);
     E.kst = sqrtf(E.tau / (E.c * E.det));
+    E.ia = 1.f / E.a;
     const bool pd = E.a > 0.f && E.c > 0.f && E.det > 0.f && E.vmax == E.vmax && E.kst == E.kst;
     E.mode = !(255.f * o >= 1.f) && o == o ? 2 : (pd ? 0 : 1);
     return E;
@@ -68,7 +69,7 @@ __device__ __forceinline__ bool row_span(const Ellipse& E, const TileRect& R, ui
     if (vlo > vhi) return false;
     const float vu = fminf(fmaxf(-E.b * E.kst, vlo), vhi);  // maximiser of the upper branch
     const float vl = fminf(fmaxf(E.b * E.kst, vlo), vhi);   // minimiser of the lower branch
-    const float ia = 1.f / E.a;
+    const float ia = E.ia;
     const float umax = (-E.b * vu + sqrtf(fmaxf(E.a * E.tau - E.det * vu * vu, 0.f))) * ia;
     const float umin = (-E.b * vl - sqrtf(fmaxf(E.a * E.tau - E.det * vl * vl, 0.f))) * ia;
     // pixel centres x in [mx - umax, mx - umin]; tile tx holds x in [16 tx, 16 tx + 15]
