@@ -68,26 +68,29 @@ struct RenderFwdArgs {
 // ulp; both products stay >= the pixel's final transmittance >= 1e-4, so
 // nothing underflows).  Samples are evaluated two at a time with packed
 // fp32 (v_pk_{add,mul,fma}_f32), and
-//  * exp(-delta^2/2) = exp2((d d) k) with d = ts - t_peak and
-//    k = (rsigma rsigma)(-0.5 log2e) per contributor: one packed multiply
-//    less per sample pair than ((d rsigma)^2)(-0.5 log2e) (a few ulp apart);
+//  * exp(-delta^2/2) = exp2(-u u) with u = ts sc - t_peak sc and
+//    sc = rsigma sqrt(0.5 log2e) per contributor: one packed fma gives a
+//    sample pair's u and the negation rides on v_exp's source modifier (the
+//    rounding differs from the reference's ((ts - t_peak) rsigma)^2 by a
+//    few ulp of u, i.e. an absolute error of ~1e-7 in g);
 //  * a non-ball splat (rsigma <= 0, g = 0 in the reference) runs with
-//    alpha_g = 0 and rsigma = 0: delta = 0, g = 1, 1 - 0*g = 1 exactly.
-// Exact shortcut (SKIP): when every sample of the window has |delta| > 7,
-// a*g < e^-24.5 < 2^-25, so 1 - a*g rounds to exactly 1.0f: B is unchanged
+//    alpha_g = 0 and sc = 0: u = 0, g = 1, 1 - 0*g = 1 exactly.
+// Exact shortcut (SKIP): when every sample of the window has |delta| > 6,
+// a*g < e^-18 < 2^-25, so 1 - a*g rounds to exactly 1.0f: B is unchanged
 // and A gains (1 - a) in front of the window, nothing behind it (the samples
 // are monotone in s, so the two window ends decide).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-constexpr float kHalfNegLog2e = -0.5f * 1.44269502162933349609375f;  // -0.5 * (float)log2(e), exact
+constexpr float kSqrtHalfLog2e = 0.84932180028801904272f;  // sqrt(0.5 log2 e)
+constexpr float kFarDelta = 6.f;  // |delta| beyond which 1 - a g == 1.0f exactly (a <= 0.99)
 
 // Samples live in packed register pairs (pair k holds samples START + 2k and
 // START + 2k + 1, so every v_pk_* operand is an aligned pair and no lane
 // moves feed them); an odd count leaves one scalar sample (A1, B1 at T1).
-// Per contributor the staged record supplies k = rsigma^2 (-0.5 log2e) and
-// the ball flag bm (1 or 0), so a_g = alpha bm and e = (d d) k.
+// Per contributor the staged record supplies sc = rsigma sqrt(0.5 log2e)
+// and the ball flag bm (1 or 0), so a_g = alpha bm and u = fma(ts, sc, -t_peak sc).
 template <int NP, bool HAS1, bool SKIP>
 __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], const f32x2 (&TS)[NP], float& A1,
-                                            float& B1, float T1, float alpha, float t_peak, float rsig, float kk,
+                                            float& B1, float T1, float alpha, float t_peak, float rsig, float sc,
                                             float bm) {
     const float om = 1.f - alpha;
     const f32x2 om2 = {om, om};
@@ -95,31 +98,32 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
         const bool ball = rsig > 0.f;
         const float d_lo = (TS[0].x - t_peak) * rsig;
         const float d_hi = ((HAS1 ? T1 : TS[NP - 1].y) - t_peak) * rsig;
-        if (ball && d_lo > 7.f) {
+        if (ball && d_lo > kFarDelta) {
 #pragma unroll
             for (int k = 0; k < NP; k++) A[k] *= om2;
             if constexpr (HAS1) A1 *= om;
             return;
         }
-        if (ball && d_hi < -7.f) return;
+        if (ball && d_hi < -kFarDelta) return;
     }
     const float ag = alpha * bm;
-    const f32x2 ag2 = {ag, ag}, kk2 = {kk, kk}, tp2 = {t_peak, t_peak};
+    const float q = -t_peak * sc;
+    const f32x2 ag2 = {ag, ag}, sc2 = {sc, sc}, q2 = {q, q};
     const f32x2 one2 = {1.f, 1.f};
 #pragma unroll
     for (int k = 0; k < NP; k++) {
         const f32x2 t = TS[k];
-        const f32x2 d = t - tp2;
-        const f32x2 e = (d * d) * kk2;
-        const f32x2 g = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+        const f32x2 u = __builtin_elementwise_fma(t, sc2, q2);
+        const f32x2 e = u * u;
+        const f32x2 g = {__builtin_amdgcn_exp2f(-e.x), __builtin_amdgcn_exp2f(-e.y)};
         const f32x2 omg = __builtin_elementwise_fma(-ag2, g, one2);
         const f32x2 sel = {t.x > t_peak ? om : omg.x, t.y > t_peak ? om : omg.y};
         A[k] *= sel;
         B[k] *= omg;
     }
     if constexpr (HAS1) {
-        const float d = T1 - t_peak;
-        const float g = __builtin_amdgcn_exp2f((d * d) * kk);
+        const float u = __builtin_fmaf(T1, sc, q);
+        const float g = __builtin_amdgcn_exp2f(-(u * u));
         const float omg = __builtin_fmaf(-ag, g, 1.f);
         A1 *= T1 > t_peak ? om : omg;
         B1 *= omg;
@@ -129,7 +133,7 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
 // Diagnostic counters (STATS builds only, option GSR_OPT_RENDER_STATS):
 // [0] bisection wave-steps and [1] active lanes on the per-lane (resident)
 // walk; [2] active lanes in passes 2-5 and [3] those whose whole window is
-// more than 7 sigma from the splat's peak (exact-constant factors).
+// more than kFarDelta sigma from the splat's peak (exact-constant factors).
 __device__ unsigned long long g_render_stats[8];
 
 template <bool GEOM, bool SKIP, bool STATS = false>
@@ -264,7 +268,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 c_w1[k] = sp->w1;
                 const float4 w2 = sp->w2;
                 const bool ball = w2.y > 0.f;  // non-ball splats: g = 0 (bisect_step)
-                c_w2[k] = make_float4(w2.x, w2.y, ball ? (w2.y * w2.y) * kHalfNegLog2e : 0.f, ball ? 1.f : 0.f);
+                c_w2[k] = make_float4(w2.x, w2.y, ball ? w2.y * kSqrtHalfLog2e : 0.f, ball ? 1.f : 0.f);
             }
         };
         if (resident && max_contrib > 0) {
@@ -274,7 +278,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         }
         // one bisection pass; FIRST evaluates all 9 samples, later passes
         // reuse the bracketing ends (render_forward.cu:560-645)
-        // Contributors whose whole pass-2 window lies more than 7 sigma from
+        // Contributors whose whole pass-2 window lies more than 6 sigma from
         // their peak have exactly constant factors in passes 3-5 (their
         // windows nest inside it; see bisect_step SKIP): pass 2 drops them
         // from the lane's mask and folds the (1 - a) of those behind the
@@ -335,9 +339,9 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                     const float4 w2 = c_w2[j];
                     const float t_peak = splat_tpeak(w1, w2, dx, dy);
                     if constexpr (STATS && !FIRST) {
-                        // lanes whose whole window is > 7 sigma from the peak
+                        // lanes whose whole window is > kFarDelta sigma from the peak
                         const float d_lo = (ts[1] - t_peak) * w2.y, d_hi = (ts[kSplit - 1] - t_peak) * w2.y;
-                        const bool far = w2.y > 0.f && (d_lo > 7.f || d_hi < -7.f);
+                        const bool far = w2.y > 0.f && (d_lo > kFarDelta || d_hi < -kFarDelta);
                         const unsigned long long m = __ballot(1);
                         const unsigned long long fm = __ballot(far);
                         if ((tid & 63) == __builtin_ctzll(m)) {
@@ -347,8 +351,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                     }
                     if constexpr (!FIRST && prune) {
                         const bool ball = w2.y > 0.f;
-                        const bool behind = ball && (ts[0] - t_peak) * w2.y > 7.f;
-                        const bool front = ball && (ts[kSplit] - t_peak) * w2.y < -7.f;
+                        const bool behind = ball && (ts[0] - t_peak) * w2.y > kFarDelta;
+                        const bool front = ball && (ts[kSplit] - t_peak) * w2.y < -kFarDelta;
                         far_A *= behind ? 1.f - alpha : 1.f;
                         keep |= (behind || front) ? 0u : jbit;
                     }
@@ -421,8 +425,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         // depth the backward will reconstruct from the mdepth output.  The
         // backward uses it when it receives that same mdepth (md_check) and
         // recomputes it otherwise.  Contributors dropped after pass 2 are
-        // > 7 sigma from every depth of the final window: their terms are
-        // below 1e-10 of the sum.
+        // > 6 sigma from every depth of the final window: each of their terms
+        // is below 0.25 e^-18 6 rsigma < 3e-8 rsigma in magnitude.
         const float nrm = pixel_ray_norm(pixx, pixy, a.W, a.H, a.focal_x, a.focal_y);
         md_out = mDepth * (1.0f / nrm);
         const float mDepth_b = md_out * nrm;
