@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(64)
                       const Splat* __restrict__ splats, const int* __restrict__ radii, uint32_t* __restrict__ M) {
     extern __shared__ unsigned long long s_dyn[];
     uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
-    const int seg = blockIdx.x, lane = threadIdx.x;
+    const int seg = (int)xcd_remap(blockIdx.x, gridDim.x), lane = threadIdx.x;  // XCD-contiguous segments
     for (uint32_t y = lane; y < gy; y += 64) s_cnt[y] = 0u;
     __syncthreads();
     const int q0 = seg * kRowSeg, q1 = min(P, q0 + kRowSeg);
@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(64)
     extern __shared__ unsigned long long s_dyn[];  // 2 x [gy] masks, then 2 x [gy] running slots
     unsigned long long* s_cov = s_dyn;
     uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * gy);
-    const int seg = blockIdx.x, lane = threadIdx.x;
+    const int seg = (int)xcd_remap(blockIdx.x, gridDim.x), lane = threadIdx.x;  // XCD-contiguous segments
     for (uint32_t y = lane; y < gy; y += 64) {
         s_run[y] = O[(size_t)y * nseg + seg];
         s_cov[y] = 0ull;
@@ -215,6 +215,23 @@ __device__ __forceinline__ TileSeg find_seg(uint32_t b, uint32_t gy, const uint3
     return S;
 }
 
+// The tile-pass kernels run a fixed grid that walks the actual segments
+// (segbase[gy], known on the device only).  Blocks are dealt round-robin over
+// the 8 XCDs; XCD x takes the x-th eighth of the segments, and its blocks
+// walk that range in lockstep strides, so the rows an XCD works on at any
+// moment are one or two, and their point-list region (~1 MB at C3) stays in
+// that XCD's L2 while the partial lines written by successive segments fill
+// up (write-back of whole lines instead of ~16-B pieces).
+constexpr int kTileBlocks = 8 * 1024;
+
+template <typename F>
+__device__ __forceinline__ void for_xcd_segments(uint32_t n, F&& f) {
+    const uint32_t xcd = blockIdx.x % 8u, slot = blockIdx.x / 8u, nslots = gridDim.x / 8u;
+    const uint32_t lo = (uint32_t)(((unsigned long long)n * xcd) / 8u);
+    const uint32_t hi = (uint32_t)(((unsigned long long)n * (xcd + 1u)) / 8u);
+    for (uint32_t l = lo + slot; l < hi; l += nslots) f(l);
+}
+
 __global__ void __launch_bounds__(64)
     tiles_count_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
                        const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
@@ -223,17 +240,19 @@ __global__ void __launch_bounds__(64)
     uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
     const int lane = threadIdx.x;
     const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
-    const TileSeg S = find_seg(blockIdx.x, gy, segbase, O_rows, nseg_rows, total);
-    if (!S.on) return;  // uniform over the (single-wave) block
-    for (uint32_t x = lane; x < gx; x += 64) s_cnt[x] = 0u;
-    __syncthreads();
-    for (uint32_t e = S.e0 + lane; e < S.e1; e += 64) {
-        const uint32_t sp = rows[e].y;
-        for (uint32_t x = sp & 0xffffu; x <= (sp >> 16); x++) atomicAdd(&s_cnt[x], 1u);
-    }
-    __syncthreads();
-    const size_t base = (size_t)gx * segbase[S.y];
-    for (uint32_t x = lane; x < gx; x += 64) M[base + (size_t)x * S.nk + S.k] = s_cnt[x];
+    for_xcd_segments(segbase[gy], [&](uint32_t l) {
+        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
+        __syncthreads();  // previous segment's counts read out
+        for (uint32_t x = lane; x < gx; x += 64) s_cnt[x] = 0u;
+        __syncthreads();
+        for (uint32_t e = S.e0 + lane; e < S.e1; e += 64) {
+            const uint32_t sp = rows[e].y;
+            for (uint32_t x = sp & 0xffffu; x <= (sp >> 16); x++) atomicAdd(&s_cnt[x], 1u);
+        }
+        __syncthreads();
+        const size_t base = (size_t)gx * segbase[S.y];
+        for (uint32_t x = lane; x < gx; x += 64) M[base + (size_t)x * S.nk + S.k] = s_cnt[x];
+    });
 }
 
 __global__ void __launch_bounds__(64)
@@ -245,38 +264,40 @@ __global__ void __launch_bounds__(64)
     uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * gx);
     const int lane = threadIdx.x;
     const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
-    const TileSeg S = find_seg(blockIdx.x, gy, segbase, O_rows, nseg_rows, total);
-    if (!S.on) return;
-    const size_t base = (size_t)gx * segbase[S.y];
-    for (uint32_t x = lane; x < gx; x += 64) {
-        s_run[x] = O[base + (size_t)x * S.nk + S.k];
-        s_cov[x] = 0ull;
-    }
-    __syncthreads();
     const unsigned long long bit = 1ull << lane, below = bit - 1ull;
-    uint32_t cur = 0;
-    for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64, cur ^= 1u) {
-        unsigned long long* cov = s_cov + cur * gx;
-        const uint32_t* run = s_run + cur * gx;
-        uint32_t* run_next = s_run + (cur ^ 1u) * gx;
+    for_xcd_segments(segbase[gy], [&](uint32_t l) {
+        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
+        const size_t base = (size_t)gx * segbase[S.y];
+        __syncthreads();  // previous segment done with the LDS
         for (uint32_t x = lane; x < gx; x += 64) {
-            run_next[x] = run[x];
-            s_cov[(cur ^ 1u) * gx + x] = 0ull;
-        }
-        const uint32_t e = c0 + lane;
-        const bool on = e < S.e1;
-        const uint2 ent = on ? rows[e] : make_uint2(0u, 1u);  // empty span when off
-        const uint32_t lo = ent.y & 0xffffu, hi = on ? (ent.y >> 16) : 0u;
-        for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&cov[x], bit);
-        __syncthreads();
-        for (uint32_t x = lo; on && x <= hi; x++) {
-            const unsigned long long m = cov[x];
-            const uint32_t r0 = run[x];
-            point_list[r0 + (uint32_t)__popcll(m & below)] = ent.x;
-            if ((m & below) == 0ull) run_next[x] = r0 + (uint32_t)__popcll(m);
+            s_run[x] = O[base + (size_t)x * S.nk + S.k];
+            s_cov[x] = 0ull;
         }
         __syncthreads();
-    }
+        uint32_t cur = 0;
+        for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64, cur ^= 1u) {
+            unsigned long long* cov = s_cov + cur * gx;
+            const uint32_t* run = s_run + cur * gx;
+            uint32_t* run_next = s_run + (cur ^ 1u) * gx;
+            for (uint32_t x = lane; x < gx; x += 64) {
+                run_next[x] = run[x];
+                s_cov[(cur ^ 1u) * gx + x] = 0ull;
+            }
+            const uint32_t e = c0 + lane;
+            const bool on = e < S.e1;
+            const uint2 ent = on ? rows[e] : make_uint2(0u, 1u);  // empty span when off
+            const uint32_t lo = ent.y & 0xffffu, hi = on ? (ent.y >> 16) : 0u;
+            for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&cov[x], bit);
+            __syncthreads();
+            for (uint32_t x = lo; on && x <= hi; x++) {
+                const unsigned long long m = cov[x];
+                const uint32_t r0 = run[x];
+                point_list[r0 + (uint32_t)__popcll(m & below)] = ent.x;
+                if ((m & below) == 0ull) run_next[x] = r0 + (uint32_t)__popcll(m);
+            }
+            __syncthreads();
+        }
+    });
 }
 
 __global__ void __launch_bounds__(256)
@@ -318,14 +339,14 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const size_t mt = (size_t)gx * L.nseg_tiles_max + 1;
     if ((e = hipMemsetAsync(bs.tiles_count, 0, sizeof(uint32_t) * mt, stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(tiles_count_kernel, dim3(L.nseg_tiles_max), dim3(64), 4 * gx, stream, gx, gy, L.nseg_rows,
+    hipLaunchKernelGGL(tiles_count_kernel, dim3(kTileBlocks), dim3(64), 4 * gx, stream, gx, gy, L.nseg_rows,
                        bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bytes = L.tmp_bytes;
     e = rocprim::exclusive_scan(bs.list_tmp, bytes, bs.tiles_count, bs.tiles_off, 0u, mt, rocprim::plus<uint32_t>(),
                                 stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tiles_emit_kernel, dim3(L.nseg_tiles_max), dim3(64), 24 * gx, stream, gx, gy, L.nseg_rows,
+    hipLaunchKernelGGL(tiles_emit_kernel, dim3(kTileBlocks), dim3(64), 24 * gx, stream, gx, gy, L.nseg_rows,
                        bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(list_ranges_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, stream, gx, gy, bs.segbase,
