@@ -50,15 +50,24 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--config", choices=["C3", "C5"], default="C3",
+                    help="C3: 1M Gaussians, SH 3 (the metric's config); C5: 5M Gaussians, SH 3 + SG 7")
+    ap.add_argument("--P", type=int, default=None)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--sh-degree", type=int, default=3)
-    ap.add_argument("--sg-degree", type=int, default=0)
+    ap.add_argument("--sg-degree", type=int, default=None)
     ap.add_argument("--no-depth", action="store_true", help="require_depth=False (iterations < 7000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-tile-stride", type=int, default=0, help="0 = auto")
-    return ap.parse_args()
+    a = ap.parse_args()
+    preset = {"C3": (1_000_000, 0), "C5": (5_000_000, 7)}[a.config]
+    a.P = preset[0] if a.P is None else a.P
+    a.sg_degree = preset[1] if a.sg_degree is None else a.sg_degree
+    # PMC traffic in profiles/ is measured on the default workload only
+    a.default_workload = (a.config == "C3" and a.P == 1_000_000 and a.sg_degree == 0 and a.width == 1920
+                          and a.height == 1080 and a.sh_degree == 3 and not a.no_depth)
+    return a
 
 
 def stage_bytes(P, K, K_live, HW, shm, sgm, geom):
@@ -127,7 +136,7 @@ def cpu_baseline(args, inputs_cpu, cam, tanx, tany, grads_cpu):
     O.set_tile_stride(1)
     per_iter = tf["preprocess_binning"] + stride * tf["render"] + stride * tb["render_bwd"] + tb["preprocess_bwd"]
     return {"value": round(1.0 / per_iter, 6), "unit": "iters/s", "cores": cores, "kind": "port",
-            "sample": (f"C oracle (oracle/gsr_oracle.c), full C3 scene: per-Gaussian preprocess, binning/sort and "
+            "sample": (f"C oracle (oracle/gsr_oracle.c), full {args.config} scene: per-Gaussian preprocess, binning/sort and "
                        f"per-Gaussian backward measured in full; forward+backward tile rendering on every "
                        f"{stride}th of {tiles} tiles, extrapolated x{stride}; {wall:.1f} s wall; "
                        f"split s: {tf['preprocess_binning']:.2f} pre+bin, {tf['render'] * stride:.2f} render, "
@@ -152,10 +161,11 @@ def main():
     geom = not args.no_depth
     if world > 1:
         cam_cpu = S.orbit_cameras(8, W, H)[rank % 8]
-        workload = f"C4: {P} Gaussians, one {W}x{H} view per GPU (orbit), fwd+bwd + RCCL grad all_reduce"
+        tag = "C4" if args.config == "C3" else "C5"
+        workload = f"{tag}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), one {W}x{H} view per GPU (orbit), fwd+bwd + RCCL grad all_reduce"
     else:
         cam_cpu = S.make_camera(W, H)
-        workload = f"C3: {P} Gaussians, {W}x{H}, fwd+bwd"
+        workload = f"{args.config}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), {W}x{H}, fwd+bwd"
     raw = S.make_gaussians(P, sh_degree=args.sh_degree, sg_degree=args.sg_degree, aspect=H / W)
     inputs_cpu = {k: v.detach().contiguous() for k, v in S.activated_inputs(raw).items()}
     grads_cpu = S.upstream_grads(H, W)
@@ -240,7 +250,7 @@ def main():
     per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in stages.items()}
     dom = max(per_launch, key=lambda k: per_launch[k])
     achieved = algo[dom] / (per_launch[dom] * 1e-3) / 1e9
-    traffic, valu = load_pmc_traffic(dom)
+    traffic, valu = load_pmc_traffic(dom) if args.default_workload else (None, None)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(algo[dom]),

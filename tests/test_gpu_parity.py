@@ -137,6 +137,7 @@ SMALL = [
     dict(P=300, W=64, H=48, seed=1),
     dict(P=500, W=100, H=70, seed=2, kernel_size=0.1),
     dict(P=400, W=61, H=53, seed=3, sgm=3, sg_degree=2),
+    dict(P=300, W=64, H=48, seed=10, sgm=7, sg_degree=7),  # C5's SH 3 + SG 7 colour model
     dict(P=400, W=64, H=48, seed=4, sh_degree=1),
     dict(P=400, W=64, H=48, seed=5, require_depth=False),
     dict(P=400, W=64, H=48, seed=6, bg=(0.3, 0.6, 0.9)),
@@ -370,6 +371,95 @@ def test_c3_backward_linearity(c3):
             x, y, z = x[:, :2], y[:, :2], z[:, :2]
         if x.numel() == 0:
             continue
+        want = (x + 2 * y).double()
+        err = float((z.double() - want).norm() / want.norm().clamp_min(1e-30))
+        assert err <= 1e-4, (name, err)
+
+
+# ------------------------------------------------------------- C2 and C5
+def _scene(P, W, H, sg_degree=0):
+    cam = S.make_camera(W, H)
+    raw = S.make_gaussians(P, sg_degree=sg_degree, aspect=H / W)
+    inp = {k: v.detach().contiguous() for k, v in S.activated_inputs(raw).items()}
+    return dict(bg=torch.zeros(3), inp=inp, cam=cam, W=W, H=H, sh_degree=3, sg_degree=sg_degree, kernel_size=0.0,
+                require_depth=True, tanx=math.tan(cam.FoVx / 2), tany=math.tan(cam.FoVy / 2))
+
+
+def test_c2_full_forward_parity():
+    """C2 (BASELINE.json configs[1]): 100k Gaussians, one 800x800 view,
+    forward only — every pixel against the oracle, K/radii/binning exact."""
+    from diff_gaussian_rasterization import _C
+
+    c = _scene(100_000, 800, 800)
+    args = Hh.oracle_args(c)
+    O.set_threads(16)
+    o = O.forward(*args)
+    out = _C.rasterize_gaussians(*[_gpu(x) for x in args], False)
+    assert out[0] == o["num_rendered"]
+    assert np.array_equal(out[5].cpu().numpy(), o["radii"])
+    _check_binning(out, o, 800, 800, dead_sample=20000)
+    for name, t in (("color", out[1]), ("alpha", out[2]), ("normal", out[3]), ("mdepth", out[4])):
+        a, b = t.cpu().numpy(), o[name]
+        bad = np.abs(a - b) > 1e-4 * np.abs(b).max()
+        assert bad.mean() <= 1e-4, (name, bad.mean())  # isolated float-decision flips only
+
+
+def test_c5_full_size_properties():
+    """C5 (BASELINE.json configs[4]): 5M Gaussians, SH 3 + SG 7, 1080p with
+    depth/normal outputs.  K, radii and the tile lists exact; tile-sampled
+    image parity; deterministic forward; backward linear in the upstream
+    gradients and zero for culled Gaussians."""
+    from diff_gaussian_rasterization import _C
+
+    W, H = 1920, 1080
+    c = _scene(5_000_000, W, H, sg_degree=7)
+    args = Hh.oracle_args(c)
+    ga = [_gpu(x) for x in args] + [False]
+    out = _C.rasterize_gaussians(*ga)
+    out2 = _C.rasterize_gaussians(*ga)
+    for k in range(1, 6):
+        assert torch.equal(out[k], out2[k])
+    del out2
+    O.set_threads(16)
+    stride = 211
+    O.set_tile_stride(stride)
+    try:
+        o = O.forward(*args)
+    finally:
+        O.set_tile_stride(1)
+    K, color, alpha, normal, mdepth, radii = out[:6]
+    assert K == o["num_rendered"]
+    assert np.array_equal(radii.cpu().numpy(), o["radii"])
+    _check_binning(out, o, H, W, dead_sample=5000)
+    gx = (W + 15) // 16
+    mask = np.zeros((H, W), bool)
+    for t in range(0, gx * ((H + 15) // 16), stride):
+        ty, tx = divmod(t, gx)
+        mask[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16] = True
+    for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
+        a = t.cpu().numpy()[:, mask]
+        b = o[name][:, mask]
+        bad = np.abs(a - b) > 1e-4 * np.abs(b).max()
+        assert bad.mean() <= 1e-4, (name, bad.mean())
+    del o
+    g1 = {k: v.to(DEV) for k, v in S.upstream_grads(H, W, seed=1).items()}
+    g2 = {k: v.to(DEV) for k, v in S.upstream_grads(H, W, seed=2).items()}
+
+    def bwd(g):
+        return _C.rasterize_gaussians_backward(*ga[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], alpha,
+                                               normal, mdepth, _gpu(c["cam"].camera_center), radii, out[6], K,
+                                               out[7], out[8], out[9], True, False)
+
+    b1, b2 = bwd(g1), bwd(g2)
+    b12 = bwd({k: g1[k] + 2 * g2[k] for k in g1})
+    culled = radii == 0
+    for name, x, y, z in zip(GRAD_NAMES, b1, b2, b12):
+        if name == "dmeans2D":
+            x, y, z = x[:, :2], y[:, :2], z[:, :2]
+        if x.numel() == 0:
+            continue
+        assert torch.isfinite(z).all(), name
+        assert float(z[culled].abs().max()) == 0.0, name
         want = (x + 2 * y).double()
         err = float((z.double() - want).norm() / want.norm().clamp_min(1e-30))
         assert err <= 1e-4, (name, err)
