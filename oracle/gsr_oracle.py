@@ -68,6 +68,16 @@ def lib():
         L.gsro_get_tiles.argtypes = [ctypes.c_void_p, _u32, _u32]
         L.gsro_get_n_contrib.argtypes = [ctypes.c_void_p, _u32]
         L.gsro_get_bwd_accum.argtypes = [ctypes.c_void_p, _d, _d, _d]
+        L.gsro_sample_forward.restype = ctypes.c_void_p
+        L.gsro_sample_forward.argtypes = ([ctypes.c_int] * 4 + [_f] * 4 + [ctypes.c_float] + [_f] * 5
+                                          + [ctypes.c_float] * 3 + [_f, _u8, _i, _i, _i])
+        L.gsro_sample_backward.restype = ctypes.c_int
+        L.gsro_sample_backward.argtypes = ([ctypes.c_void_p] + [_f] * 4 + [ctypes.c_float] + [_f] * 4
+                                           + [ctypes.c_float] * 3 + [_u8, _f] + [_f] * 6)
+        L.gsro_sample_free.argtypes = [ctypes.c_void_p]
+        L.gsro_sample_get_points.argtypes = [ctypes.c_void_p, _f, _u32, _u32, _f]
+        L.gsro_sample_gaussians.restype = ctypes.c_void_p
+        L.gsro_sample_gaussians.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -113,9 +123,9 @@ class State:
         self.ptr, self.P, self.W, self.H, self.K = ptr, P, W, H, K
 
     def __del__(self):
-        if getattr(self, "ptr", None) and _lib is not None:
+        if getattr(self, "ptr", None) and _lib is not None and not hasattr(self, "_borrowed_from"):
             _lib.gsro_free(self.ptr)
-            self.ptr = None
+        self.ptr = None
 
     @property
     def tiles(self):
@@ -257,3 +267,85 @@ def eval_color(D, mean, campos, sh, sg_axis=None, sg_sharpness=None, sg_color=No
 
 def higher_msb(n: int) -> int:
     return int(lib().gsro_higher_msb(int(n)))
+
+
+class SampleState:
+    """Owns the oracle's sample_depth state (Gaussian binning + per-point results)."""
+
+    def __init__(self, ptr, P, PN, W, H, K):
+        self.ptr, self.P, self.PN, self.W, self.H, self.K = ptr, P, PN, W, H, K
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.gsro_sample_free(self.ptr)
+            self.ptr = None
+
+    def points(self) -> dict:
+        PN = self.PN
+        out = dict(points2D=np.zeros((PN, 2), np.float32), tile=np.zeros(PN, np.uint32),
+                   n_contrib=np.zeros(PN, np.uint32), median_depth=np.zeros(PN, np.float32))
+        lib().gsro_sample_get_points(self.ptr, _p(out["points2D"]), _p(out["tile"], _u32),
+                                     _p(out["n_contrib"], _u32), _p(out["median_depth"]))
+        return out
+
+    def gaussians(self) -> State:
+        """The Gaussian side as a borrowed State (binning, geometry accessors)."""
+        st = State.__new__(State)
+        st.ptr, st.P, st.W, st.H, st.K = lib().gsro_sample_gaussians(self.ptr), self.P, self.W, self.H, self.K
+        st._borrowed_from = self
+        return st
+
+
+def sample_forward(points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+                   projmatrix, tan_fovx, tan_fovy, kernel_size, image_height, image_width, campos,
+                   prefiltered=False) -> dict:
+    """Same argument list as _C.sample_rasterized_depth (DGR/rasterize_points.cu:459-476)."""
+    L = lib()
+    pts = _np(points3D)
+    shape = tuple(points3D.shape) if hasattr(points3D, "shape") else np.asarray(points3D).shape
+    PN = 0 if pts is None else pts.size // 3
+    means3D = _np(means3D)
+    P = 0 if means3D is None else means3D.shape[0]
+    H, W = int(image_height), int(image_width)
+    output = np.zeros(shape, np.float32)
+    inside = np.zeros(shape[:-1], np.uint8)
+    if P == 0 or PN == 0:
+        return dict(num_rendered=0, num_points=0, num_duplicated_tiles=0, output=output, inside=inside.astype(bool),
+                    state=None)
+    keep = [pts, means3D, _np(opacity), _np(scales), _np(rotations), _np(cov3D_precomp), _np(viewmatrix),
+            _np(projmatrix), _np(campos)]
+    K, RN, TN = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    ptr = L.gsro_sample_forward(PN, P, W, H, _p(keep[0]), _p(keep[1]), _p(keep[2]), _p(keep[3]),
+                                float(scale_modifier), _p(keep[4]), _p(keep[5]), _p(keep[6]), _p(keep[7]),
+                                _p(keep[8]), float(tan_fovx), float(tan_fovy), float(kernel_size), _p(output),
+                                _p(inside, _u8), ctypes.byref(K), ctypes.byref(RN), ctypes.byref(TN))
+    st = SampleState(ptr, P, PN, W, H, K.value)
+    return dict(num_rendered=K.value, num_points=RN.value, num_duplicated_tiles=TN.value, output=output,
+                inside=inside.astype(bool), state=st)
+
+
+def sample_backward(state: SampleState, points3D, means3D, opacity, scales, rotations, scale_modifier,
+                    cov3D_precomp, viewmatrix, projmatrix, inside, dL_doutput, tan_fovx, tan_fovy,
+                    kernel_size) -> dict:
+    """Same meaning as _C.sample_rasterized_depth_backward (DGR/rasterize_points.cu:555-633):
+    returns dopacity, dmeans3D, dcov3D, dscales, drotations, dpoints3D."""
+    L = lib()
+    pts = _np(points3D)
+    shape = tuple(points3D.shape) if hasattr(points3D, "shape") else np.asarray(points3D).shape
+    means3D = _np(means3D)
+    P = means3D.shape[0]
+    out = dict(dopacity=np.zeros((P, 1), np.float32), dmeans3D=np.zeros((P, 3), np.float32),
+               dcov3D=np.zeros((P, 6), np.float32), dscales=np.zeros((P, 3), np.float32),
+               drotations=np.zeros((P, 4), np.float32), dpoints3D=np.zeros(shape, np.float32))
+    if state is None:
+        return out
+    keep = [pts, means3D, _np(opacity), _np(scales), _np(rotations), _np(cov3D_precomp), _np(viewmatrix),
+            _np(projmatrix), _np(inside, np.uint8), _np(dL_doutput)]
+    rc = L.gsro_sample_backward(state.ptr, _p(keep[0]), _p(keep[1]), _p(keep[2]), _p(keep[3]),
+                                float(scale_modifier), _p(keep[4]), _p(keep[5]), _p(keep[6]), _p(keep[7]),
+                                float(tan_fovx), float(tan_fovy), float(kernel_size), _p(keep[8], _u8),
+                                _p(keep[9]), _p(out["dopacity"]), _p(out["dmeans3D"]), _p(out["dcov3D"]),
+                                _p(out["dscales"]), _p(out["drotations"]), _p(out["dpoints3D"]))
+    if rc != 0:
+        raise RuntimeError(f"oracle sample backward failed: {rc}")
+    return out

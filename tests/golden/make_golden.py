@@ -15,6 +15,9 @@ reference's CUDA rasterizer, which cannot build in this image):
   boundary.json    DGR/diff_gaussian_rasterization/__init__.py:23-336 — the
                    exact _C argument tuples (order, kinds, dtypes, shapes) and
                    the 12-gradient routing, recorded with a stub `_C`.
+  boundary_sample.json  DGR/diff_gaussian_rasterization/__init__.py:470-655 —
+                   the same for GaussianRasterizer.sample_depth / _SampleDepth
+                   (_C.sample_rasterized_depth{,_backward}).
 """
 from __future__ import annotations
 
@@ -168,8 +171,26 @@ def boundary_fixture():
         calls["mark_visible"] = [describe(a) for a in args]
         return torch.ones(P, dtype=torch.bool)
 
+    scalls = {}
+    PTS = (4, 6, 3)
+
+    def sample_rasterized_depth(*args):
+        scalls["forward"] = [describe(a) for a in args]
+        out = torch.full(PTS, 5.0)
+        inside = torch.ones(PTS[:-1], dtype=torch.bool)
+        bufs = [torch.zeros(3, dtype=torch.uint8) for _ in range(6)]
+        return (11, 7, 3, out, inside, *bufs)
+
+    def sample_rasterized_depth_backward(*args):
+        scalls["backward"] = [describe(a) for a in args]
+        scalls["backward_counts"] = [args[23], args[24], args[25]]
+        shapes = [(P, 1), (P, 3), (P, 6), (P, 3), (P, 4), PTS]
+        return tuple(torch.full(s, float(i + 1)) for i, s in enumerate(shapes))
+
     _stub("diff_gaussian_rasterization._C", rasterize_gaussians=rasterize_gaussians,
-          rasterize_gaussians_backward=rasterize_gaussians_backward, mark_visible=mark_visible)
+          rasterize_gaussians_backward=rasterize_gaussians_backward, mark_visible=mark_visible,
+          sample_rasterized_depth=sample_rasterized_depth,
+          sample_rasterized_depth_backward=sample_rasterized_depth_backward)
     pkg = types.ModuleType("diff_gaussian_rasterization")
     pkg.__path__ = [os.path.join(REF, "submodules/diff-gaussian-rasterization/diff_gaussian_rasterization")]
     sys.modules["diff_gaussian_rasterization"] = pkg
@@ -212,6 +233,29 @@ def boundary_fixture():
     calls["settings_fields"] = list(dgr.GaussianRasterizationSettings._fields)
     with open(os.path.join(OUT, "boundary.json"), "w") as f:
         json.dump(calls, f, indent=1)
+
+    # sample_depth (DGR/__init__.py:470-655)
+    sin = dict(points3D=torch.zeros(PTS), means3D=torch.zeros(P, 3), opacities=torch.zeros(P, 1),
+               scales=torch.zeros(P, 3), rotations=torch.zeros(P, 4))
+    for v in sin.values():
+        v.requires_grad_(True)
+    depth, inside = rz.sample_depth(**sin)
+    scalls["forward_outputs"] = [describe(depth), describe(inside)]
+    (depth * 2.0).sum().backward()
+    scalls["grad_routing"] = {k: (None if v.grad is None else float(v.grad.flatten()[0])) for k, v in sin.items()}
+    errs = {}
+    for name, kw in [("no_cov", dict(scales=None)), ("both_cov", dict(cov3D_precomp=torch.zeros(P, 6)))]:
+        args = dict(sin)
+        args.update(kw)
+        try:
+            rz.sample_depth(**args)
+            errs[name] = None
+        except Exception as e:  # noqa: BLE001 - record the reference's behaviour
+            errs[name] = type(e).__name__ + ": " + str(e)
+    scalls["errors"] = errs
+    scalls["settings_kernel_size"] = 0.1
+    with open(os.path.join(OUT, "boundary_sample.json"), "w") as f:
+        json.dump(scalls, f, indent=1)
 
 
 def main():

@@ -322,3 +322,92 @@ def test_mark_visible():
     cam = S.make_camera(16, 16)
     means = np.array([[0, 0, 0.1], [0, 0, 0.3], [5, 5, 1.0], [0, 0, -1]], np.float32)
     assert list(O.mark_visible(means, cam.world_view_transform)) == [False, True, True, False]
+
+
+# ------------------------------------------------------------ sample_depth
+def sample_points(c, n, seed, z_range=(1.5, 4.5)):
+    """Random 3D points in the camera's view (pixel position + depth), plus a
+    few behind the near plane and a few projecting outside the image."""
+    g = torch.Generator().manual_seed(seed)
+    W, H = c["W"], c["H"]
+    fx, fy = W / (2 * c["tanx"]), H / (2 * c["tany"])
+    px = torch.rand(n, generator=g) * (W + 8) - 4
+    py = torch.rand(n, generator=g) * (H + 8) - 4
+    z = torch.rand(n, generator=g) * (z_range[1] - z_range[0]) + z_range[0]
+    z[: max(1, n // 50)] = 0.1  # behind the near plane
+    cam_pts = torch.stack([(px - (W - 1) / 2) / fx * z, (py - (H - 1) / 2) / fy * z, z], 1)
+    V = c["cam"].world_view_transform  # p_view = p @ V[:3, :3] + V[3, :3]
+    world = (cam_pts - V[3, :3]) @ torch.linalg.inv(V[:3, :3])
+    return world.float().contiguous()
+
+
+def sample_args(c, pts, kernel_size=0.0):
+    inp = c["inp"]
+    return (pts, inp["means3D"], inp["opacities"], inp["scales"], inp["rotations"], 1.0, None,
+            c["cam"].world_view_transform, c["cam"].full_proj_transform, c["tanx"], c["tany"], kernel_size, c["H"],
+            c["W"], c["cam"].camera_center, False)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_sample_depth_matches_float64_autograd(seed):
+    """sample_depth forward (median depth at points, sample_forward.cu:430-657)
+    and every gradient of its backward (sample_backward.cu:42-359 + the
+    Gaussian preprocess backward) against the float64 autograd restatement."""
+    c = Hh.small_case(P=150, W=40, H=32, seed=seed)
+    pts = sample_points(c, 300, seed + 10).reshape(20, 15, 3)
+    o = O.sample_forward(*sample_args(c, pts))
+    assert o["num_points"] > 150 and o["inside"].sum() > 50
+    op = o["state"].points()
+    cam = c["cam"]
+    inp = {k: v.double().clone().requires_grad_(True) for k, v in c["inp"].items()}
+    p64 = pts.double().clone().requires_grad_(True)
+    m2d = torch.zeros(150, 3, dtype=torch.float64)
+    pre = R.preprocess(inp["means3D"], inp["scales"], inp["rotations"], inp["opacities"], inp["shs"],
+                       inp["sg_axis"], inp["sg_sharpness"], inp["sg_color"], m2d, cam.world_view_transform.double(),
+                       cam.full_proj_transform.double(), cam.camera_center.double(), c["W"], c["H"], c["tanx"],
+                       c["tany"], 0.0, 3, 0)
+    lists, _ = R.binning(pre, c["W"], c["H"])
+    out = R.sample(pre, lists, p64, cam.world_view_transform.double(), cam.full_proj_transform.double(), c["W"],
+                   c["H"], mdepth_override=op["median_depth"].astype(np.float64))
+    assert np.array_equal(o["inside"], out["inside"].numpy())
+    assert np.array_equal(op["n_contrib"], out["n_contrib"].numpy())
+    ref_md = out["mdepth"].numpy()
+    assert Hh.rel_err(op["median_depth"], ref_md) < 5e-5
+    assert Hh.rel_err(o["output"], out["output"].detach().numpy()) < 5e-5
+    g = torch.randn(pts.shape, generator=torch.Generator().manual_seed(seed)) * 1e-2
+    L = (out["output"] * g.double()).sum() + R.sample_surrogate(out, g.double())
+    L.backward()
+    b = O.sample_backward(o["state"], *sample_args(c, pts)[:9], o["inside"], g, c["tanx"], c["tany"], 0.0)
+    q = c["inp"]["rotations"].double().numpy()
+    tang = lambda v: v - q * (q * v).sum(1, keepdims=True)  # noqa: E731
+    checks = {"dmeans3D": (b["dmeans3D"], inp["means3D"].grad.numpy()),
+              "dscales": (b["dscales"], inp["scales"].grad.numpy()),
+              "drotations": (tang(b["drotations"]), tang(inp["rotations"].grad.numpy())),
+              "dopacity": (b["dopacity"], inp["opacities"].grad.numpy()),
+              "dpoints3D": (b["dpoints3D"], p64.grad.numpy())}
+    for k, (mine, ref) in checks.items():
+        assert np.abs(ref).max() > 0, k
+        assert Hh.rel_err(mine, ref) < 2e-4, (k, Hh.rel_err(mine, ref))
+
+
+def test_sample_depth_at_pixel_centres_equals_render():
+    """A point placed on a pixel's ray samples the median depth the render
+    forward computed for that pixel (same algorithm, same Gaussian lists)."""
+    c = Hh.small_case(P=300, W=64, H=48, seed=1)
+    o = O.forward(*Hh.oracle_args(c))
+    md = o["mdepth"][0]
+    md_in = np.zeros_like(md)
+    md_in[1:-1, 1:-1] = md[1:-1, 1:-1]  # border centres may round outside [0, W-1] and be culled
+    ys, xs = np.nonzero(md_in > 0)
+    W, H = c["W"], c["H"]
+    fx, fy = W / (2 * c["tanx"]), H / (2 * c["tany"])
+    z = torch.tensor(md[ys, xs])
+    cam_pts = torch.stack([(torch.tensor(xs, dtype=torch.float32) - (W - 1) / 2) / fx * z,
+                           (torch.tensor(ys, dtype=torch.float32) - (H - 1) / 2) / fy * z, z], 1)
+    V = c["cam"].world_view_transform
+    pts = ((cam_pts - V[3, :3]) @ torch.linalg.inv(V[:3, :3])).float().contiguous()
+    s = O.sample_forward(*sample_args(c, pts))
+    zs = s["output"][:, 2]
+    close = np.abs(zs - md[ys, xs]) <= 1e-4 * np.abs(md).max()
+    assert close.mean() > 0.995, close.mean()  # points land within ~1e-5 px of the centre
+    assert s["inside"].mean() > 0.995

@@ -342,3 +342,138 @@ def median_depth_surrogate(out, dL_dmdepth):
         kappa = torch.where(valid, kappa, torch.zeros_like(kappa))
         tot = tot + (kappa.detach() * 0.5 * logT).sum()
     return tot
+
+
+def sample(pre, lists, points3D, view, proj, W, H, split=8, iters=5, sample_range=0.4, mdepth_override=None):
+    """Median depth at 3D points (sample_forward.cu:9-53, 430-657), float64.
+
+    Returns output [N, 3] = (pnx, pny, 1) * mdepth * rln with the median depth
+    held constant (its gradient comes from `sample_surrogate`, the implicit
+    derivative the reference's sample backward computes,
+    sample_backward.cu:170-354), the inside flags, the per-point median depth
+    (along-ray) and the surrogate pieces."""
+    dt = pre["xy"].dtype
+    pts = points3D.reshape(-1, 3)
+    N = pts.shape[0]
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    t = pts @ view[:3, :3] + view[3, :3]
+    p_hom = pts @ proj[:3] + proj[3]
+    ndc = p_hom[:, :2] / (p_hom[:, 3:4] + 1e-7)
+    xy = torch.stack([((ndc[:, 0] + 1.0) * W - 1.0) * 0.5, ((ndc[:, 1] + 1.0) * H - 1.0) * 0.5], 1)
+    xyd = xy.detach()
+    valid = ((t[:, 2] > 0.2) & (xyd[:, 0] >= 0) & (xyd[:, 0] <= W - 1) & (xyd[:, 1] >= 0)
+             & (xyd[:, 1] <= H - 1)).detach()
+    tx = torch.clamp(((xyd[:, 0] + 0.5) / 16).floor().long(), 0, gx - 1)
+    ty = torch.clamp(((xyd[:, 1] + 0.5) / 16).floor().long(), 0, gy - 1)
+    tile = torch.where(valid, ty * gx + tx, torch.full_like(tx, -1))
+    fx = W / (2.0 * pre["_tanx"])
+    fy = H / (2.0 * pre["_tany"])
+    pnx = (xy[:, 0] - (W - 1) / 2.0) / fx
+    pny = (xy[:, 1] - (H - 1) / 2.0) / fy
+    rln = 1.0 / torch.sqrt(pnx ** 2 + pny ** 2 + 1)
+    tm_all = torch.zeros(N, dtype=dt)
+    inside = torch.zeros(N, dtype=torch.bool)
+    last_all = torch.zeros(N, dtype=torch.long)
+    terms = []
+    for tl in torch.unique(tile[tile >= 0]).tolist():
+        idx = torch.nonzero(tile == tl)[:, 0]
+        lst = lists[tl]
+        n = idx.shape[0]
+        pxy = xy[idx]
+        T = torch.ones(n, dtype=dt)
+        m0 = torch.zeros(n, dtype=dt)
+        done = torch.zeros(n, dtype=torch.bool)
+        last = torch.zeros(n, dtype=torch.long)
+        used = []
+        for k, g in enumerate(lst):
+            d = pre["xy"][g][None] - pxy
+            co = pre["conic"][g]
+            power = -0.5 * (co[0] * d[:, 0] ** 2 + co[2] * d[:, 1] ** 2) - co[1] * d[:, 0] * d[:, 1]
+            al = torch.clamp(pre["opac"][g] * torch.exp(power), max=0.99)
+            ok = (~done) & (power <= 0).detach() & (al >= 1.0 / 255.0).detach()
+            test_T = T * (1 - al)
+            stop = ok & (test_T < 1e-4).detach()
+            done = done | stop
+            ok = ok & ~stop
+            rp = pre["ray_plane"][g]
+            tp = rp[0] * d[:, 0] + rp[1] * d[:, 1] + rp[2]
+            m0 = torch.where(ok & (T > 0.5).detach(), tp.detach(), m0)
+            T = torch.where(ok, test_T, T)
+            last = torch.where(ok, torch.full_like(last, k + 1), last)
+            used.append((al, tp, rp[3], (power <= 0).detach() & (al >= 1.0 / 255.0).detach()))
+        with torch.no_grad():
+            dmin = torch.clamp(m0 - sample_range, min=0.0)
+            dmax = torch.clamp(m0 + sample_range, min=0.0)
+            in_range = T.detach() <= 0.45
+            Tp = torch.ones(n, split + 1, dtype=dt)
+            for it in range(iters):
+                first = it == 0
+                ids = range(0, split + 1) if first else range(1, split)
+                for sidx in ids:
+                    Tp[:, sidx] = 1.0
+                interval = (dmax - dmin) / split
+                for k, (al, tp, rs, mask) in enumerate(used):
+                    m = mask & ((k + 1) <= last) & in_range
+                    if not bool(m.any()):
+                        continue
+                    for sidx in ids:
+                        ts = dmin + interval * sidx
+                        delta = (ts - tp) * rs
+                        gg = torch.exp(-0.5 * delta * delta) if float(rs) > 0 else torch.zeros_like(ts)
+                        omg = 1 - al * gg
+                        f = torch.where(ts > tp, 1 - al, omg) / torch.sqrt(omg)
+                        Tp[:, sidx] = torch.where(m, Tp[:, sidx] * f, Tp[:, sidx])
+                if first:
+                    in_range = (Tp[:, 0] >= 0.5) & (Tp[:, split] <= 0.5) & in_range
+                start = torch.zeros(n, dtype=torch.long)
+                for p_ in range(1, split):
+                    start = torch.where(Tp[:, p_] >= 0.5, torch.full_like(start, p_), start)
+                dmax = dmin + (start + 1) * interval
+                dmin = dmin + start * interval
+                Tp0 = Tp.gather(1, start[:, None])[:, 0]
+                Tp8 = Tp.gather(1, (start + 1)[:, None])[:, 0]
+                Tp[:, 0], Tp[:, split] = Tp0, Tp8
+            wmax = ((Tp[:, 0] - 0.5) / (Tp[:, 0] - Tp[:, split])).nan_to_num(0.0).clamp(0, 1)
+            tm = torch.where(in_range, wmax * dmax + (1 - wmax) * dmin, torch.zeros_like(dmin))
+        tm_all[idx] = tm
+        inside[idx] = in_range
+        last_all[idx] = last
+        if mdepth_override is not None:
+            tm = torch.as_tensor(mdepth_override, dtype=dt).reshape(-1)[idx]
+        logT = torch.zeros(n, dtype=dt)
+        dlogT_dt = torch.zeros(n, dtype=dt)
+        valid_pt = in_range & (last > 0)
+        for k, (al, tp, rs, mask) in enumerate(used):
+            m = mask & ((k + 1) <= last) & valid_pt
+            if not bool(m.any()):
+                continue
+            delta = (tm - tp) * rs
+            Gt = al * torch.exp(-0.5 * delta * delta)
+            f = torch.where(tm > tp, torch.log(1 - al) - 0.5 * torch.log(1 - Gt), 0.5 * torch.log(1 - Gt))
+            if float(rs.detach()) <= 0:
+                f = torch.where(tm > tp, torch.log(1 - al), torch.zeros_like(f))
+            logT = logT + torch.where(m, f, torch.zeros_like(f))
+            with torch.no_grad():
+                dd = -0.5 * Gt / (1 - Gt) * delta.abs() * rs
+                dlogT_dt = dlogT_dt + torch.where(m, dd, torch.zeros_like(dd))
+        terms.append((idx, logT, dlogT_dt, valid_pt))
+    tm_used = tm_all if mdepth_override is None else torch.as_tensor(mdepth_override, dtype=dt).reshape(-1)
+    depth = tm_used.detach() * rln
+    out = torch.stack([pnx * depth, pny * depth, depth], 1)
+    out = torch.where(valid[:, None], out, torch.zeros_like(out))
+    return dict(output=out.reshape(points3D.shape), inside=inside.reshape(points3D.shape[:-1]), mdepth=tm_all,
+                n_contrib=last_all, tile=tile, _terms=terms, _pn=(pnx.detach(), pny.detach(), rln.detach()))
+
+
+def sample_surrogate(out, dL_doutput):
+    """Scalar whose gradient is the reference's implicit median-depth gradient
+    of the sampled points (sample_backward.cu:138-215, 289-301)."""
+    g = dL_doutput.reshape(-1, 3)
+    pnx, pny, rln = out["_pn"]
+    dL_dDepth = rln * (g[:, 0] * pnx + g[:, 1] * pny + g[:, 2])
+    tot = 0.0
+    for idx, logT, dlogT_dt, valid in out["_terms"]:
+        kappa = dL_dDepth[idx] / torch.clamp(-0.5 * dlogT_dt, min=1e-7)
+        kappa = torch.where(valid, kappa, torch.zeros_like(kappa))
+        tot = tot + (kappa.detach() * 0.5 * logT).sum()
+    return tot
