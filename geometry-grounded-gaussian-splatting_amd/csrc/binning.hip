@@ -91,13 +91,14 @@ __device__ __forceinline__ uint32_t live_count(const Ellipse& E, const TileRect&
 // Live tiles per Gaussian, in index order (coalesced reads).
 __global__ void __launch_bounds__(256)
     live_tiles_kernel(int P, const uint32_t* __restrict__ tiles_touched, const Splat* __restrict__ splats,
-                      const int* __restrict__ radii, uint32_t gx, uint32_t gy, uint32_t* __restrict__ tiles_live) {
+                      const int* __restrict__ radii, uint32_t gx, uint32_t gy, float pad,
+                      uint32_t* __restrict__ tiles_live) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= P) return;
     uint32_t live = 0;
     if (tiles_touched[idx]) {
         const float4 w0 = splats[idx].w0, w1 = splats[idx].w1;
-        live = live_count(make_ellipse(w0, w1), tile_rect(w0.x, w0.y, radii[idx], gx, gy));
+        live = live_count(make_ellipse(w0, w1, pad), tile_rect(w0.x, w0.y, radii[idx], gx, gy));
     }
     tiles_live[idx] = live;
 }
@@ -124,7 +125,7 @@ hipError_t launch_live_counts(const FwdParams& p, const GeomState& gs, const int
     const int P = p.P;
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(live_tiles_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, P, gs.tiles_touched,
-                       gs.splats, radii, p.grid_x, p.grid_y, gs.tiles_live);
+                       gs.splats, radii, p.grid_x, p.grid_y, p.cull_pad, gs.tiles_live);
     hipLaunchKernelGGL(gather_counts_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, P, gs.order,
                        gs.tiles_touched, gs.tiles_live, gs.counts);
     return hipGetLastError();
@@ -163,7 +164,7 @@ template <typename KeyT>
 __global__ void __launch_bounds__(256)
     emit_keys_kernel(int P, const uint32_t* __restrict__ order, const Splat* __restrict__ splats,
                      const uint2* __restrict__ offsets, const int* __restrict__ radii, uint32_t grid_x,
-                     uint32_t grid_y, KeyT* __restrict__ keys, uint32_t* __restrict__ values) {
+                     uint32_t grid_y, float pad, KeyT* __restrict__ keys, uint32_t* __restrict__ values) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const bool in = q < P;
@@ -175,7 +176,7 @@ __global__ void __launch_bounds__(256)
     TileRect R{0, 0, 0, 0};
     if (n) {
         const float4 w0 = splats[idx].w0, w1 = splats[idx].w1;
-        E = make_ellipse(w0, w1);
+        E = make_ellipse(w0, w1, pad);
         R = tile_rect(w0.x, w0.y, radii[idx], grid_x, grid_y);
     }
     const bool big = n > kCoopLive;
@@ -231,10 +232,12 @@ hipError_t launch_emit_keys(const FwdParams& p, const GeomState& gs, const int* 
     const dim3 grid((p.P + 255) / 256);
     if (bs.key_bytes == 2)
         hipLaunchKernelGGL(emit_keys_kernel<uint16_t>, grid, dim3(256), 0, stream, p.P, gs.order, gs.splats,
-                           gs.offsets, radii, p.grid_x, p.grid_y, (uint16_t*)bs.keys_unsorted, bs.values_unsorted);
+                           gs.offsets, radii, p.grid_x, p.grid_y, p.cull_pad, (uint16_t*)bs.keys_unsorted,
+                           bs.values_unsorted);
     else
         hipLaunchKernelGGL(emit_keys_kernel<uint32_t>, grid, dim3(256), 0, stream, p.P, gs.order, gs.splats,
-                           gs.offsets, radii, p.grid_x, p.grid_y, (uint32_t*)bs.keys_unsorted, bs.values_unsorted);
+                           gs.offsets, radii, p.grid_x, p.grid_y, p.cull_pad, (uint32_t*)bs.keys_unsorted,
+                           bs.values_unsorted);
     return hipGetLastError();
 }
 

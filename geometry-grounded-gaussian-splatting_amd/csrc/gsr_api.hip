@@ -120,6 +120,45 @@ size_t carve_bwd(void* base, int P, BwdState& s) {
     return c.off;
 }
 
+// sample_depth buffers (the reference's pointBuffer, point_binningBuffer,
+// tileBuffer<true> and duplicatedTileBuffer, rasterizer_impl.h)
+size_t carve_points(void* base, int PN, PointState& s) {
+    Carver c(base);
+    s.xy = c.take<float2>(PN);
+    s.last = c.take<uint32_t>(PN);
+    s.mdepth = c.take<float>(PN);
+    s.dT = c.take<float>(PN);
+    s.cached = c.take<uint8_t>(PN);
+    return c.off + 256;
+}
+
+size_t carve_point_binning(void* base, int PN, uint32_t tiles, PointBinState& s) {
+    Carver c(base);
+    s.keys_unsorted = c.take<uint32_t>(PN);
+    s.keys = c.take<uint32_t>(PN);
+    s.pt_list = c.take<uint32_t>(PN);
+    s.sort_tmp_bytes = point_sort_temp_bytes(PN, tiles);
+    s.sort_tmp = c.take<char>(s.sort_tmp_bytes);
+    return c.off + 256;
+}
+
+size_t carve_sample_tiles(void* base, int T, TileState& ts, SampleTiles& st) {
+    Carver c(base);
+    ts.ranges = c.take<uint2>(T);
+    ts.max_contrib = c.take<uint32_t>(T);
+    st.counts = c.take<uint32_t>(T);
+    st.pt_ranges = c.take<uint2>(T);
+    st.chunk_off = c.take<uint32_t>((size_t)T + 1);
+    st.totals = c.take<uint32_t>(4);
+    return c.off + 256;
+}
+
+size_t carve_chunks(void* base, uint32_t n, ChunkState& s) {
+    Carver c(base);
+    s.chunk_max = c.take<uint32_t>(n ? n : 1);
+    return c.off + 256;
+}
+
 // 256-B alignment of the carve base (callbacks may return any alignment)
 void* aligned_base(void* p) {
     return reinterpret_cast<void*>(align_up(reinterpret_cast<uintptr_t>(p), 256));
@@ -162,6 +201,8 @@ FwdParams make_params(int P, int D, int SHM, int SGD, int SGM, const float* back
     p.grid_x = (W + kTile - 1) / kTile;
     p.grid_y = (H + kTile - 1) / kTile;
     p.require_depth = require_depth != 0;
+    p.no_color = false;
+    p.cull_pad = 0.f;
     return p;
 }
 
@@ -275,6 +316,21 @@ int gsr_debug_binning(const void* binning_buffer, const void* tile_buffer, int R
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "debug binning", e);
 }
 
+int gsr_debug_sample_points(const void* point_buffer, int PN, float* median_depth_out, uint32_t* last_out,
+                            void* stream_ptr) {
+    if (!point_buffer || PN < 0) return fail(GSR_ERR_ARGS, "invalid arguments");
+    PointState ps;
+    carve_points(aligned_base(const_cast<void*>(point_buffer)), PN, ps);
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    hipError_t e = hipSuccess;
+    if (median_depth_out && PN)
+        e = hipMemcpyAsync(median_depth_out, ps.mdepth, sizeof(float) * PN, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess && last_out && PN)
+        e = hipMemcpyAsync(last_out, ps.last, sizeof(uint32_t) * PN, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "debug sample points", e);
+}
+
 int gsr_set_option(int opt, int value) {
     if (opt < 0 || opt >= gsr::kNumOptions) return fail(GSR_ERR_ARGS, "unknown option");
     gsr::g_options[opt] = value;
@@ -282,7 +338,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 4; }
+int gsr_abi_version(void) { return 5; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -315,7 +371,9 @@ int gsr_timing_collect(double* ms, int* launches) {
 
 const char* gsr_stage_name(int stage) {
     static const char* names[GSR_NUM_STAGES] = {"preprocess", "scan", "emit_keys", "sort", "tile_ranges",
-                                                 "render_fwd", "bwd_clear", "render_bwd", "preprocess_bwd", "depth_order", "tile_lists"};
+                                                 "render_fwd", "bwd_clear", "render_bwd", "preprocess_bwd",
+                                                 "depth_order", "tile_lists", "sample_points", "sample_fwd",
+                                                 "sample_bwd"};
     return (stage >= 0 && stage < GSR_NUM_STAGES) ? names[stage] : "?";
 }
 
@@ -480,6 +538,172 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
     GSR_STAGE(GSR_STAGE_BWD_CLEAR, hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
     GSR_STAGE(GSR_STAGE_RENDER_BWD, launch_render_bwd(b, gs, bs, is, ts, ws, stream), "render backward");
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_bwd(b, gs, ws, stream), "preprocess backward");
+    return GSR_OK;
+}
+
+int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn point_alloc, void* point_ctx, gsr_alloc_fn point_binning_alloc,
+                             void* point_binning_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                             gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P, int width, int height,
+                             const float* points3D, const float* means3D, const float* opacities,
+                             const float* scales, float scale_modifier, const float* rotations,
+                             const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                             const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size,
+                             int prefiltered, float* output, uint8_t* inside, int debug, void* stream_ptr,
+                             int* num_rendered, int* num_points, int* num_duplicated_tiles) {
+    (void)prefiltered;
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    if (num_rendered) *num_rendered = 0;
+    if (num_points) *num_points = 0;
+    if (num_duplicated_tiles) *num_duplicated_tiles = 0;
+    if (P < 0 || PN < 0 || width <= 0 || height <= 0) return fail(GSR_ERR_ARGS, "invalid P / PN / image size");
+    if (P == 0 || PN == 0) return GSR_OK;  // rasterize_points.cu:517: nothing sampled, zero outputs
+    static const float kZeroBg[3] = {0.f, 0.f, 0.f};
+    FwdParams p = make_params(P, 0, 0, 0, 0, kZeroBg, width, height, means3D, nullptr, opacities, scales, rotations,
+                              cov3D_precomp, nullptr, nullptr, nullptr, nullptr, scale_modifier, viewmatrix,
+                              projmatrix, cam_pos, tan_fovx, tan_fovy, kernel_size, 1);
+    p.no_color = true;
+    p.cull_pad = 0.5f;
+    if (!means3D || !opacities || !viewmatrix || !projmatrix || !points3D) return fail(GSR_ERR_ARGS, "missing input");
+    if ((scales && rotations) == (cov3D_precomp != nullptr))
+        return fail(GSR_ERR_ARGS, "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (!output || !inside) return fail(GSR_ERR_ARGS, "missing output buffer");
+    if (!geom_alloc || !binning_alloc || !point_alloc || !point_binning_alloc || !tile_alloc || !dup_tile_alloc)
+        return fail(GSR_ERR_ARGS, "missing allocator");
+    const uint32_t tiles = p.grid_x * p.grid_y;
+
+    GeomState gs;
+    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, gs));
+    if (!gbuf) return fail(GSR_ERR_ALLOC, "geometry buffer allocation failed");
+    carve_geom(aligned_base(gbuf), P, gs);
+    TileState ts;
+    SampleTiles st;
+    void* tbuf = tile_alloc(tile_ctx, carve_sample_tiles(nullptr, (int)tiles, ts, st));
+    if (!tbuf) return fail(GSR_ERR_ALLOC, "tile buffer allocation failed");
+    carve_sample_tiles(aligned_base(tbuf), (int)tiles, ts, st);
+    PointState ps;
+    void* pbuf = point_alloc(point_ctx, carve_points(nullptr, PN, ps));
+    if (!pbuf) return fail(GSR_ERR_ALLOC, "point buffer allocation failed");
+    carve_points(aligned_base(pbuf), PN, ps);
+    PointBinState pb;
+    void* pbbuf = point_binning_alloc(point_binning_ctx, carve_point_binning(nullptr, PN, tiles, pb));
+    if (!pbbuf) return fail(GSR_ERR_ALLOC, "point binning buffer allocation failed");
+    carve_point_binning(aligned_base(pbbuf), PN, tiles, pb);
+
+    GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, gs.radii, stream), "preprocess");
+    const bool lists = list_binning(p.grid_x, p.grid_y);
+    uint2 Ks = make_uint2(0u, 0u);
+    GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+    if (lists) {
+        GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
+    } else {
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_live_counts(p, gs, gs.radii, stream), "live counts");
+        GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
+    }
+    GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_points(p, PN, points3D, ps, pb, st, stream), "sample points");
+    GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_setup(PN, tiles, pb, st, stream), "sample setup");
+    uint32_t totals[4] = {0, 0, 0, 0};
+    if (lists)
+        GSR_TRY(hipMemcpyAsync(&Ks.x, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
+    else
+        GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
+    GSR_TRY(hipMemcpyAsync(totals, st.totals, sizeof(totals), hipMemcpyDeviceToHost, stream), "memcpy totals");
+    {
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
+    }
+    const uint32_t K = Ks.x, K_live = Ks.y, n_chunks = totals[2];
+    BinningState bs;
+    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, bs));
+    if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
+    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, bs);
+    ChunkState cs;
+    void* cbuf = dup_tile_alloc(dup_tile_ctx, carve_chunks(nullptr, n_chunks, cs));
+    if (!cbuf) return fail(GSR_ERR_ALLOC, "duplicated-tile buffer allocation failed");
+    carve_chunks(aligned_base(cbuf), n_chunks, cs);
+    if (lists) {
+        GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_list_binning(p, gs, gs.radii, bs, ts, (int)K, stream), "tile lists");
+    } else {
+        const int tile_bits = (int)higher_msb(tiles);
+        GSR_STAGE(GSR_STAGE_EMIT_KEYS, launch_emit_keys(p, gs, gs.radii, bs, stream), "emit keys");
+        GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K_live, tile_bits, stream), "sort");
+        GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K_live, ts, (int)tiles, stream), "tile ranges");
+    }
+    GSR_STAGE(GSR_STAGE_SAMPLE_FWD,
+              launch_sample_fwd(p, gs, bs, ts, ps, pb, st, cs, n_chunks, output, inside, stream), "sample");
+    if (num_rendered) *num_rendered = (int)K;
+    if (num_points) *num_points = (int)totals[0];
+    if (num_duplicated_tiles) *num_duplicated_tiles = (int)totals[1];
+    return GSR_OK;
+}
+
+int gsr_sample_depth_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int PN, int P, int RN, int R, int TN,
+                              int width, int height, const float* points3D, const float* means3D,
+                              const float* opacities, const float* scales, float scale_modifier,
+                              const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                              const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                              float kernel_size, const void* geom_buffer, const void* binning_buffer,
+                              const void* point_buffer, const void* point_binning_buffer, const void* tile_buffer,
+                              const void* dup_tile_buffer, const uint8_t* inside, const float* dL_doutput,
+                              float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale,
+                              float* dL_drot, float* dL_dpoints3D, int debug, void* stream_ptr) {
+    (void)RN;
+    (void)TN;
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    if (P == 0 || PN == 0) return GSR_OK;
+    if (P < 0 || PN < 0 || width <= 0 || height <= 0) return fail(GSR_ERR_ARGS, "invalid P / PN / image size");
+    static const float kZeroBg[3] = {0.f, 0.f, 0.f};
+    SampleBwdParams b;
+    b.f = make_params(P, 0, 0, 0, 0, kZeroBg, width, height, means3D, nullptr, opacities, scales, rotations,
+                      cov3D_precomp, nullptr, nullptr, nullptr, nullptr, scale_modifier, viewmatrix, projmatrix,
+                      campos, tan_fovx, tan_fovy, kernel_size, 1);
+    b.f.no_color = true;
+    b.f.cull_pad = 0.5f;
+    b.PN = PN;
+    b.points3D = points3D;
+    b.inside = inside;
+    b.dL_doutput = dL_doutput;
+    b.dL_dpoints3D = dL_dpoints3D;
+    if (!geom_buffer || !binning_buffer || !point_buffer || !point_binning_buffer || !tile_buffer ||
+        !dup_tile_buffer || !inside || !dL_doutput || !dL_dopacity || !dL_dmean3D || !dL_dpoints3D || !points3D)
+        return fail(GSR_ERR_ARGS, "missing backward buffer");
+    if (scales && (!dL_dscale || !dL_drot)) return fail(GSR_ERR_ARGS, "missing scale/rotation gradients");
+    if (cov3D_precomp && !dL_dcov3D) return fail(GSR_ERR_ARGS, "missing cov3D gradient");
+    const uint32_t tiles = b.f.grid_x * b.f.grid_y;
+    GeomState gs;
+    carve_geom(aligned_base(const_cast<void*>(geom_buffer)), P, gs);
+    BinningState bs;
+    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, P, b.f.grid_x, b.f.grid_y, bs);
+    PointState ps;
+    carve_points(aligned_base(const_cast<void*>(point_buffer)), PN, ps);
+    PointBinState pb;
+    carve_point_binning(aligned_base(const_cast<void*>(point_binning_buffer)), PN, tiles, pb);
+    TileState ts;
+    SampleTiles st;
+    carve_sample_tiles(aligned_base(const_cast<void*>(tile_buffer)), (int)tiles, ts, st);
+    ChunkState cs;
+    {
+        Carver c(aligned_base(const_cast<void*>(dup_tile_buffer)));
+        cs.chunk_max = c.take<uint32_t>(1);  // first in the buffer (carve_chunks)
+    }
+    BwdState ws;
+    const size_t wbytes = carve_bwd(nullptr, P, ws);
+    void* wbuf = geom_bwd_alloc(geom_bwd_ctx, wbytes + 256);
+    if (!wbuf) return fail(GSR_ERR_ALLOC, "backward buffer allocation failed");
+    void* wb = aligned_base(wbuf);
+    carve_bwd(wb, P, ws);
+    GSR_STAGE(GSR_STAGE_BWD_CLEAR, hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
+    GSR_STAGE(GSR_STAGE_SAMPLE_BWD, launch_sample_bwd(b, gs, bs, ts, ps, pb, st, cs, ws, stream), "sample backward");
+    BwdParams pbw{};
+    pbw.f = b.f;
+    pbw.R = R;
+    pbw.radii = gs.radii;
+    pbw.dL_dmean3D = dL_dmean3D;
+    pbw.dL_dopacity = dL_dopacity;
+    pbw.dL_dscale = dL_dscale;
+    pbw.dL_drot = dL_drot;
+    pbw.dL_dcov3D = dL_dcov3D;
+    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_bwd(pbw, gs, ws, stream), "preprocess backward");
     return GSR_OK;
 }
 

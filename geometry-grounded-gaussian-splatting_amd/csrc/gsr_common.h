@@ -112,6 +112,32 @@ struct TileState {
     uint2* ranges;
     uint32_t* max_contrib;
 };
+// ---- sample_depth state (PointState / DuplicatedTileState, rasterizer_impl.h) ----
+constexpr uint32_t kNoTile = 0xffffffffu;
+struct PointState {  // per point (point buffer)
+    float2* xy;        // projected position (pixels)
+    uint32_t* last;    // last contributor
+    float* mdepth;     // median depth along the ray (the reference's pointState.median_depth)
+    float* dT;         // dT/dt_m at mdepth, computed by the forward when `cached`
+    uint8_t* cached;
+};
+struct PointBinState {  // point binning buffer
+    uint32_t* keys_unsorted;  // tile of each point (num_tiles when culled: sorts last)
+    uint32_t* keys;
+    uint32_t* pt_list;        // point indices stably sorted by tile
+    void* sort_tmp;
+    size_t sort_tmp_bytes;
+};
+struct SampleTiles {  // per tile, after TileState in the tile buffer
+    uint32_t* counts;     // valid points per tile
+    uint2* pt_ranges;     // [first, end) in pt_list
+    uint32_t* chunk_off;  // [tiles + 1]: exclusive scan of ceil(count / 256)
+    uint32_t* totals;     // [4]: valid points, reference blocks (512 points each), chunks, 0
+};
+struct ChunkState {  // duplicated-tile buffer: one entry per 256-point chunk
+    uint32_t* chunk_max;  // max contributor over the chunk's points
+};
+
 // ---- backward scratch (replaces GeometryBwdState) ----
 struct BwdState {
     float* acc;      // [P][16]

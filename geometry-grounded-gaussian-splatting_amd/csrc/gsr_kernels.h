@@ -32,6 +32,8 @@ struct FwdParams {
     float tan_fovx, tan_fovy, focal_x, focal_y, kernel_size;
     uint32_t grid_x, grid_y;
     bool require_depth;
+    bool no_color;   // sample_depth: preprocess skips the colour (rasterizer_impl.cu:1080)
+    float cull_pad;  // tile-culling pad in pixels (tiles.h): 0 render, 0.5 sample_depth
 };
 
 struct BwdParams {
@@ -92,6 +94,30 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
 
 // preprocess_bwd.hip
 hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const BwdState& ws, hipStream_t stream);
+
+// render_fwd.hip: the forward raster in SAMPLE mode (median depth at points)
+hipError_t launch_sample_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const TileState& ts,
+                             const PointState& ps, const PointBinState& pb, const SampleTiles& st,
+                             const ChunkState& cs, uint32_t num_chunks, float* out_points, uint8_t* out_inside,
+                             hipStream_t stream);
+
+// sample.hip
+size_t point_sort_temp_bytes(int PN, uint32_t tiles);
+hipError_t launch_sample_points(const FwdParams& p, int PN, const float* points3D, const PointState& ps,
+                                const PointBinState& pb, const SampleTiles& st, hipStream_t stream);
+hipError_t launch_sample_setup(int PN, uint32_t tiles, const PointBinState& pb, const SampleTiles& st,
+                               hipStream_t stream);
+struct SampleBwdParams {
+    FwdParams f;
+    int PN;
+    const float* points3D;
+    const uint8_t* inside;
+    const float* dL_doutput;
+    float* dL_dpoints3D;
+};
+hipError_t launch_sample_bwd(const SampleBwdParams& b, const GeomState& gs, const BinningState& bs,
+                             const TileState& ts, const PointState& ps, const PointBinState& pb,
+                             const SampleTiles& st, const ChunkState& cs, const BwdState& ws, hipStream_t stream);
 
 // mark visible
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,

@@ -76,13 +76,18 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
     const float* acc = a.acc + (size_t)idx * kAccFields;
-    // extension outputs straight from the accumulator (zero for culled Gaussians)
-    a.dL_dmean2D[3 * idx + 0] = acc[kAccMean2D + 0];
-    a.dL_dmean2D[3 * idx + 1] = acc[kAccMean2D + 1];
-    a.dL_dmean2D[3 * idx + 2] = a.acc_abs[idx];
-    a.dL_dcolor[3 * idx + 0] = acc[kAccColor + 0];
-    a.dL_dcolor[3 * idx + 1] = acc[kAccColor + 1];
-    a.dL_dcolor[3 * idx + 2] = acc[kAccColor + 2];
+    // extension outputs straight from the accumulator (zero for culled
+    // Gaussians); sample_depth returns neither (rasterize_points.cu:633)
+    if (a.dL_dmean2D) {
+        a.dL_dmean2D[3 * idx + 0] = acc[kAccMean2D + 0];
+        a.dL_dmean2D[3 * idx + 1] = acc[kAccMean2D + 1];
+        a.dL_dmean2D[3 * idx + 2] = a.acc_abs[idx];
+    }
+    if (a.dL_dcolor) {
+        a.dL_dcolor[3 * idx + 0] = acc[kAccColor + 0];
+        a.dL_dcolor[3 * idx + 1] = acc[kAccColor + 1];
+        a.dL_dcolor[3 * idx + 2] = acc[kAccColor + 2];
+    }
     if (!(a.radii[idx] > 0)) {
         zero_outputs(a, idx);
         return;

@@ -44,6 +44,7 @@ struct PreprocessArgs {
     float* depths;
     Splat* splats;
     uint32_t* tiles_touched;
+    bool no_color;
 };
 
 // ndc2Pix in double, as the reference (auxiliary.h:38-40)
@@ -195,7 +196,10 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
 
     // colour (render_forward.cu:22-78)
     float col[3];
-    if (a.colors_precomp == nullptr) {
+    if (a.no_color) {  // sample_depth (rasterizer_impl.cu:1080): colour unused
+        col[0] = col[1] = col[2] = 0.f;
+        a.clamped[idx] = 0;
+    } else if (a.colors_precomp == nullptr) {
         float dx = px - a.campos[0], dy = py - a.campos[1], dz = pz - a.campos[2];
         const float dl = sqrtf(dx * dx + dy * dy + dz * dz);
         dx /= dl;
@@ -263,6 +267,7 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
     a.H = p.H;
     a.means3D = p.means3D;
     a.colors_precomp = p.colors_precomp;
+    a.no_color = p.no_color;
     a.opacities = p.opacities;
     a.scales = p.scales;
     a.rotations = p.rotations;

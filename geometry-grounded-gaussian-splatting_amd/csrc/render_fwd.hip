@@ -57,6 +57,20 @@ struct RenderFwdArgs {
     float* out_normal;
     float* out_mdepth;
     int passes;  // bisection passes (kSplitIterations; fewer only for GSR_OPT_BISECT_PASSES timing runs)
+    // SAMPLE mode (sample_depth, sample.hip): a workgroup is one chunk of
+    // kTilePixels points of one tile instead of the tile's pixels
+    uint32_t num_chunks;
+    const uint32_t* chunk_off;  // [tiles + 1] exclusive scan of chunks per tile
+    const uint2* pt_ranges;     // [tiles] points of each tile in pt_list
+    const uint32_t* pt_list;    // point indices grouped by tile
+    const float2* pt_xy;        // projected point positions
+    float* out_points;          // [PN][3] camera-space point at the median depth
+    uint8_t* out_inside;        // [PN]
+    uint32_t* pt_last;          // [PN] last contributor
+    float* pt_mdepth;           // [PN] median depth along the ray
+    float* pt_dT;               // [PN] dT/dt_m at pt_mdepth (valid where pt_cached)
+    uint8_t* pt_cached;         // [PN]
+    uint32_t* chunk_max;        // [chunks] max contributor of the chunk
 };
 
 // One contributor's factor on the bisection samples (render_forward.cu:610-621):
@@ -136,7 +150,11 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
 // more than kFarDelta sigma from the splat's peak (exact-constant factors).
 __device__ unsigned long long g_render_stats[8];
 
-template <bool GEOM, bool SKIP, bool STATS = false>
+// SAMPLE: the median depth at arbitrary points (sampleDepthCUDA,
+// sample_forward.cu:430-657) — lanes hold points of one tile's chunk, the
+// composite keeps only T / last / m0 / blended set, and the outputs are the
+// per-point ones.  Everything else (batching, bisection) is shared.
+template <bool GEOM, bool SKIP, bool STATS = false, bool SAMPLE = false>
 __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 256 x 16 B = 16 KB) aliased with the
     // bisection cache (3 x 384 x 16 B = 18 KB), plus the 12 KB of masks:
@@ -151,11 +169,36 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
-    const uint32_t tile = xcd_remap(blockIdx.x, a.num_tiles);
-    const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
-    const int px = tx * kTile + (tid & 15), py = ty * kTile + (tid >> 4);
-    const bool inside = px < a.W && py < a.H;
-    const float pixx = (float)px, pixy = (float)py;
+    uint32_t tile, chunk = 0, pid = 0;
+    int px = 0, py = 0;
+    bool inside;
+    float pixx, pixy;
+    if constexpr (SAMPLE) {
+        // chunks of one tile are consecutive: XCD-contiguous runs of chunks share Gaussian lists
+        chunk = xcd_remap(blockIdx.x, a.num_chunks);
+        uint32_t lo = 0, hi = a.num_tiles;  // last tile with chunk_off[t] <= chunk
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.chunk_off[mid] <= chunk) lo = mid;
+            else hi = mid;
+        }
+        tile = lo;
+        const uint2 pr = a.pt_ranges[tile];
+        const uint32_t slot = pr.x + (chunk - a.chunk_off[tile]) * kTilePixels + tid;
+        inside = slot < pr.y;
+        pid = inside ? a.pt_list[slot] : 0u;
+        const float2 xy = inside ? a.pt_xy[pid] : make_float2(0.f, 0.f);
+        pixx = xy.x;
+        pixy = xy.y;
+    } else {
+        tile = xcd_remap(blockIdx.x, a.num_tiles);
+        const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
+        px = tx * kTile + (tid & 15);
+        py = ty * kTile + (tid >> 4);
+        inside = px < a.W && py < a.H;
+        pixx = (float)px;
+        pixy = (float)py;
+    }
 
     const uint2 range = a.ranges[tile];
     const int total = (int)(range.y - range.x);
@@ -190,11 +233,11 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         if (!(s_alive[i & 1][0] | s_alive[i & 1][1] | s_alive[i & 1][2] | s_alive[i & 1][3])) break;
         const int k = i * kTilePixels + tid;
         if (k < total) {
-            const Splat sp = a.splats[a.point_list[range.x + k]];
-            s_w0[tid] = sp.w0;
-            s_w1[tid] = sp.w1;
-            s_w2[tid] = sp.w2;
-            s_w3[tid] = sp.w3;
+            const Splat* sp = a.splats + a.point_list[range.x + k];
+            s_w0[tid] = sp->w0;
+            s_w1[tid] = sp->w1;
+            s_w2[tid] = sp->w2;
+            if constexpr (!SAMPLE) s_w3[tid] = sp->w3;
         }
         __syncthreads();
         const int n = min(kTilePixels, toDo);
@@ -214,15 +257,19 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             }
             const float aT = alpha * T;
             const float4 w2 = s_w2[j];
-            const float4 w3 = s_w3[j];
-            C0 = __builtin_fmaf(w2.z, aT, C0);
-            C1 = __builtin_fmaf(w2.w, aT, C1);
-            C2 = __builtin_fmaf(w3.x, aT, C2);
+            if constexpr (!SAMPLE) {
+                const float4 w3 = s_w3[j];
+                C0 = __builtin_fmaf(w2.z, aT, C0);
+                C1 = __builtin_fmaf(w2.w, aT, C1);
+                C2 = __builtin_fmaf(w3.x, aT, C2);
+                if constexpr (GEOM) {
+                    N0 = __builtin_fmaf(w3.y, aT, N0);
+                    N1 = __builtin_fmaf(w3.z, aT, N1);
+                    N2 = __builtin_fmaf(w3.w, aT, N2);
+                }
+            }
             if constexpr (GEOM) {
                 const float t = splat_tpeak(w1, w2, dx, dy);
-                N0 = __builtin_fmaf(w3.y, aT, N0);
-                N1 = __builtin_fmaf(w3.z, aT, N1);
-                N2 = __builtin_fmaf(w3.w, aT, N2);
                 m_init = T > 0.5f ? t : m_init;
                 const int g = i * kTilePixels + j;
                 if (g < kResident) {
@@ -248,7 +295,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     const uint32_t max_contrib = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
 
     float mDepth = 0.f, md_out = 0.f, md_dT = 0.f;
-    bool md_ok = false;
+    bool md_ok = false, md_in_range = false;
     if constexpr (GEOM) {
         unsigned long long st[4] = {0, 0, 0, 0};
         float Tp[kSplit + 1];
@@ -419,6 +466,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         w_max = fminf(fmaxf(w_max, 0.f), 1.f);  // __saturatef (NaN -> 0)
         const float w_min = 1.f - w_max;
         mDepth = in_range ? __builtin_fmaf(w_max, dmax, w_min * dmin) : 0.f;
+        md_in_range = in_range;
 
         // The backward's median-depth pre-pass (render_backward.cu:835-880),
         // done here while the blended set is still in LDS: dT/dt_m at the
@@ -427,9 +475,14 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         // recomputes it otherwise.  Contributors dropped after pass 2 are
         // > 6 sigma from every depth of the final window: each of their terms
         // is below 0.25 e^-18 6 rsigma < 3e-8 rsigma in magnitude.
-        const float nrm = pixel_ray_norm(pixx, pixy, a.W, a.H, a.focal_x, a.focal_y);
-        md_out = mDepth * (1.0f / nrm);
-        const float mDepth_b = md_out * nrm;
+        float mDepth_b;
+        if constexpr (SAMPLE) {
+            mDepth_b = mDepth;  // the sample backward reads the median depth itself (sample_backward.cu:135)
+        } else {
+            const float nrm = pixel_ray_norm(pixx, pixy, a.W, a.H, a.focal_x, a.focal_y);
+            md_out = mDepth * (1.0f / nrm);
+            mDepth_b = md_out * nrm;
+        }
         float dT_dtm = 0.f;
         if (resident && inside && mDepth_b != 0.f && last != 0) {
             const int nwords = (int)((last + 31) >> 5);
@@ -454,6 +507,25 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         md_ok = resident;
     }
 
+    if constexpr (SAMPLE) {
+        if (inside) {
+            // sample_forward.cu:647-657
+            const float pnx = (pixx - (float)(a.W - 1) / 2.f) / a.focal_x;
+            const float pny = (pixy - (float)(a.H - 1) / 2.f) / a.focal_y;
+            const float rln = 1.0f / sqrtf(pnx * pnx + pny * pny + 1.f);
+            const float depth = mDepth * rln;
+            a.out_points[3 * pid + 0] = pnx * depth;
+            a.out_points[3 * pid + 1] = pny * depth;
+            a.out_points[3 * pid + 2] = depth;
+            a.out_inside[pid] = (uint8_t)(md_in_range ? 1 : 0);
+            a.pt_last[pid] = last;
+            a.pt_mdepth[pid] = mDepth;
+            a.pt_dT[pid] = md_dT;
+            a.pt_cached[pid] = (uint8_t)(md_ok ? 1 : 0);
+        }
+        if (tid == 0) a.chunk_max[chunk] = max_contrib;
+        return;
+    }
     if (inside) {
         const int HW = a.H * a.W;
         const int pix = a.W * py + px;
@@ -484,7 +556,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
 hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const ImageState& is,
                              const TileState& ts, float* out_color, float* out_alpha, float* out_normal,
                              float* out_mdepth, hipStream_t stream) {
-    RenderFwdArgs a;
+    RenderFwdArgs a{};
     a.ranges = ts.ranges;
     a.point_list = bs.point_list;
     a.splats = gs.splats;
@@ -519,6 +591,39 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     } else {
         hipLaunchKernelGGL((render_fwd_kernel<false, false>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_sample_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const TileState& ts,
+                             const PointState& ps, const PointBinState& pb, const SampleTiles& st,
+                             const ChunkState& cs, uint32_t num_chunks, float* out_points, uint8_t* out_inside,
+                             hipStream_t stream) {
+    RenderFwdArgs a{};
+    a.ranges = ts.ranges;
+    a.point_list = bs.point_list;
+    a.splats = gs.splats;
+    a.W = p.W;
+    a.H = p.H;
+    a.grid_x = p.grid_x;
+    a.num_tiles = p.grid_x * p.grid_y;
+    a.focal_x = p.focal_x;
+    a.focal_y = p.focal_y;
+    a.passes = kSplitIterations;
+    a.num_chunks = num_chunks;
+    a.chunk_off = st.chunk_off;
+    a.pt_ranges = st.pt_ranges;
+    a.pt_list = pb.pt_list;
+    a.pt_xy = ps.xy;
+    a.out_points = out_points;
+    a.out_inside = out_inside;
+    a.pt_last = ps.last;
+    a.pt_mdepth = ps.mdepth;
+    a.pt_dT = ps.dT;
+    a.pt_cached = ps.cached;
+    a.chunk_max = cs.chunk_max;
+    if (num_chunks == 0) return hipSuccess;
+    hipLaunchKernelGGL((render_fwd_kernel<true, false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0, stream,
+                       a);
     return hipGetLastError();
 }
 

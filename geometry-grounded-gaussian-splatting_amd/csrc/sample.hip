@@ -1,0 +1,403 @@
+// sample.hip — sample_depth on gfx950: the median depth of the Gaussian
+// field at arbitrary 3D points (the multi-view geometric-consistency term of
+// the reference's training loss, utils/loss_utils.py:160), and its backward.
+//
+// Replaces, in CR/rasterizer_impl.cu:1042-1394 (Rasterizer::sampleDepth /
+// sampleDepthBackward): preprocessPointsCUDA (sample_forward.cu:9-53),
+// createWithKeys + SortPairs + identifyTileRanges on the points (:109-137,
+// 745-779), countPointBatches + InclusiveSum + setBlockId (:163-183,
+// 781-790), sampleDepthCUDA backward (sample_backward.cu:77-359) and
+// preprocessPointsCUDA backward (:42-75).  The forward raster itself is
+// render_fwd.hip in SAMPLE mode; the Gaussian side reuses preprocess_fwd,
+// the binning and preprocess_bwd.
+//
+// Points are grouped per tile (stable radix sort on the tile id, as the
+// reference) and cut into chunks of 256 points, one 256-lane workgroup each
+// (the reference uses 512-point blocks, 2 points per thread: a point's result
+// does not depend on the grouping, every point stops at its own last
+// contributor).  No host synchronisation besides the forward's one: the
+// chunk count is derived on the device (sample_setup_kernel) and read
+// together with K.
+#pragma clang fp contract(off)
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include "gsr_kernels.h"
+
+namespace gsr {
+
+using PointSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                   rocprim::default_config, 0>;
+
+// bits to hold 0..tiles (culled points carry key = tiles and sort last)
+static unsigned point_key_bits(uint32_t tiles) { return 32u - (unsigned)__builtin_clz(tiles | 1u); }
+
+size_t point_sort_temp_bytes(int PN, uint32_t tiles) {
+    size_t bytes = 0;
+    (void)rocprim::radix_sort_pairs<PointSortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                     rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr,
+                                                     (size_t)PN, 0u, point_key_bits(tiles));
+    return bytes;
+}
+
+// ndc2Pix in double, as the reference (auxiliary.h:38-40)
+__device__ inline float ndc2pix_d(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+// preprocessPointsCUDA (sample_forward.cu:9-53) + the point's tile
+// (createWithKeys, rasterizer_impl.cu:127-131) + per-tile counts.
+__global__ void __launch_bounds__(256)
+    sample_points_kernel(int PN, const float* __restrict__ pts, const float* __restrict__ V,
+                         const float* __restrict__ M, int W, int H, uint32_t gx, uint32_t gy,
+                         float2* __restrict__ xy_out, uint32_t* __restrict__ keys, uint32_t* __restrict__ counts) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= PN) return;
+    const uint32_t tiles = gx * gy;
+    keys[idx] = tiles;
+    const float x = pts[3 * idx], y = pts[3 * idx + 1], z = pts[3 * idx + 2];
+    const float vz = V[2] * x + V[6] * y + V[10] * z + V[14];
+    if (vz <= kNearPlane) return;  // in_frustum (auxiliary.h:133-153)
+    const float hx = M[0] * x + M[4] * y + M[8] * z + M[12];
+    const float hy = M[1] * x + M[5] * y + M[9] * z + M[13];
+    const float hw = M[3] * x + M[7] * y + M[11] * z + M[15];
+    const float p_w = 1.0f / (hw + 0.0000001f);
+    const float px = ndc2pix_d(hx * p_w, W), py = ndc2pix_d(hy * p_w, H);
+    if (px < 0 || px > W - 1 || py < 0 || py > H - 1) return;
+    xy_out[idx] = make_float2(px, py);
+    const uint32_t tx = (uint32_t)min((int)gx - 1, max(0, (int)((px + 0.5f) / kTile)));
+    const uint32_t ty = (uint32_t)min((int)gy - 1, max(0, (int)((py + 0.5f) / kTile)));
+    const uint32_t t = ty * gx + tx;
+    keys[idx] = t;
+    atomicAdd(&counts[t], 1u);
+}
+
+hipError_t launch_sample_points(const FwdParams& p, int PN, const float* points3D, const PointState& ps,
+                                const PointBinState& pb, const SampleTiles& st, hipStream_t stream) {
+    const uint32_t tiles = p.grid_x * p.grid_y;
+    hipError_t e = hipMemsetAsync(st.counts, 0, sizeof(uint32_t) * tiles, stream);
+    if (e != hipSuccess || PN == 0) return e;
+    hipLaunchKernelGGL(sample_points_kernel, dim3((PN + 255) / 256), dim3(256), 0, stream, PN, points3D, p.view,
+                       p.proj, p.W, p.H, p.grid_x, p.grid_y, ps.xy, pb.keys_unsorted, st.counts);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t bytes = pb.sort_tmp_bytes;
+    return rocprim::radix_sort_pairs<PointSortConfig>(pb.sort_tmp, bytes, pb.keys_unsorted, pb.keys,
+                                                      rocprim::counting_iterator<uint32_t>(0), pb.pt_list,
+                                                      (size_t)PN, 0u, point_key_bits(tiles), stream);
+}
+
+// Block-wide exclusive scan of three counters (1024 lanes = 16 waves).
+struct Scan3 {
+    uint32_t a, b, c;
+};
+__device__ inline Scan3 block_exclusive_scan3(Scan3 v, Scan3* s_wave, Scan3& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    Scan3 inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t ua = __shfl_up(inc.a, o, 64), ub = __shfl_up(inc.b, o, 64), uc = __shfl_up(inc.c, o, 64);
+        if (lane >= o) {
+            inc.a += ua;
+            inc.b += ub;
+            inc.c += uc;
+        }
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    Scan3 base{0, 0, 0};
+    total = Scan3{0, 0, 0};
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+        const Scan3 t = s_wave[w];
+        if (w < wave) {
+            base.a += t.a;
+            base.b += t.b;
+            base.c += t.c;
+        }
+        total.a += t.a;
+        total.b += t.b;
+        total.c += t.c;
+    }
+    __syncthreads();
+    return Scan3{base.a + inc.a - v.a, base.b + inc.b - v.b, base.c + inc.c - v.c};
+}
+
+// countPointBatches + InclusiveSum + the point ranges: per tile, its points
+// [first, end) in pt_list, its first 256-point chunk, and the totals
+// (valid points, the reference's 512-point block count, chunks).
+__global__ void __launch_bounds__(1024)
+    sample_setup_kernel(uint32_t tiles, const uint32_t* __restrict__ counts, uint2* __restrict__ pt_ranges,
+                        uint32_t* __restrict__ chunk_off, uint32_t* __restrict__ totals) {
+    __shared__ Scan3 s_wave[16];
+    Scan3 carry{0, 0, 0};
+    for (uint32_t base = 0; base < tiles; base += blockDim.x) {
+        const uint32_t t = base + threadIdx.x;
+        const uint32_t n = t < tiles ? counts[t] : 0u;
+        Scan3 tot;
+        const Scan3 ex = block_exclusive_scan3(Scan3{n, (n + kTilePixels - 1) / kTilePixels, (n + 511u) / 512u},
+                                               s_wave, tot);
+        if (t < tiles) {
+            const uint32_t first = carry.a + ex.a;
+            pt_ranges[t] = make_uint2(first, first + n);
+            chunk_off[t] = carry.b + ex.b;
+        }
+        carry.a += tot.a;
+        carry.b += tot.b;
+        carry.c += tot.c;
+    }
+    if (threadIdx.x == 0) {
+        chunk_off[tiles] = carry.b;
+        totals[0] = carry.a;
+        totals[1] = carry.c;
+        totals[2] = carry.b;
+        totals[3] = 0u;
+    }
+}
+
+hipError_t launch_sample_setup(int PN, uint32_t tiles, const PointBinState& pb, const SampleTiles& st,
+                               hipStream_t stream) {
+    (void)PN;
+    (void)pb;
+    hipLaunchKernelGGL(sample_setup_kernel, dim3(1), dim3(1024), 0, stream, tiles, st.counts, st.pt_ranges,
+                       st.chunk_off, st.totals);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ backward
+struct SampleBwdArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const Splat* splats;
+    const uint32_t* chunk_off;
+    const uint2* pt_ranges;
+    const uint32_t* pt_list;
+    const uint32_t* totals;
+    const uint32_t* chunk_max;
+    const float2* pt_xy;
+    const uint32_t* pt_last;
+    const float* pt_mdepth;
+    const float* pt_dT;
+    const uint8_t* pt_cached;
+    const float* points3D;
+    const uint8_t* inside;
+    const float* dL_doutput;
+    float* dL_dpoints3D;
+    const float* proj;
+    int W, H;
+    uint32_t num_tiles;
+    float focal_x, focal_y;
+    float* acc;  // [P][16] (gsr_common.h AccField): mean2D, conic, ray-plane
+};
+
+// sampleDepthCUDA backward (sample_backward.cu:77-359), one 256-lane
+// workgroup per chunk, one point per lane.  Per (wave, Gaussian) the 10
+// gradient terms are summed by the wave transpose reduction of render_bwd
+// (wave_transpose_reduce16) and added with one atomic instruction into the
+// Gaussian's accumulator record; the point's own gradient (through its
+// projected position) stays in registers, and the projection backward of
+// the point (preprocessPointsCUDA bwd, sample_backward.cu:42-75) is fused at
+// the end.  The grid is an upper bound on the chunk count (read on the
+// device); surplus workgroups exit at once.
+__global__ void __launch_bounds__(256) sample_bwd_kernel(SampleBwdArgs a) {
+    __shared__ float4 s_w0[kTilePixels], s_w1[kTilePixels], s_w2[kTilePixels];
+    __shared__ uint32_t s_id[kTilePixels];
+
+    const uint32_t chunk = xcd_remap(blockIdx.x, gridDim.x);
+    if (chunk >= a.totals[2]) return;  // uniform over the block
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t lo = 0, hi = a.num_tiles;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.chunk_off[mid] <= chunk) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t tile = lo;
+    const uint2 range = a.ranges[tile];
+    const int max_contrib = (int)a.chunk_max[chunk];
+    const uint2 pr = a.pt_ranges[tile];
+    const uint32_t slot = pr.x + (chunk - a.chunk_off[tile]) * kTilePixels + tid;
+    const bool in = slot < pr.y;
+    const uint32_t pid = in ? a.pt_list[slot] : 0u;
+
+    // per-point seed (sample_backward.cu:138-158)
+    float pixx = 0.f, pixy = 0.f, mDepth = 0.f, dL_dDepth = 0.f, dpx = 0.f, dpy = 0.f, dT = 0.f;
+    uint32_t last = 0;
+    bool on = false, cached = false;
+    if (in) {
+        const float2 xy = a.pt_xy[pid];
+        pixx = xy.x;
+        pixy = xy.y;
+        last = a.pt_last[pid];
+        mDepth = a.pt_mdepth[pid];
+        const bool in_r = a.inside[pid] != 0;
+        const float g0 = a.dL_doutput[3 * pid], g1 = a.dL_doutput[3 * pid + 1], g2 = a.dL_doutput[3 * pid + 2];
+        const float pnx = (pixx - (float)(a.W - 1) / 2.f) / a.focal_x;
+        const float pny = (pixy - (float)(a.H - 1) / 2.f) / a.focal_y;
+        const float rln = 1.0f / sqrtf(pnx * pnx + pny * pny + 1.f);
+        const float rln2 = 1.f / (pnx * pnx + pny * pny + 1.f);
+        const float depth = mDepth * rln;
+        const float dL_ddepth = g0 * pnx + g1 * pny + g2;
+        dL_dDepth = rln * dL_ddepth;
+        const float aux = dL_ddepth * rln2;
+        dpx = (g0 - aux * pnx) * depth / a.focal_x;
+        dpy = (g1 - aux * pny) * depth / a.focal_y;
+        on = last != 0 && in_r;
+        cached = a.pt_cached[pid] != 0;
+        dT = cached ? a.pt_dT[pid] : 0.f;
+    }
+    const int rounds = (max_contrib + kTilePixels - 1) / kTilePixels;
+    auto stage = [&](int i, bool ids) {
+        const int c = i * kTilePixels + tid;
+        if (c < max_contrib) {
+            const uint32_t g = a.point_list[range.x + c];
+            const Splat* sp = a.splats + g;
+            s_w0[tid] = sp->w0;
+            s_w1[tid] = sp->w1;
+            s_w2[tid] = sp->w2;
+            if (ids) s_id[tid] = g;
+        }
+    };
+
+    // pre-pass dT/dt_m (sample_backward.cu:170-215) unless the forward cached it
+    {
+        const bool need = on && !cached;
+        const uint32_t wave_last = wave_max_u(need ? last : 0u);
+        const bool block_needs = __syncthreads_or(wave_last != 0u);
+        uint32_t c = 0;
+        int toDo = max_contrib;
+        for (int i = 0; block_needs && i < rounds; i++, toDo -= kTilePixels) {
+            __syncthreads();
+            stage(i, false);
+            __syncthreads();
+            const int n = min(kTilePixels, toDo);
+            for (int j = 0; j < n && c < wave_last; j++) {
+                c++;
+                const float4 w0 = s_w0[j], w1 = s_w1[j];
+                const float dx = w0.x - pixx, dy = w0.y - pixy;
+                const float power = splat_power(w0, w1, dx, dy);
+                const float alpha = fminf(0.99f, w1.y * __expf(power));
+                if (!(need && c <= last && !(power > 0.f) && !(alpha < 1.0f / 255.0f))) continue;
+                const float4 w2 = s_w2[j];
+                const float t_peak = splat_tpeak(w1, w2, dx, dy);
+                const float t_delta = (mDepth - t_peak) * w2.y;
+                const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
+                dT += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
+            }
+        }
+    }
+    const float kappa = on ? dL_dDepth / fmaxf(-dT, 1e-7f) : 0.f;
+
+    // main pass, front to back (sample_backward.cu:228-354)
+    const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
+    uint32_t contributor = 0;
+    int toDo = max_contrib;
+    for (int i = 0; i < rounds; i++, toDo -= kTilePixels) {
+        __syncthreads();
+        stage(i, true);
+        __syncthreads();
+        const int n = min(kTilePixels, toDo);
+        for (int j = 0; j < n; j++) {
+            contributor++;
+            const float4 w0 = s_w0[j], w1 = s_w1[j];
+            const float dx = w0.x - pixx, dy = w0.y - pixy;
+            const float power = splat_power(w0, w1, dx, dy);
+            const float G = __expf(power);
+            const bool valid = on && contributor <= last && !(power > 0.f) && !(w1.y * G < 1.0f / 255.0f);
+            if (__ballot(valid) == 0ull) continue;  // wave-uniform skip (warp.any)
+            const float4 w2 = s_w2[j];
+            const float alpha = fminf(0.99f, w1.y * G);
+            const float t_peak = splat_tpeak(w1, w2, dx, dy);
+            const float rsig = w2.y;
+            const float t_delta = (mDepth - t_peak) * rsig;
+            const float G_exp = __expf(-0.5f * t_delta * t_delta);
+            const float Gt = alpha * G_exp;
+            float dL_dGt = kappa * 0.25f * fast_rcp(1.f - Gt);
+            dL_dGt = mDepth > t_peak ? dL_dGt : -dL_dGt;
+            dL_dGt = rsig > 0.f ? dL_dGt : 0.f;
+            const float dL_dopa = dL_dGt * G_exp - kappa * (t_delta > 0.f ? 0.5f * fast_rcp(1.f - alpha) : 0.f);
+            const float dL_ddelta = -dL_dGt * Gt * t_delta;
+            const float dL_drsig = dL_ddelta * (mDepth - t_peak);
+            const float dL_dt = -dL_ddelta * rsig;
+            const float dL_dG = w1.y * dL_dopa;
+            const float gdx = G * dx, gdy = G * dy;
+            const float dG_ddelx = -gdx * w0.z - gdy * w0.w;
+            const float dG_ddely = -gdy * w1.x - gdx * w0.w;
+            float dL_ddelx = dL_dG * dG_ddelx + dL_dt * w1.z;
+            float dL_ddely = dL_dG * dG_ddely + dL_dt * w1.w;
+            float f[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) f[q] = 0.f;
+            if (valid) {
+                dpx -= dL_ddelx;
+                dpy -= dL_ddely;
+                f[kAccMean2D + 0] = dL_ddelx * ddelx_dx;
+                f[kAccMean2D + 1] = dL_ddely * ddely_dy;
+                f[kAccConic + 0] = -0.5f * gdx * dx * dL_dG;
+                f[kAccConic + 1] = -0.5f * gdx * dy * dL_dG;
+                f[kAccConic + 2] = -0.5f * gdy * dy * dL_dG;
+                f[kAccConic + 3] = G * dL_dopa;
+                f[kAccPlane + 0] = dL_dt * dx;
+                f[kAccPlane + 1] = dL_dt * dy;
+                f[kAccPlane + 2] = dL_dt;
+                f[kAccPlane + 3] = dL_drsig;
+            }
+            const float red = wave_transpose_reduce16(f);
+            // lanes 4k hold field k; colour (0-2) and normal (9-11) are zero here
+            const int field = lane >> 2;
+            const bool field_lane = (lane & 3) == 0 && field >= kAccMean2D &&
+                                    (field < kAccNormal || field >= kAccPlane);
+            if (field_lane) atomicAdd(a.acc + (size_t)s_id[j] * kAccFields + field, red);
+        }
+    }
+    if (in) {
+        // dL/dpoints2D in NDC units, then the projection backward
+        // (preprocessPointsCUDA bwd, sample_backward.cu:42-75)
+        const float gx2 = dpx * ddelx_dx, gy2 = dpy * ddely_dy;
+        const float* Pm = a.proj;
+        const float mx = a.points3D[3 * pid], my = a.points3D[3 * pid + 1], mz = a.points3D[3 * pid + 2];
+        const float hw = Pm[3] * mx + Pm[7] * my + Pm[11] * mz + Pm[15];
+        const float m_w = 1.0f / (hw + 0.0000001f);
+        const float mul1 = (Pm[0] * mx + Pm[4] * my + Pm[8] * mz + Pm[12]) * m_w * m_w;
+        const float mul2 = (Pm[1] * mx + Pm[5] * my + Pm[9] * mz + Pm[13]) * m_w * m_w;
+        a.dL_dpoints3D[3 * pid + 0] = (Pm[0] * m_w - Pm[3] * mul1) * gx2 + (Pm[1] * m_w - Pm[3] * mul2) * gy2;
+        a.dL_dpoints3D[3 * pid + 1] = (Pm[4] * m_w - Pm[7] * mul1) * gx2 + (Pm[5] * m_w - Pm[7] * mul2) * gy2;
+        a.dL_dpoints3D[3 * pid + 2] = (Pm[8] * m_w - Pm[11] * mul1) * gx2 + (Pm[9] * m_w - Pm[11] * mul2) * gy2;
+    }
+}
+
+hipError_t launch_sample_bwd(const SampleBwdParams& b, const GeomState& gs, const BinningState& bs,
+                             const TileState& ts, const PointState& ps, const PointBinState& pb,
+                             const SampleTiles& st, const ChunkState& cs, const BwdState& ws, hipStream_t stream) {
+    const FwdParams& p = b.f;
+    const uint32_t tiles = p.grid_x * p.grid_y;
+    if (b.PN == 0 || p.P == 0) return hipSuccess;
+    SampleBwdArgs a;
+    a.ranges = ts.ranges;
+    a.point_list = bs.point_list;
+    a.splats = gs.splats;
+    a.chunk_off = st.chunk_off;
+    a.pt_ranges = st.pt_ranges;
+    a.pt_list = pb.pt_list;
+    a.totals = st.totals;
+    a.chunk_max = cs.chunk_max;
+    a.pt_xy = ps.xy;
+    a.pt_last = ps.last;
+    a.pt_mdepth = ps.mdepth;
+    a.pt_dT = ps.dT;
+    a.pt_cached = ps.cached;
+    a.points3D = b.points3D;
+    a.inside = b.inside;
+    a.dL_doutput = b.dL_doutput;
+    a.dL_dpoints3D = b.dL_dpoints3D;
+    a.proj = p.proj;
+    a.W = p.W;
+    a.H = p.H;
+    a.num_tiles = tiles;
+    a.focal_x = p.focal_x;
+    a.focal_y = p.focal_y;
+    a.acc = ws.acc;
+    // chunks <= ceil(points / 256) + tiles holding points
+    const uint32_t bound = (uint32_t)((b.PN + kTilePixels - 1) / kTilePixels) + min(tiles, (uint32_t)b.PN);
+    hipLaunchKernelGGL(sample_bwd_kernel, dim3(bound), dim3(kTilePixels), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -74,21 +74,21 @@ struct QGauss {  // one Gaussian in q order, as the row kernels need it
     TileRect R;
 };
 __device__ __forceinline__ QGauss load_q(int q, int q1, const uint32_t* order, const Splat* splats,
-                                         const int* radii, uint32_t gx, uint32_t gy) {
+                                         const int* radii, uint32_t gx, uint32_t gy, float pad) {
     QGauss G{};
     if (q >= q1) return G;
     G.g = order[q];
     const int r = radii[G.g];
     if (r <= 0) return G;
     const float4 w0 = splats[G.g].w0, w1 = splats[G.g].w1;
-    G.E = make_ellipse(w0, w1);
+    G.E = make_ellipse(w0, w1, pad);
     G.R = tile_rect(w0.x, w0.y, r, gx, gy);
     G.on = G.E.mode != 2 && G.R.x1 > G.R.x0 && G.R.y1 > G.R.y0;
     return G;
 }
 
 __global__ void __launch_bounds__(64)
-    rows_count_kernel(int P, int nseg, uint32_t gx, uint32_t gy, const uint32_t* __restrict__ order,
+    rows_count_kernel(int P, int nseg, uint32_t gx, uint32_t gy, float pad, const uint32_t* __restrict__ order,
                       const Splat* __restrict__ splats, const int* __restrict__ radii, uint32_t* __restrict__ M) {
     extern __shared__ unsigned long long s_dyn[];
     uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(64)
     __syncthreads();
     const int q0 = seg * kRowSeg, q1 = min(P, q0 + kRowSeg);
     for (int q = q0 + lane; q < q1; q += 64) {
-        const QGauss G = load_q(q, q1, order, splats, radii, gx, gy);
+        const QGauss G = load_q(q, q1, order, splats, radii, gx, gy, pad);
         if (!G.on) continue;
         uint32_t lo, hi;
         for (uint32_t y = G.R.y0; y < G.R.y1; y++)
@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(64)
 // entries does rank, write and advance.  The row-wide prologue of each chunk
 // carries the untouched running slots over and clears the next chunk's masks.
 __global__ void __launch_bounds__(64)
-    rows_emit_kernel(int P, int nseg, uint32_t gx, uint32_t gy, const uint32_t* __restrict__ order,
+    rows_emit_kernel(int P, int nseg, uint32_t gx, uint32_t gy, float pad, const uint32_t* __restrict__ order,
                      const Splat* __restrict__ splats, const int* __restrict__ radii, const uint32_t* __restrict__ O,
                      uint2* __restrict__ rows) {
     extern __shared__ unsigned long long s_dyn[];  // 2 x [gy] masks, then 2 x [gy] running slots
@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(64)
             run_next[y] = run[y];
             s_cov[(cur ^ 1u) * gy + y] = 0ull;
         }
-        const QGauss G = load_q(c0 + lane, q1, order, splats, radii, gx, gy);
+        const QGauss G = load_q(c0 + lane, q1, order, splats, radii, gx, gy, pad);
         uint32_t lo, hi;
         if (G.on)
             for (uint32_t y = G.R.y0; y < G.R.y1; y++)
@@ -322,14 +322,16 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     const ListLayout& L = bs.lists;
     hipError_t e;
     // rows pass
-    hipLaunchKernelGGL(rows_count_kernel, dim3(L.nseg_rows), dim3(64), 4 * gy, stream, p.P, L.nseg_rows, gx, gy, gs.order,
+    hipLaunchKernelGGL(rows_count_kernel, dim3(L.nseg_rows), dim3(64), 4 * gy, stream, p.P, L.nseg_rows, gx, gy,
+                       p.cull_pad, gs.order,
                        gs.splats, radii, bs.rows_count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     size_t bytes = L.tmp_bytes;
     e = rocprim::exclusive_scan(bs.list_tmp, bytes, bs.rows_count, bs.rows_off, 0u, (size_t)gy * L.nseg_rows,
                                 rocprim::plus<uint32_t>(), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, gx, gy, gs.order,
+    hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, gx, gy,
+                       p.cull_pad, gs.order,
                        gs.splats, radii, bs.rows_off, bs.rows);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // tiles pass

@@ -34,12 +34,17 @@ __device__ __forceinline__ TileRect tile_rect(float mx, float my, int r, uint32_
 // rectangle is <= tau", with tau raised by a margin (x1.001 + 0.01) far above
 // the rounding of the per-pixel power and exp.  Non-positive-definite conics
 // keep their whole rect; o < 1/255 keeps nothing.
+// pad widens every tile by that many pixels on each side: 0 for the
+// render path (pixel centres), 0.5 for sample_depth, whose points in tile tx
+// lie anywhere in [16 tx - 0.5, 16 tx + 15.5) (createWithKeys,
+// rasterizer_impl.cu:129-130).
 struct Ellipse {
-    float mx, my, a, b, c, det, tau, vmax, kst, ia;
+    float mx, my, a, b, c, det, tau, vmax, kst, ia, pad;
     int mode;  // 0 = interval test, 1 = whole rect, 2 = nothing
 };
-__device__ __forceinline__ Ellipse make_ellipse(const float4& w0, const float4& w1) {
+__device__ __forceinline__ Ellipse make_ellipse(const float4& w0, const float4& w1, float pad) {
     Ellipse E;
+    E.pad = pad;
     E.mx = w0.x;
     E.my = w0.y;
     E.a = w0.z;
@@ -64,18 +69,18 @@ __device__ __forceinline__ bool row_span(const Ellipse& E, const TileRect& R, ui
         *hi = R.x1 - 1;
         return R.x1 > R.x0;
     }
-    const float vlo = fmaxf(E.my - (float)(ty * kTile + kTile - 1), -E.vmax);
-    const float vhi = fminf(E.my - (float)(ty * kTile), E.vmax);
+    const float vlo = fmaxf(E.my - ((float)(ty * kTile + kTile - 1) + E.pad), -E.vmax);
+    const float vhi = fminf(E.my - ((float)(ty * kTile) - E.pad), E.vmax);
     if (vlo > vhi) return false;
     const float vu = fminf(fmaxf(-E.b * E.kst, vlo), vhi);  // maximiser of the upper branch
     const float vl = fminf(fmaxf(E.b * E.kst, vlo), vhi);   // minimiser of the lower branch
     const float ia = E.ia;
     const float umax = (-E.b * vu + sqrtf(fmaxf(E.a * E.tau - E.det * vu * vu, 0.f))) * ia;
     const float umin = (-E.b * vl - sqrtf(fmaxf(E.a * E.tau - E.det * vl * vl, 0.f))) * ia;
-    // pixel centres x in [mx - umax, mx - umin]; tile tx holds x in [16 tx, 16 tx + 15]
+    // pixel centres x in [mx - umax, mx - umin]; tile tx holds x in [16 tx - pad, 16 tx + 15 + pad]
     const float xlo = E.mx - umax, xhi = E.mx - umin;
-    const int t0 = (int)ceilf((xlo - (float)(kTile - 1)) * (1.f / kTile));
-    const int t1 = (int)floorf(xhi * (1.f / kTile));
+    const int t0 = (int)ceilf((xlo - ((float)(kTile - 1) + E.pad)) * (1.f / kTile));
+    const int t1 = (int)floorf((xhi + E.pad) * (1.f / kTile));
     const int l = max(t0, (int)R.x0), h = min(t1, (int)R.x1 - 1);
     if (l > h) return false;
     *lo = (uint32_t)l;

@@ -10,6 +10,11 @@ names, argument order, return tuples and error behaviour:
                                              dsg_axis, dsg_sharpness, dsg_color, dscales, drotations)
                                              (DGR/rasterize_points.cu:141-258)
   mark_visible(means3D, view, proj)      -> bool[P]  (DGR/rasterize_points.cu:260-277)
+  sample_rasterized_depth(17 args)       -> (num_rendered, num_points, num_duplicated_tiles, output, inside,
+                                             geomBuffer, binningBuffer, pointBuffer, pointBinningBuffer,
+                                             tileBuffer, duplicatedTileBuffer)  (DGR/rasterize_points.cu:459-553)
+  sample_rasterized_depth_backward(28)   -> (dopacity, dmeans3D, dcov3D, dscales, drotations, dpoints3D)
+                                             (DGR/rasterize_points.cu:555-633)
 
 The C ABI (include/gsr.h) takes raw device pointers and allocation callbacks;
 here torch provides the memory (caching allocator), the current HIP stream and
@@ -46,10 +51,17 @@ def _load():
     L.gsr_rasterize_backward.restype = i
     L.gsr_rasterize_backward.argtypes = ([_ALLOC, vp] + [i] * 6 + [vp, i, i] + [vp] * 10 + [f] + [vp] * 3
                                          + [f] * 3 + [vp] * 4 + [vp] * 4 + [vp] * 4 + [vp] * 11 + [i, i, vp])
+    L.gsr_sample_depth_forward.restype = i
+    L.gsr_sample_depth_forward.argtypes = ([_ALLOC, vp] * 6 + [i] * 4 + [vp] * 4 + [f] + [vp] * 5 + [f] * 3 + [i]
+                                           + [vp, vp, i, vp] + [ctypes.POINTER(i)] * 3)
+    L.gsr_sample_depth_backward.restype = i
+    L.gsr_sample_depth_backward.argtypes = ([_ALLOC, vp] + [i] * 7 + [vp] * 4 + [f] + [vp] * 5 + [f] * 3
+                                            + [vp] * 6 + [vp] * 2 + [vp] * 6 + [i, vp])
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     L.gsr_set_option.argtypes = [i, i]
     L.gsr_debug_binning.argtypes = [vp, vp, i, i, i, vp, vp, vp]
+    L.gsr_debug_sample_points.argtypes = [vp, i, vp, vp, vp]
     L.gsr_debug_render_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i]
     L.gsr_timing_enable.argtypes = [i]
     L.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i)]
@@ -66,7 +78,7 @@ def loaded_library_path() -> str:
     return LIB_PATH
 
 
-NUM_STAGES = 11
+NUM_STAGES = 14
 # debugging aid: keep the last backward's accumulator buffer (gsr_api.hip
 # carve_bwd layout: 256-B aligned base, float acc[P][16], then float acc_abs[P])
 KEEP_BWD_SCRATCH = False
@@ -100,6 +112,20 @@ def debug_binning(binningBuffer, tileBuffer, R: int, image_height: int, image_wi
                                      int(image_height), plist.ctypes.data_as(ctypes.c_void_p) if with_list else None,
                                      ranges.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream)))
     return plist, ranges
+
+
+def debug_sample_points(pointBuffer, PN: int):
+    """(median depth along the ray [PN] float32, last contributor [PN] uint32)
+    of a sample_rasterized_depth forward's point buffer (gsr_debug_sample_points)."""
+    import numpy as np
+
+    md = np.zeros(PN, np.float32)
+    last = np.zeros(PN, np.uint32)
+    stream = torch.cuda.current_stream(pointBuffer.device).cuda_stream
+    _check(_load().gsr_debug_sample_points(ctypes.c_void_p(pointBuffer.data_ptr()), int(PN),
+                                           md.ctypes.data_as(ctypes.c_void_p), last.ctypes.data_as(ctypes.c_void_p),
+                                           ctypes.c_void_p(stream)))
+    return md, last
 
 
 def set_option(opt: int, value: int) -> None:
@@ -269,3 +295,72 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         with torch.cuda.device(means3D.device):
             _check(L.gsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(means3D.device)))
     return present
+
+
+def sample_rasterized_depth(points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                            viewmatrix, projmatrix, tan_fovx, tan_fovy, kernel_size, image_height, image_width,
+                            campos, prefiltered, debug):
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    if points3D.ndimension() < 1 or points3D.size(-1) != 3:
+        raise RuntimeError("points3D must have shape (..., 3) with last dimension == 3")
+    L = _load()
+    PN = points3D.numel() // 3
+    P = means3D.size(0)
+    H, W = int(image_height), int(image_width)
+    dev = means3D.device
+    output = torch.zeros_like(points3D)
+    inside = torch.zeros(points3D.shape[:-1], dtype=torch.bool, device=points3D.device)
+    bufs = [_ByteBuffer(dev) for _ in range(6)]
+    K, RN, TN = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    if P != 0 and PN != 0:
+        a = {k: _dev_contig(v, k) for k, v in dict(
+            points3D=points3D, means3D=means3D, opacity=opacity, scales=scales, rotations=rotations,
+            cov3D_precomp=cov3D_precomp, viewmatrix=viewmatrix, projmatrix=projmatrix, campos=campos).items()}
+        with torch.cuda.device(dev):
+            rc = L.gsr_sample_depth_forward(
+                bufs[0].cb, None, bufs[1].cb, None, bufs[2].cb, None, bufs[3].cb, None, bufs[4].cb, None,
+                bufs[5].cb, None, PN, P, W, H, _ptr(a["points3D"]), _ptr(a["means3D"]), _ptr(a["opacity"]),
+                _ptr(a["scales"]), float(scale_modifier), _ptr(a["rotations"]), _ptr(a["cov3D_precomp"]),
+                _ptr(a["viewmatrix"]), _ptr(a["projmatrix"]), _ptr(a["campos"]), float(tan_fovx), float(tan_fovy),
+                float(kernel_size), int(bool(prefiltered)), _ptr(output), _ptr(inside), int(bool(debug)),
+                _stream(dev), ctypes.byref(K), ctypes.byref(RN), ctypes.byref(TN))
+        _check(rc)
+    return (K.value, RN.value, TN.value, output, inside, *[b.tensor for b in bufs])
+
+
+def sample_rasterized_depth_backward(points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                                     viewmatrix, projmatrix, inside, dL_doutput, tan_fovx, tan_fovy, kernel_size,
+                                     image_height, image_width, campos, geomBuffer, binningBuffer, pointBuffer,
+                                     pointBinningBuffer, tileBuffer, duplicatedTileBuffer, R, RN, TN, prefiltered,
+                                     debug):
+    L = _load()
+    PN = points3D.numel() // 3
+    P = means3D.size(0)
+    dev = means3D.device
+    fopt = dict(dtype=torch.float32, device=dev)
+    alloc = torch.zeros if (P == 0 or PN == 0) else torch.empty  # the kernels overwrite every element
+    outs = dict(dopacity=alloc(P, 1, **fopt), dmeans3D=alloc(P, 3, **fopt), dcov3D=alloc(P, 6, **fopt),
+                dscales=alloc(P, 3, **fopt), drotations=alloc(P, 4, **fopt), dpoints3D=torch.zeros_like(points3D))
+    if P != 0 and PN != 0:
+        a = {k: _dev_contig(v, k) for k, v in dict(
+            points3D=points3D, means3D=means3D, opacity=opacity, scales=scales, rotations=rotations,
+            cov3D_precomp=cov3D_precomp, viewmatrix=viewmatrix, projmatrix=projmatrix, campos=campos,
+            dL_doutput=dL_doutput).items()}
+        ins = inside.contiguous()
+        if not ins.is_cuda or ins.dtype != torch.bool:
+            raise RuntimeError("gsr: `inside` must be the forward's bool device tensor")
+        scratch = _ByteBuffer(dev)
+        with torch.cuda.device(dev):
+            rc = L.gsr_sample_depth_backward(
+                scratch.cb, None, PN, P, int(RN), int(R), int(TN), int(image_width), int(image_height),
+                _ptr(a["points3D"]), _ptr(a["means3D"]), _ptr(a["opacity"]), _ptr(a["scales"]), float(scale_modifier),
+                _ptr(a["rotations"]), _ptr(a["cov3D_precomp"]), _ptr(a["viewmatrix"]), _ptr(a["projmatrix"]),
+                _ptr(a["campos"]), float(tan_fovx), float(tan_fovy), float(kernel_size), _ptr(geomBuffer),
+                _ptr(binningBuffer), _ptr(pointBuffer), _ptr(pointBinningBuffer), _ptr(tileBuffer),
+                _ptr(duplicatedTileBuffer), _ptr(ins), _ptr(a["dL_doutput"]), _ptr(outs["dopacity"]),
+                _ptr(outs["dmeans3D"]), _ptr(outs["dcov3D"]), _ptr(outs["dscales"]), _ptr(outs["drotations"]),
+                _ptr(outs["dpoints3D"]), int(bool(debug)), _stream(dev))
+        _check(rc)
+    return (outs["dopacity"], outs["dmeans3D"], outs["dcov3D"], outs["dscales"], outs["drotations"],
+            outs["dpoints3D"])

@@ -10,8 +10,9 @@ GaussianRasterizer` (gaussian_renderer/__init__.py:14) works unchanged once
 this directory's parent is on sys.path.  The compute lives in libgsr.so
 (hand-written HIP for gfx950) behind `_C`.
 
-The point-query entry points of the reference (integrate, evaluate_sdf,
-sample_depth, DGR/__init__.py:338-655) are the next rows of the build
+  GaussianRasterizer.sample_depth + _SampleDepth (autograd.Function)  (:470-655)
+The other point-query entry points of the reference (integrate,
+evaluate_sdf, DGR/__init__.py:338-468) are later rows of the build
 (SURVEY.md §8(f)); they raise NotImplementedError here.
 """
 from __future__ import annotations
@@ -145,5 +146,71 @@ class GaussianRasterizer(nn.Module):
     def evaluate_sdf(self, *args, **kwargs):
         raise NotImplementedError("evaluate_sdf (DGR/__init__.py:382-440) is a next-round row (SURVEY.md §8(f))")
 
-    def sample_depth(self, *args, **kwargs):
-        raise NotImplementedError("sample_depth (DGR/__init__.py:442-483) is a next-round row (SURVEY.md §8(f))")
+    def sample_depth(self, points3D, means3D, opacities, scales=None, rotations=None, cov3D_precomp=None):
+        """Median depth of the Gaussians at world points seen from this camera
+        (DGR/__init__.py:470-483): returns (camera-space point at the median
+        depth along its ray [..., 3], inside [...] bool)."""
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or (
+                (scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        if scales is None:
+            scales = torch.Tensor([])
+        if rotations is None:
+            rotations = torch.Tensor([])
+        if cov3D_precomp is None:
+            cov3D_precomp = torch.Tensor([])
+        return _SampleDepth.apply(points3D, means3D, opacities, scales, rotations, cov3D_precomp, self.raster_settings)
+
+
+class _SampleDepth(torch.autograd.Function):
+    """DGR/__init__.py:486-655.  The forward passes kernel_size 0.0 and the
+    backward the settings' kernel_size, as the reference does (:500-518, 598)."""
+
+    @staticmethod
+    def forward(ctx, points3D, means3D, opacities, scales, rotations, cov3D_precomp, raster_settings):
+        s = raster_settings
+        args = (points3D, means3D, opacities, scales, rotations, s.scale_modifier, cov3D_precomp, s.viewmatrix,
+                s.projmatrix, s.tanfovx, s.tanfovy, 0.0, s.image_height, s.image_width, s.campos, s.prefiltered,
+                s.debug)
+        if s.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                out = _C.sample_rasterized_depth(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_fw.dump")
+                print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
+                raise ex
+        else:
+            out = _C.sample_rasterized_depth(*args)
+        (num_rendered, num_points, num_duplicated_tiles, camera_points, inside, geomBuffer, binningBuffer,
+         pointBuffer, pointBinningBuffer, tileBuffer, duplicatedTileBuffer) = out
+        ctx.raster_settings = raster_settings
+        ctx.num_rendered = num_rendered
+        ctx.num_points = num_points
+        ctx.num_duplicated_tiles = num_duplicated_tiles
+        ctx.save_for_backward(points3D, means3D, opacities, scales, rotations, cov3D_precomp, inside, geomBuffer,
+                              binningBuffer, pointBuffer, pointBinningBuffer, tileBuffer, duplicatedTileBuffer)
+        return camera_points, inside
+
+    @staticmethod
+    def backward(ctx, grad_camera_points, grad_inside):
+        s = ctx.raster_settings
+        (points3D, means3D, opacities, scales, rotations, cov3D_precomp, inside, geomBuffer, binningBuffer,
+         pointBuffer, pointBinningBuffer, tileBuffer, duplicatedTileBuffer) = ctx.saved_tensors
+        args = (points3D, means3D, opacities, scales, rotations, s.scale_modifier, cov3D_precomp, s.viewmatrix,
+                s.projmatrix, inside, grad_camera_points, s.tanfovx, s.tanfovy, s.kernel_size, s.image_height,
+                s.image_width, s.campos, geomBuffer, binningBuffer, pointBuffer, pointBinningBuffer, tileBuffer,
+                duplicatedTileBuffer, ctx.num_rendered, ctx.num_points, ctx.num_duplicated_tiles, s.prefiltered,
+                s.debug)
+        if s.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                grads = _C.sample_rasterized_depth_backward(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_bw.dump")
+                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
+                raise ex
+        else:
+            grads = _C.sample_rasterized_depth_backward(*args)
+        grad_opacities, grad_means3D, grad_cov3D_precomp, grad_scales, grad_rotations, grad_points3D = grads
+        return grad_points3D, grad_means3D, grad_opacities, grad_scales, grad_rotations, grad_cov3D_precomp, None

@@ -2,8 +2,8 @@
 gaussian_renderer/__init__.py:18-98 (argument meaning, settings construction,
 returned dict).  Differences: the screen-space dummy tensor is created on the
 Gaussians' device instead of a hard-coded "cuda", and `pipe` may be any object
-with a `debug` attribute.  integrate / evaluate_sdf / sample_depth (:101-278)
-are next-round rows.
+with a `debug` attribute.  sample_depth (:225-278) follows; integrate /
+evaluate_sdf (:101-222) are later rows.
 """
 from __future__ import annotations
 
@@ -47,3 +47,35 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, kernel_size, scal
         opacities=opacity, scales=scales, rotations=_get("get_rotation"), cov3D_precomp=None)
     return {"render": image, "mask": alpha, "median_depth": median_depth, "viewspace_points": screenspace_points,
             "visibility_filter": radii > 0, "radii": radii, "normal": normal}
+
+
+def sample_depth(points3D, viewpoint_camera, pc, pipe, kernel_size, scaling_modifier=1.0):
+    """Median depth of the Gaussians at world points seen from
+    `viewpoint_camera` (gaussian_renderer/__init__.py:225-278; called by the
+    multi-view loss, utils/loss_utils.py:160).  `pc` exposes get_xyz,
+    get_opacity_with_3D_filter, get_scaling_with_3D_filter, get_rotation
+    (and get_covariance when pipe.compute_cov3D_python)."""
+
+    def _get(name, *a):
+        v = getattr(pc, name)
+        return v(*a) if callable(v) else v
+
+    tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
+    tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
+    raster_settings = GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+        tanfovx=tanfovx, tanfovy=tanfovy, kernel_size=kernel_size, bg=0, scale_modifier=scaling_modifier,
+        viewmatrix=viewpoint_camera.world_view_transform, projmatrix=viewpoint_camera.full_proj_transform,
+        sh_degree=pc.active_sh_degree, sg_degree=pc.active_sg_degree, campos=viewpoint_camera.camera_center,
+        prefiltered=False, debug=getattr(pipe, "debug", False), require_depth=True)
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    scales = rotations = cov3D_precomp = None
+    if getattr(pipe, "compute_cov3D_python", False):
+        cov3D_precomp = _get("get_covariance", scaling_modifier)
+    else:
+        scales = _get("get_scaling_with_3D_filter")
+        rotations = _get("get_rotation")
+    depth, inside = rasterizer.sample_depth(points3D=points3D, means3D=_get("get_xyz"),
+                                            opacities=_get("get_opacity_with_3D_filter"), scales=scales,
+                                            rotations=rotations, cov3D_precomp=cov3D_precomp)
+    return {"sampled_depth": depth, "inside": inside}

@@ -100,6 +100,60 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
                      uint8_t* present, void* stream);
 
 /*
+ * sample_depth: the median depth of the Gaussian field
+ * at PN arbitrary world points seen from one camera — the multi-view
+ * geometric-consistency term of the reference's training loss
+ * (utils/loss_utils.py:160, gaussian_renderer/__init__.py:225-278).
+ *
+ * Replaces CudaRasterizer::Rasterizer::sampleDepth (rasterizer.h:170-195,
+ * rasterizer_impl.cu:1042-1245), bound as _C.sample_rasterized_depth
+ * (DGR/ext.cpp:21, rasterize_points.cu:459-553).  The six resize callbacks
+ * are the reference's geometry, binning, point, point-binning, tile and
+ * duplicated-tile buffers.  points3D [PN,3]; output [PN,3] is the
+ * camera-space point (x, y, z) at the median depth along its ray and
+ * inside [PN] (uint8) whether the median is defined; both are written for the
+ * points that project into the image and left untouched for the others (the
+ * reference zero-initialises them, so callers pass zeroed buffers).
+ * kernel_size is whatever the caller passes: the reference's Python wrapper
+ * passes 0.0 here (DGR/__init__.py:500-518) and the settings' value to the
+ * backward.  Synchronises `stream` once (K, valid points, block count).
+ * *num_points = points that project into the image, *num_duplicated_tiles =
+ * the reference's count of 512-point blocks (both opaque to callers; the
+ * backward ignores them).
+ */
+int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn point_alloc, void* point_ctx, gsr_alloc_fn point_binning_alloc,
+                             void* point_binning_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                             gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P, int width, int height,
+                             const float* points3D, const float* means3D, const float* opacities,
+                             const float* scales, float scale_modifier, const float* rotations,
+                             const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                             const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size,
+                             int prefiltered, float* output, uint8_t* inside, int debug, void* stream,
+                             int* num_rendered, int* num_points, int* num_duplicated_tiles);
+
+/*
+ * Replaces CudaRasterizer::Rasterizer::sampleDepthBackward (rasterizer.h:197-233,
+ * rasterizer_impl.cu:1247-1394), bound as _C.sample_rasterized_depth_backward
+ * (rasterize_points.cu:555-633).  The six buffers are the forward's; R, RN, TN
+ * its three counts.  Gradients written: dL_dopacity [P,1], dL_dmean3D [P,3],
+ * dL_dscale [P,3] + dL_drot [P,4] (scale/rotation path) or dL_dcov3D [P,6]
+ * (precomputed covariance), all fully overwritten; dL_dpoints3D [PN,3] is
+ * written for the points that project into the image only (callers pass a
+ * zeroed buffer, as the reference's torch::zeros_like).
+ */
+int gsr_sample_depth_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int PN, int P, int RN, int R, int TN,
+                              int width, int height, const float* points3D, const float* means3D,
+                              const float* opacities, const float* scales, float scale_modifier,
+                              const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                              const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                              float kernel_size, const void* geom_buffer, const void* binning_buffer,
+                              const void* point_buffer, const void* point_binning_buffer, const void* tile_buffer,
+                              const void* dup_tile_buffer, const uint8_t* inside, const float* dL_doutput,
+                              float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale,
+                              float* dL_drot, float* dL_dpoints3D, int debug, void* stream);
+
+/*
  * Per-stage GPU timing (no reference equivalent; SURVEY §5 "tracing").  While
  * enabled, every kernel stage of the calls above is bracketed by two hipEvents
  * on the call's stream.  gsr_timing_collect() waits for the recorded events,
@@ -119,6 +173,9 @@ enum gsr_stage {
     GSR_STAGE_PREPROCESS_BWD,
     GSR_STAGE_DEPTH_ORDER, /* stable depth sort of the Gaussians (binning.hip) */
     GSR_STAGE_TILE_LISTS,  /* per-tile lists without an instance sort (tilelists.hip; grids <= 1024^2 tiles) */
+    GSR_STAGE_SAMPLE_POINTS, /* sample_depth: point projection, per-tile point lists and chunks (sample.hip) */
+    GSR_STAGE_SAMPLE_FWD,    /* sample_depth forward raster (render_fwd.hip, SAMPLE mode) */
+    GSR_STAGE_SAMPLE_BWD,    /* sample_depth backward raster + point projection backward (sample.hip) */
     GSR_NUM_STAGES
 };
 int gsr_timing_enable(int on);
@@ -154,6 +211,14 @@ int gsr_debug_render_stats(unsigned long long* out8, int reset);
  */
 int gsr_debug_binning(const void* binning_buffer, const void* tile_buffer, int R, int width, int height,
                       uint32_t* point_list_out, uint32_t* ranges_out, void* stream);
+
+/*
+ * Introspection of a sample_depth forward's point buffer (test hook): the
+ * per-point median depth along the ray and last contributor (index into the
+ * culled per-tile list) for PN points; synchronises `stream`.
+ */
+int gsr_debug_sample_points(const void* point_buffer, int PN, float* median_depth_out, uint32_t* last_out,
+                            void* stream);
 
 /* Human-readable message for the last non-OK status on this thread. */
 const char* gsr_last_error(void);

@@ -75,6 +75,7 @@ def lib():
         L.gsro_sample_backward.argtypes = ([ctypes.c_void_p] + [_f] * 4 + [ctypes.c_float] + [_f] * 4
                                            + [ctypes.c_float] * 3 + [_u8, _f] + [_f] * 6)
         L.gsro_sample_free.argtypes = [ctypes.c_void_p]
+        L.gsro_sample_set_median_depth.argtypes = [ctypes.c_void_p, _f]
         L.gsro_sample_get_points.argtypes = [ctypes.c_void_p, _f, _u32, _u32, _f]
         L.gsro_sample_gaussians.restype = ctypes.c_void_p
         L.gsro_sample_gaussians.argtypes = [ctypes.c_void_p]
@@ -287,6 +288,12 @@ class SampleState:
         lib().gsro_sample_get_points(self.ptr, _p(out["points2D"]), _p(out["tile"], _u32),
                                      _p(out["n_contrib"], _u32), _p(out["median_depth"]))
         return out
+
+    def set_median_depth(self, md) -> None:
+        """Make the backward use these per-point median depths (e.g. the GPU forward's)."""
+        md = np.ascontiguousarray(np.asarray(md, np.float32).reshape(-1))
+        assert md.size == self.PN
+        lib().gsro_sample_set_median_depth(self.ptr, _p(md))
 
     def gaussians(self) -> State:
         """The Gaussian side as a borrowed State (binning, geometry accessors)."""

@@ -20,6 +20,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "boundary.json")))
+GOLD_SAMPLE = json.load(open(os.path.join(ROOT, "tests", "golden", "boundary_sample.json")))
 
 
 def _describe(a):
@@ -86,6 +87,66 @@ def test_wrapper_marshals_reference_tuples(monkeypatch):
         assert type(ei.value).__name__ + ": " + str(ei.value) == GOLD["errors"][name]
 
 
+def test_sample_depth_marshals_reference_tuples(monkeypatch):
+    """GaussianRasterizer.sample_depth / _SampleDepth: the reference's
+    _C.sample_rasterized_depth{,_backward} tuples (kernel_size 0.0 forward,
+    the settings' value backward), output kinds, gradient routing and errors
+    (tests/golden/boundary_sample.json, DGR/__init__.py:470-655)."""
+    import diff_gaussian_rasterization as dgr
+
+    calls = {}
+    P, H, W = 5, 8, 12
+    PTS = (4, 6, 3)
+
+    def fwd(*args):
+        calls["forward"] = [_describe(a) for a in args]
+        return (11, 7, 3, torch.full(PTS, 5.0), torch.ones(PTS[:-1], dtype=torch.bool),
+                *[torch.zeros(3, dtype=torch.uint8) for _ in range(6)])
+
+    def bwd(*args):
+        calls["backward"] = [_describe(a) for a in args]
+        calls["backward_counts"] = [args[23], args[24], args[25]]
+        shapes = [(P, 1), (P, 3), (P, 6), (P, 3), (P, 4), PTS]
+        return tuple(torch.full(s, float(i + 1)) for i, s in enumerate(shapes))
+
+    monkeypatch.setattr(dgr._C, "sample_rasterized_depth", fwd)
+    monkeypatch.setattr(dgr._C, "sample_rasterized_depth_backward", bwd)
+    settings = dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=0.5, tanfovy=0.4, kernel_size=GOLD_SAMPLE["settings_kernel_size"],
+        bg=torch.zeros(3), scale_modifier=1.0, viewmatrix=torch.eye(4), projmatrix=torch.eye(4), sh_degree=3,
+        sg_degree=1, campos=torch.zeros(3), prefiltered=False, require_depth=True, debug=False)
+    rz = dgr.GaussianRasterizer(settings)
+    sin = dict(points3D=torch.zeros(PTS), means3D=torch.zeros(P, 3), opacities=torch.zeros(P, 1),
+               scales=torch.zeros(P, 3), rotations=torch.zeros(P, 4))
+    for v in sin.values():
+        v.requires_grad_(True)
+    depth, inside = rz.sample_depth(**sin)
+    assert [_describe(depth), _describe(inside)] == GOLD_SAMPLE["forward_outputs"]
+    (depth * 2.0).sum().backward()
+    assert calls["forward"] == GOLD_SAMPLE["forward"]
+    assert calls["backward"] == GOLD_SAMPLE["backward"]
+    assert calls["backward_counts"] == GOLD_SAMPLE["backward_counts"]
+    routing = {k: (None if v.grad is None else float(v.grad.flatten()[0])) for k, v in sin.items()}
+    assert routing == GOLD_SAMPLE["grad_routing"]
+    for name, kw in [("no_cov", dict(scales=None)), ("both_cov", dict(cov3D_precomp=torch.zeros(P, 6)))]:
+        args = dict(sin)
+        args.update(kw)
+        with pytest.raises(Exception) as ei:
+            rz.sample_depth(**args)
+        assert type(ei.value).__name__ + ": " + str(ei.value) == GOLD_SAMPLE["errors"][name]
+
+
+def test_sample_depth_no_cpu_fallback():
+    from diff_gaussian_rasterization import _C
+
+    with pytest.raises(RuntimeError, match="HIP device tensor"):
+        _C.sample_rasterized_depth(torch.zeros(4, 3), torch.zeros(2, 3), torch.zeros(2, 1), torch.ones(2, 3),
+                                   torch.zeros(2, 4), 1.0, torch.Tensor([]), torch.eye(4), torch.eye(4), 0.5, 0.5,
+                                   0.0, 8, 8, torch.zeros(3), False, False)
+    with pytest.raises(RuntimeError, match="points3D must have shape"):
+        _C.sample_rasterized_depth(torch.zeros(4, 2), torch.zeros(2, 3), *([None] * 15))
+
+
 def test_library_exports_header_symbols():
     header = open(os.path.join(ROOT, "include", "gsr.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(gsr_\w+)\s*\(", header, re.M)))
@@ -96,7 +157,7 @@ def test_library_exports_header_symbols():
     for n in names:
         assert hasattr(lib, n), n
     lib.gsr_abi_version.restype = ctypes.c_int
-    assert lib.gsr_abi_version() == 4
+    assert lib.gsr_abi_version() == 5
     lib.gsr_stage_name.restype = ctypes.c_char_p
     assert lib.gsr_stage_name(5) == b"render_fwd"
 
