@@ -1,0 +1,77 @@
+"""sample_depth timing at full size (development / DESIGN numbers).
+
+1M Gaussians (the C3 scene), 1080p: the points are the C3 view's median-depth
+points (one per pixel, [H, W, 3]) re-observed by an orbit camera — the
+multi-view loss's call (utils/loss_utils.py:147-166).  Times
+GaussianRasterizer.sample_depth forward + autograd backward and prints the
+per-stage HIP-event times as one JSON line.
+"""
+import json, math, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd")]
+import torch
+import gsr_scene as S
+from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, _C
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+dev = torch.device("cuda")
+W, H, P = 1920, 1080, 1_000_000
+cam0 = S.make_camera(W, H).to(dev)
+raw = S.make_gaussians(P, aspect=H / W)
+inp = {k: v.to(dev).contiguous() for k, v in S.activated_inputs(raw).items()}
+tanx, tany = math.tan(cam0.FoVx / 2), math.tan(cam0.FoVy / 2)
+
+
+def settings(cam):
+    return GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=tanx, tanfovy=tany, kernel_size=0.0, bg=torch.zeros(3, device=dev),
+        scale_modifier=1.0, viewmatrix=cam.world_view_transform, projmatrix=cam.full_proj_transform, sh_degree=3,
+        sg_degree=0, campos=cam.camera_center, prefiltered=False, require_depth=True, debug=False)
+
+
+with torch.no_grad():
+    color, radii, md, alpha, normal = GaussianRasterizer(settings(cam0))(
+        means3D=inp["means3D"], means2D=torch.zeros(P, 3, device=dev), opacities=inp["opacities"], shs=inp["shs"],
+        sg_axis=inp["sg_axis"], sg_sharpness=inp["sg_sharpness"], sg_color=inp["sg_color"], scales=inp["scales"],
+        rotations=inp["rotations"])
+fx, fy = W / (2 * tanx), H / (2 * tany)
+ys, xs = torch.meshgrid(torch.arange(H, device=dev, dtype=torch.float32),
+                        torch.arange(W, device=dev, dtype=torch.float32), indexing="ij")
+d = md[0]
+pts = torch.stack([(xs - (W - 1) / 2) / fx * d, (ys - (H - 1) / 2) / fy * d, d], -1).contiguous()
+cam1 = S.orbit_cameras(8, W, H)[1].to(dev)
+rz = GaussianRasterizer(settings(cam1))
+params = {k: inp[k].clone().requires_grad_(True) for k in ("means3D", "opacities", "scales", "rotations")}
+pts.requires_grad_(True)
+g = torch.randn_like(pts) * 1e-2
+
+
+def step():
+    for t in list(params.values()) + [pts]:
+        t.grad = None
+    depth, inside = rz.sample_depth(points3D=pts, means3D=params["means3D"], opacities=params["opacities"],
+                                    scales=params["scales"], rotations=params["rotations"])
+    torch.autograd.backward([depth], [g])
+    return inside
+
+
+for _ in range(3):
+    inside = step()
+torch.cuda.synchronize()
+_C.timing_collect()
+_C.timing_enable(True)
+t0 = time.perf_counter()
+for _ in range(steps):
+    step()
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / steps
+_C.timing_enable(False)
+st = _C.timing_collect()
+out = _C.sample_rasterized_depth(pts.detach(), params["means3D"].detach(), params["opacities"].detach(),
+                                 params["scales"].detach(), params["rotations"].detach(), 1.0, torch.Tensor([]),
+                                 cam1.world_view_transform, cam1.full_proj_transform, tanx, tany, 0.0, H, W,
+                                 cam1.camera_center, False, False)
+print(json.dumps({"what": "sample_depth fwd+bwd (autograd), 1M Gaussians, 1920x1080 points from a second view",
+                  "ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1 / dt, 2), "num_rendered": out[0],
+                  "num_points": out[1], "inside": int(out[4].sum()),
+                  "stage_ms": {k: round(v / n, 4) for k, (v, n) in st.items() if n}}))
