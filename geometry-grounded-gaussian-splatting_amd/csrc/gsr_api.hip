@@ -707,6 +707,37 @@ int gsr_sample_depth_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
     return GSR_OK;
 }
 
+int gsr_adam_step(int n_groups, const gsr_adam_group* groups, double step, double beta1, double beta2, double eps,
+                  void* stream_ptr) {
+    if (n_groups < 0 || n_groups > kMaxAdamGroups || (n_groups > 0 && !groups) || !(step >= 1.0))
+        return fail(GSR_ERR_ARGS, "adam: 0..16 groups and step >= 1");
+    AdamGroup g[kMaxAdamGroups];
+    double lr[kMaxAdamGroups];
+    for (int k = 0; k < n_groups; k++) {
+        const gsr_adam_group& s = groups[k];
+        if (s.n < 0 || (s.n > 0 && (!s.param || !s.grad || !s.exp_avg || !s.exp_avg_sq)))
+            return fail(GSR_ERR_ARGS, "adam: missing group buffer");
+        g[k].param = s.param;
+        g[k].grad = s.grad;
+        g[k].exp_avg = s.exp_avg;
+        g[k].exp_avg_sq = s.exp_avg_sq;
+        g[k].n = s.n;
+        const uintptr_t bits = (uintptr_t)s.param | (uintptr_t)s.grad | (uintptr_t)s.exp_avg | (uintptr_t)s.exp_avg_sq;
+        g[k].aligned = (bits & 15u) == 0;
+        lr[k] = s.lr;
+    }
+    hipError_t e = launch_adam(n_groups, g, lr, step, beta1, beta2, eps, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "adam", e);
+}
+
+int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_radii2D, float* accum,
+                      float* accum_abs, float* denom, void* stream_ptr) {
+    if (P < 0 || (P > 0 && (!vgrad || !radii || !max_radii2D || !accum || !accum_abs || !denom)))
+        return fail(GSR_ERR_ARGS, "densify stats: invalid arguments");
+    hipError_t e = launch_densify_stats(P, vgrad, radii, max_radii2D, accum, accum_abs, denom, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "densify stats", e);
+}
+
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream_ptr) {
     (void)projmatrix;

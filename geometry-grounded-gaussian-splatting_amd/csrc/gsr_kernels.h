@@ -119,6 +119,21 @@ hipError_t launch_sample_bwd(const SampleBwdParams& b, const GeomState& gs, cons
                              const TileState& ts, const PointState& ps, const PointBinState& pb,
                              const SampleTiles& st, const ChunkState& cs, const BwdState& ws, hipStream_t stream);
 
+// optim.hip: multi-tensor Adam step and densification statistics
+constexpr int kMaxAdamGroups = 16;
+struct AdamGroup {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    long long n;
+    int aligned;  // all four pointers 16-B aligned: float4 path
+};
+hipError_t launch_adam(int n_groups, const AdamGroup* groups, const double* lr, double step, double beta1,
+                       double beta2, double eps, hipStream_t stream);
+hipError_t launch_densify_stats(int P, const float* vgrad, const int* radii, float* max_radii2D, float* accum,
+                                float* accum_abs, float* denom, hipStream_t stream);
+
 // mark visible
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t stream);

@@ -1,0 +1,127 @@
+// optim.hip — the per-iteration parameter update of training on gfx950
+// (SURVEY §8(f) rank 2): a multi-tensor Adam step over all Gaussian
+// parameter groups in one launch, and the densification statistics.
+//
+// Replaces, for the Gaussian parameters:
+//   torch.optim.Adam(..., eps=1e-15).step()   (scene/gaussian_model.py:347-351,
+//                                              train.py:259-261)
+//     exp_avg    = lerp(exp_avg, g, 1 - beta1)
+//     exp_avg_sq = beta2 exp_avg_sq + (1 - beta2) g^2
+//     p         -= lr / (1 - beta1^t) * exp_avg / (sqrt(exp_avg_sq) / sqrt(1 - beta2^t) + eps)
+//   (torch/optim/adam.py _single_tensor_adam, the published Adam of
+//   Kingma & Ba with torch's rounding order);
+//   GaussianModel.add_densification_stats + the max_radii2D update
+//     (scene/gaussian_model.py:818-821, train.py:236-237).
+// Both are pure HBM streams (28 B per parameter element, 24 B + 3 x 4 B per
+// Gaussian for the statistics): float4 loads/stores, grid-stride over all
+// groups, no LDS.
+#include "gsr_kernels.h"
+
+namespace gsr {
+
+struct AdamArgs {
+    int n_groups;
+    float beta1, beta2, one_m_beta1, one_m_beta2;
+    AdamGroup g[kMaxAdamGroups];
+    float step_size[kMaxAdamGroups];   // lr / (1 - beta1^t)
+    float bc2_sqrt[kMaxAdamGroups];    // sqrt(1 - beta2^t)
+    unsigned long long vec_begin[kMaxAdamGroups + 1];  // prefix of float4 counts
+};
+
+__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float b2, float omb1, float omb2,
+                                          float step_size, float bc2s, float eps) {
+    // torch: exp_avg.lerp_(grad, 1 - beta1); exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
+    m = m + omb1 * (g - m);           // lerp, weight < 0.5 branch (ATen Lerp.h)
+    v = v * b2 + (omb2 * g) * g;      // addcmul: self + value * t1 * t2, left to right
+    const float denom = sqrtf(v) / bc2s + eps;
+    p = p - step_size * (m / denom);
+    return p;
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(AdamArgs a, float eps) {
+    const unsigned long long total = a.vec_begin[a.n_groups];
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    int gi = 0;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        while (i >= a.vec_begin[gi + 1]) gi++;  // groups are visited in increasing order per thread
+        const AdamGroup& G = a.g[gi];
+        const unsigned long long e0 = (i - a.vec_begin[gi]) * 4ull;
+        const float ss = a.step_size[gi], bc = a.bc2_sqrt[gi];
+        if (e0 + 4 <= (unsigned long long)G.n && G.aligned) {
+            float4 p = reinterpret_cast<float4*>(G.param)[e0 / 4];
+            const float4 g = reinterpret_cast<const float4*>(G.grad)[e0 / 4];
+            float4 m = reinterpret_cast<float4*>(G.exp_avg)[e0 / 4];
+            float4 v = reinterpret_cast<float4*>(G.exp_avg_sq)[e0 / 4];
+            adam_one(p.x, g.x, m.x, v.x, a.beta2, a.one_m_beta1, a.one_m_beta2, ss, bc, eps);
+            adam_one(p.y, g.y, m.y, v.y, a.beta2, a.one_m_beta1, a.one_m_beta2, ss, bc, eps);
+            adam_one(p.z, g.z, m.z, v.z, a.beta2, a.one_m_beta1, a.one_m_beta2, ss, bc, eps);
+            adam_one(p.w, g.w, m.w, v.w, a.beta2, a.one_m_beta1, a.one_m_beta2, ss, bc, eps);
+            reinterpret_cast<float4*>(G.param)[e0 / 4] = p;
+            reinterpret_cast<float4*>(G.exp_avg)[e0 / 4] = m;
+            reinterpret_cast<float4*>(G.exp_avg_sq)[e0 / 4] = v;
+        } else {
+            for (unsigned long long e = e0; e < e0 + 4 && e < (unsigned long long)G.n; e++)
+                adam_one(G.param[e], G.grad[e], G.exp_avg[e], G.exp_avg_sq[e], a.beta2, a.one_m_beta1,
+                         a.one_m_beta2, ss, bc, eps);
+        }
+    }
+}
+
+hipError_t launch_adam(int n_groups, const AdamGroup* groups, const double* lr, double step, double beta1,
+                       double beta2, double eps, hipStream_t stream) {
+    if (n_groups <= 0) return hipSuccess;
+    AdamArgs a;
+    a.n_groups = n_groups;
+    // as torch: Python-float (double) scalars, rounded to fp32 where they meet the tensors
+    a.beta1 = (float)beta1;
+    a.beta2 = (float)beta2;
+    a.one_m_beta1 = (float)(1.0 - beta1);
+    a.one_m_beta2 = (float)(1.0 - beta2);
+    a.vec_begin[0] = 0;
+    // bias corrections as torch computes them for a CPU float step (python floats, double)
+    const double bc1 = 1.0 - pow(beta1, step);
+    const double bc2 = 1.0 - pow(beta2, step);
+    for (int k = 0; k < n_groups; k++) {
+        a.g[k] = groups[k];
+        a.step_size[k] = (float)(lr[k] / bc1);
+        a.bc2_sqrt[k] = (float)sqrt(bc2);
+        a.vec_begin[k + 1] = a.vec_begin[k] + (unsigned long long)((groups[k].n + 3) / 4);
+    }
+    const unsigned long long total = a.vec_begin[n_groups];
+    if (total == 0) return hipSuccess;
+    const unsigned long long blocks = (total + 255) / 256;
+    const unsigned grid = (unsigned)(blocks < 256ull * 32ull ? blocks : 256ull * 32ull);  // 32 blocks per CU
+    hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, stream, a, (float)eps);
+    return hipGetLastError();
+}
+
+// add_densification_stats + max_radii2D (scene/gaussian_model.py:818-821,
+// train.py:236-237), for the Gaussians with radii > 0:
+//   max_radii2D = max(max_radii2D, radii)
+//   xyz_gradient_accum     += |grad[:2]|    (norm of the screen-space x, y gradient)
+//   xyz_gradient_accum_abs += |grad[2:]|    (the |.|-sum channel, render_backward.cu:1028)
+//   denom += 1
+__global__ void __launch_bounds__(256)
+    densify_stats_kernel(int P, const float* __restrict__ vgrad, const int* __restrict__ radii,
+                         float* __restrict__ max_radii2D, float* __restrict__ accum, float* __restrict__ accum_abs,
+                         float* __restrict__ denom) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int r = radii[i];
+    if (!(r > 0)) return;
+    const float gx = vgrad[3 * i], gy = vgrad[3 * i + 1], gz = vgrad[3 * i + 2];
+    max_radii2D[i] = fmaxf(max_radii2D[i], (float)r);
+    accum[i] += sqrtf(gx * gx + gy * gy);
+    accum_abs[i] += fabsf(gz);
+    denom[i] += 1.f;
+}
+
+hipError_t launch_densify_stats(int P, const float* vgrad, const int* radii, float* max_radii2D, float* accum,
+                                float* accum_abs, float* denom, hipStream_t stream) {
+    if (P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(densify_stats_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, P, vgrad, radii,
+                       max_radii2D, accum, accum_abs, denom);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -36,6 +36,13 @@ _ALLOC = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 _lib = None
 
 
+class AdamGroup(ctypes.Structure):
+    """gsr_adam_group (include/gsr.h)."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_longlong), ("lr", ctypes.c_double)]
+
+
+
 def _load():
     global _lib
     if _lib is not None:
@@ -57,6 +64,11 @@ def _load():
     L.gsr_sample_depth_backward.restype = i
     L.gsr_sample_depth_backward.argtypes = ([_ALLOC, vp] + [i] * 7 + [vp] * 4 + [f] + [vp] * 5 + [f] * 3
                                             + [vp] * 6 + [vp] * 2 + [vp] * 6 + [i, vp])
+    L.gsr_adam_step.restype = i
+    L.gsr_adam_step.argtypes = [i, ctypes.POINTER(AdamGroup), ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                ctypes.c_double, vp]
+    L.gsr_densify_stats.restype = i
+    L.gsr_densify_stats.argtypes = [i] + [vp] * 7
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     L.gsr_set_option.argtypes = [i, i]
@@ -364,3 +376,45 @@ def sample_rasterized_depth_backward(points3D, means3D, opacity, scales, rotatio
         _check(rc)
     return (outs["dopacity"], outs["dmeans3D"], outs["dcov3D"], outs["dscales"], outs["drotations"],
             outs["dpoints3D"])
+
+
+MAX_ADAM_GROUPS = 16
+
+
+def adam_step(tensors, lrs, step: float, beta1: float, beta2: float, eps: float) -> None:
+    """One Adam update (gsr_adam_step) of up to 16 (param, grad, exp_avg,
+    exp_avg_sq) fp32 device tensors, contiguous, each with its learning rate,
+    all at step count `step` (after increment)."""
+    L = _load()
+    if not tensors:
+        return
+    arr = (AdamGroup * len(tensors))()
+    dev = None
+    for k, ((p, g, m, v), lr) in enumerate(zip(tensors, lrs)):
+        for t, name in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+            if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != p.numel():
+                raise RuntimeError(f"gsr adam: `{name}` must be a contiguous fp32 HIP tensor shaped like its param")
+        dev = p.device
+        arr[k] = AdamGroup(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr))
+    with torch.cuda.device(dev):
+        _check(L.gsr_adam_step(len(tensors), arr, float(step), float(beta1), float(beta2), float(eps), _stream(dev)))
+
+
+def densify_stats(viewspace_grad, radii, max_radii2D, accum, accum_abs, denom) -> None:
+    """add_densification_stats + max_radii2D (gsr_densify_stats), in place."""
+    L = _load()
+    P = radii.numel()
+    for t, name in ((viewspace_grad, "viewspace_grad"), (max_radii2D, "max_radii2D"), (accum, "accum"),
+                    (accum_abs, "accum_abs"), (denom, "denom")):
+        if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError(f"gsr densify_stats: `{name}` must be a contiguous fp32 HIP tensor")
+    if radii.dtype != torch.int32 or not radii.is_cuda:
+        raise RuntimeError("gsr densify_stats: `radii` must be an int32 HIP tensor")
+    if viewspace_grad.numel() != 3 * P or max_radii2D.numel() != P or accum.numel() != P or accum_abs.numel() != P \
+            or denom.numel() != P:
+        raise RuntimeError("gsr densify_stats: shape mismatch")
+    dev = radii.device
+    r = radii.contiguous()
+    with torch.cuda.device(dev):
+        _check(L.gsr_densify_stats(P, _ptr(viewspace_grad), _ptr(r), _ptr(max_radii2D), _ptr(accum), _ptr(accum_abs),
+                                   _ptr(denom), _stream(dev)))

@@ -154,6 +154,38 @@ int gsr_sample_depth_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
                               float* dL_drot, float* dL_dpoints3D, int debug, void* stream);
 
 /*
+ * Training update.  One Adam step over up to 16
+ * parameter groups in a single launch — torch.optim.Adam's update with its
+ * rounding order (scene/gaussian_model.py:347-351 builds it with eps 1e-15;
+ * train.py:259-261 steps it), every group at the same step count `step`
+ * (>= 1, the value after increment) with its own learning rate.  Groups are
+ * flat fp32 arrays of n elements; param, exp_avg and exp_avg_sq are updated
+ * in place.
+ */
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    long long n;
+    double lr;
+} gsr_adam_group;
+/* lr, betas and eps are doubles, like the Python floats torch combines them
+ * in before rounding to fp32 (e.g. 1 - beta2). */
+int gsr_adam_step(int n_groups, const gsr_adam_group* groups, double step, double beta1, double beta2, double eps,
+                  void* stream);
+
+/*
+ * GaussianModel.add_densification_stats + the max_radii2D update
+ * (scene/gaussian_model.py:818-821, train.py:236-237) for the P Gaussians
+ * with radii > 0: max_radii2D = max(max_radii2D, radii), accum += |vgrad.xy|,
+ * accum_abs += |vgrad.z|, denom += 1.  vgrad [P,3] is the viewspace-points
+ * gradient (dL/dmeans2D of the backward); the four statistics are [P] fp32.
+ */
+int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_radii2D, float* accum,
+                      float* accum_abs, float* denom, void* stream);
+
+/*
  * Per-stage GPU timing (no reference equivalent; SURVEY §5 "tracing").  While
  * enabled, every kernel stage of the calls above is bracketed by two hipEvents
  * on the call's stream.  gsr_timing_collect() waits for the recorded events,
