@@ -738,6 +738,22 @@ int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_ra
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "densify stats", e);
 }
 
+int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const int* uvs, const float* R,
+                       const float* T, const float* image_r, const float* image_n, float fx_r, float fy_r,
+                       float cx_r, float cy_r, float fx_n, float fy_n, float cx_n, float cy_n, int image_height_r,
+                       int image_width_r, int image_height_n, int image_width_n, float* ncc, float* grad_depths,
+                       float* grad_normals, uint8_t* valid, void* stream_ptr) {
+    if (P < 0 || image_height_r <= 0 || image_width_r <= 0 || image_height_n <= 0 || image_width_n <= 0)
+        return fail(GSR_ERR_ARGS, "warp_patch_ncc: invalid sizes");
+    if (P > 0 && (!depths || !normals || !uvs || !R || !T || !image_r || !image_n || !ncc || !grad_depths ||
+                  !grad_normals || !valid))
+        return fail(GSR_ERR_ARGS, "warp_patch_ncc: missing buffer");
+    NccParams q{P, depths, normals, uvs, R, T, image_r, image_n, fx_r, fy_r, cx_r, cy_r, fx_n, fy_n, cx_n, cy_n,
+                image_height_r, image_width_r, image_height_n, image_width_n, ncc, grad_depths, grad_normals, valid};
+    hipError_t e = launch_ncc(q, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "warp_patch_ncc", e);
+}
+
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream_ptr) {
     (void)projmatrix;

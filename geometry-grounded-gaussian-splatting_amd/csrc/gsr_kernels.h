@@ -134,6 +134,25 @@ hipError_t launch_adam(int n_groups, const AdamGroup* groups, const double* lr, 
 hipError_t launch_densify_stats(int P, const float* vgrad, const int* radii, float* max_radii2D, float* accum,
                                 float* accum_abs, float* denom, hipStream_t stream);
 
+// ncc.hip: warp-patch NCC with forward-mode gradients
+struct NccParams {
+    int P;
+    const float* depths;
+    const float* normals;
+    const int* uvs;
+    const float* R;
+    const float* T;
+    const float* image_r;
+    const float* image_n;
+    float fx_r, fy_r, cx_r, cy_r, fx_n, fy_n, cx_n, cy_n;
+    int Hr, Wr, Hn, Wn;
+    float* ncc;
+    float* grad_depths;
+    float* grad_normals;
+    uint8_t* valid;
+};
+hipError_t launch_ncc(const NccParams& q, hipStream_t stream);
+
 // mark visible
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t stream);

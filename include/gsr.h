@@ -186,6 +186,23 @@ int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_ra
                       float* accum_abs, float* denom, void* stream);
 
 /*
+ * Multi-view photometric term: replaces WarpPatchNCC /
+ * forward_mode_differentiation (submodules/warp-patch-ncc/warp_patch_ncc.cu:5-52,
+ * cuda_warp_patch_ncc/warp_patch_ncc_impl.cu:18-302), bound as
+ * warp_patch_ncc._C.warp_patch_ncc.  For P reference pixels uvs [P,2] (int32)
+ * with depths [P], normals [P,3]: the NCC of the 7x7 half-step patch against
+ * its homography warp into image_n, and d(NCC)/d(depth) [P],
+ * d(NCC)/d(normal) [P,3]; valid [P] (uint8).  R [9] is the r-to-n rotation
+ * as the reference's column-major float33, T [3]; images are [H,W] fp32
+ * (grey).  Every output element is written.
+ */
+int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const int* uvs, const float* R,
+                       const float* T, const float* image_r, const float* image_n, float fx_r, float fy_r,
+                       float cx_r, float cy_r, float fx_n, float fy_n, float cx_n, float cy_n, int image_height_r,
+                       int image_width_r, int image_height_n, int image_width_n, float* ncc, float* grad_depths,
+                       float* grad_normals, uint8_t* valid, void* stream);
+
+/*
  * Per-stage GPU timing (no reference equivalent; SURVEY §5 "tracing").  While
  * enabled, every kernel stage of the calls above is bracketed by two hipEvents
  * on the call's stream.  gsr_timing_collect() waits for the recorded events,

@@ -77,6 +77,8 @@ def lib():
         L.gsro_sample_free.argtypes = [ctypes.c_void_p]
         L.gsro_sample_set_median_depth.argtypes = [ctypes.c_void_p, _f]
         L.gsro_sample_get_points.argtypes = [ctypes.c_void_p, _f, _u32, _u32, _f]
+        L.gsro_warp_patch_ncc.argtypes = ([ctypes.c_int, _f, _f, _i, _f, _f, _f, _f] + [ctypes.c_float] * 8
+                                          + [ctypes.c_int] * 4 + [_f, _f, _f, _u8])
         L.gsro_sample_gaussians.restype = ctypes.c_void_p
         L.gsro_sample_gaussians.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -355,4 +357,26 @@ def sample_backward(state: SampleState, points3D, means3D, opacity, scales, rota
                                 _p(out["dscales"]), _p(out["drotations"]), _p(out["dpoints3D"]))
     if rc != 0:
         raise RuntimeError(f"oracle sample backward failed: {rc}")
+    return out
+
+
+def warp_patch_ncc(depths, normals, uvs, R, T, image_r, image_n, fx_r, fy_r, cx_r, cy_r, fx_n, fy_n, cx_n, cy_n):
+    """Same meaning as the reference's _C.warp_patch_ncc (submodules/warp-patch-ncc/warp_patch_ncc.cu:5-52):
+    returns dict(ncc [P], grad_depths [P], grad_normals [P,3], valid [P] bool)."""
+    d = _np(depths)
+    P = 0 if d is None else d.size
+    out = dict(ncc=np.zeros(P, np.float32), grad_depths=np.zeros(P, np.float32),
+               grad_normals=np.zeros((P, 3), np.float32), valid=np.zeros(P, np.uint8))
+    if P == 0:
+        out["valid"] = out["valid"].astype(bool)
+        return out
+    ir, inn = _np(image_r), _np(image_n)
+    Hr, Wr = np.asarray(image_r.shape if hasattr(image_r, "shape") else ir.shape)[-2:]
+    Hn, Wn = np.asarray(image_n.shape if hasattr(image_n, "shape") else inn.shape)[-2:]
+    keep = [d, _np(normals), _np(uvs, np.int32), _np(R), _np(T), ir, inn]
+    lib().gsro_warp_patch_ncc(P, _p(keep[0]), _p(keep[1]), _p(keep[2], _i), _p(keep[3]), _p(keep[4]), _p(keep[5]),
+                              _p(keep[6]), float(fx_r), float(fy_r), float(cx_r), float(cy_r), float(fx_n),
+                              float(fy_n), float(cx_n), float(cy_n), int(Hr), int(Wr), int(Hn), int(Wn),
+                              _p(out["ncc"]), _p(out["grad_depths"]), _p(out["grad_normals"]), _p(out["valid"], _u8))
+    out["valid"] = out["valid"].astype(bool)
     return out

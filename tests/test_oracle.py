@@ -20,6 +20,7 @@ import torch
 import gsr_scene as S
 import helpers as Hh
 import torch_ref as R
+import torch_ref as R_
 from oracle import gsr_oracle as O
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -411,3 +412,52 @@ def test_sample_depth_at_pixel_centres_equals_render():
     close = np.abs(zs - md[ys, xs]) <= 1e-4 * np.abs(md).max()
     assert close.mean() > 0.995, close.mean()  # points land within ~1e-5 px of the centre
     assert s["inside"].mean() > 0.995
+
+
+# ---------------------------------------------------------- warp_patch_ncc
+def ncc_case(P, seed, Wr=48, Hr=40, Wn=52, Hn=44):
+    """Two smooth textured images, a relative pose (r to n) and random
+    pixels with depths and normals facing the camera."""
+    g = torch.Generator().manual_seed(seed)
+
+    def texture(H, W):
+        base = torch.rand(1, 1, H // 4 + 2, W // 4 + 2, generator=g)
+        img = torch.nn.functional.interpolate(base, size=(H, W), mode="bicubic", align_corners=True)[0, 0]
+        return (img + 0.05 * torch.rand(H, W, generator=g)).float().contiguous()
+
+    img_r, img_n = texture(Hr, Wr), texture(Hn, Wn)
+    a = torch.randn(3, generator=g, dtype=torch.float64)
+    a = a / a.norm()
+    th = 0.08
+    K = torch.tensor([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]], dtype=torch.float64)
+    Rm = torch.eye(3, dtype=torch.float64) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+    T = (torch.randn(3, generator=g) * 0.1).float()
+    R = Rm.T.reshape(-1).float().contiguous()  # column-major float33: column i at [3i:3i+3]
+    uvs = torch.stack([torch.randint(3, Wr - 3, (P,), generator=g), torch.randint(3, Hr - 3, (P,), generator=g)],
+                      1).int().contiguous()
+    depths = (torch.rand(P, generator=g) * 2 + 2).float()
+    nrm = torch.randn(P, 3, generator=g) * 0.3
+    nrm[:, 2] = -1.0
+    normals = (nrm / nrm.norm(dim=1, keepdim=True)).float().contiguous()
+    K = dict(fx_r=50.0, fy_r=52.0, cx_r=Wr / 2 - 0.3, cy_r=Hr / 2 + 0.2, fx_n=55.0, fy_n=54.0, cx_n=Wn / 2,
+             cy_n=Hn / 2 - 0.4)
+    return depths, normals, uvs, R, T, img_r, img_n, K
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_warp_patch_ncc_matches_float64_autograd(seed):
+    """warp_patch_ncc (warp_patch_ncc_impl.cu:18-266): NCC values, valid flags
+    and the forward-mode d(NCC)/d(depth, normal) against autograd of an
+    independent float64 restatement (textured images, so var_r var_n >> 1e-8
+    and the reference's -ncc / (var_n + 1e-8) term is the exact derivative)."""
+    d, n, uv, R, T, ir, inn, K = ncc_case(400, seed)
+    o = O.warp_patch_ncc(d, n, uv, R, T, ir, inn, *K.values())
+    assert o["valid"].sum() > 100
+    dd = d.double().clone().requires_grad_(True)
+    nd = n.double().clone().requires_grad_(True)
+    ncc, valid = R_.warp_patch_ncc(dd, nd, uv, R, T, ir, inn, *K.values())
+    assert np.array_equal(valid.numpy(), o["valid"])
+    assert Hh.rel_err(o["ncc"], ncc.detach().numpy()) < 5e-4  # fp32 one-pass variances cancel
+    ncc.sum().backward()
+    assert Hh.rel_err(o["grad_depths"], dd.grad.numpy()) < 1e-3
+    assert Hh.rel_err(o["grad_normals"], nd.grad.numpy()) < 1e-3

@@ -477,3 +477,58 @@ def sample_surrogate(out, dL_doutput):
         kappa = torch.where(valid, kappa, torch.zeros_like(kappa))
         tot = tot + (kappa.detach() * 0.5 * logT).sum()
     return tot
+
+
+def _bilinear(img, u, v):
+    """Bilinear sample of img [H, W] at (u, v) with taps (floor, floor + 1),
+    clamped to the image, differentiable in (u, v) (warp_patch_ncc_impl.cu:178-199)."""
+    H, W = img.shape
+    u0f, v0f = torch.floor(u.detach()), torch.floor(v.detach())
+    u0 = u0f.long().clamp(0, W - 1)
+    v0 = v0f.long().clamp(0, H - 1)
+    u1 = (u0f + 1).long().clamp(0, W - 1)
+    v1 = (v0f + 1).long().clamp(0, H - 1)
+    wu1, wv1 = u - u0f, v - v0f
+    wu0, wv0 = (u0f + 1) - u, (v0f + 1) - v
+    c00, c01, c10, c11 = img[v0, u0], img[v0, u1], img[v1, u0], img[v1, u1]
+    return wv0 * (wu0 * c00 + wu1 * c01) + wv1 * (wu0 * c10 + wu1 * c11)
+
+
+def warp_patch_ncc(depths, normals, uvs, R, T, image_r, image_n, fx_r, fy_r, cx_r, cy_r, fx_n, fy_n, cx_n, cy_n):
+    """Dense float64 restatement of the warp-patch NCC (warp_patch_ncc_impl.cu:18-266): the 7x7 half-step patch
+    around each reference pixel is mapped by the plane-induced homography H = K_n (R - T n^T / d) K_r^-1 with
+    d = -n . K_r^-1 (u, v, 1) * depth; NCC = cross^2 / (var_r var_n + 1e-8).  Returns (ncc, valid) with ncc
+    differentiable in depths and normals (autograd replaces the reference's forward-mode derivative).
+    R is indexed as the reference's column-major float33 (column i = R[3i:3i+3])."""
+    dt = depths.dtype
+    P = depths.shape[0]
+    u = uvs[:, 0].to(dt)
+    v = uvs[:, 1].to(dt)
+    pnr = torch.stack([(u - cx_r) / fx_r, (v - cy_r) / fy_r, torch.ones_like(u)], 1)
+    dist = -(pnr * normals).sum(1) * depths
+    Rm = R.reshape(3, 3).T.to(dt)  # math matrix: column i = R[3i:3i+3]
+    Kn = torch.tensor([[fx_n, 0, cx_n], [0, fy_n, cy_n], [0, 0, 1]], dtype=dt)
+    Kr_inv = torch.tensor([[1 / fx_r, 0, -cx_r / fx_r], [0, 1 / fy_r, -cy_r / fy_r], [0, 0, 1]], dtype=dt)
+    Hn = Rm[None] - T.to(dt)[None, :, None] * (normals / dist[:, None])[:, None, :]
+    H = Kn[None] @ Hn @ Kr_inv[None]
+    offs = torch.arange(-3, 4, dtype=dt) * 0.5
+    dv, du = torch.meshgrid(offs, offs, indexing="ij")
+    ur = u[:, None] + du.reshape(1, -1)
+    vr = v[:, None] + dv.reshape(1, -1)
+    c_r = _bilinear(image_r.to(dt), ur, vr)
+    hom = torch.stack([ur, vr, torch.ones_like(ur)], -1)  # [P, 49, 3]
+    w = hom @ H.transpose(1, 2)
+    un, vn = w[..., 0] / w[..., 2], w[..., 1] / w[..., 2]
+    Hn_img, Wn_img = image_n.shape
+    inside_n = ((un - 1.5 > 0) & (un + 1.5 < Wn_img - 1) & (vn - 1.5 > 0) & (vn + 1.5 < Hn_img - 1)).all(1)
+    Hr_img, Wr_img = image_r.shape
+    inside_r = (u - 1.5 > 0) & (u + 1.5 < Wr_img - 1) & (v - 1.5 > 0) & (v + 1.5 < Hr_img - 1)
+    c_n = _bilinear(image_n.to(dt), un, vn)
+    n = 49.0
+    s_r, s_n = c_r.sum(1), c_n.sum(1)
+    cross = (c_r * c_n).sum(1) - s_r * s_n / n
+    var_r = (c_r * c_r).sum(1) - s_r * s_r / n
+    var_n = (c_n * c_n).sum(1) - s_n * s_n / n
+    ncc = cross * cross / (var_r * var_n + 1e-8)
+    valid = (inside_r & inside_n & (var_r > 5e-6) & (var_n > 5e-6)).detach()
+    return torch.where(valid, ncc, torch.zeros_like(ncc)), valid
