@@ -754,6 +754,32 @@ int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const i
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "warp_patch_ncc", e);
 }
 
+int gsr_fused_ssim_forward(gsr_alloc_fn scratch_alloc, void* scratch_ctx, int NC, int H, int W, int valid,
+                           const float* img1, const float* img2, float* out_mean, float* factors, void* stream_ptr) {
+    if (NC <= 0 || H <= 0 || W <= 0 || (valid && (H <= 10 || W <= 10)))
+        return fail(GSR_ERR_ARGS, "fused_ssim: invalid sizes (valid padding needs H, W > 10)");
+    if (!img1 || !img2 || !out_mean || !scratch_alloc) return fail(GSR_ERR_ARGS, "fused_ssim: missing buffer");
+    const size_t n = ssim_partials(NC, H, W);
+    void* buf = scratch_alloc(scratch_ctx, n * sizeof(float) + 256);
+    if (!buf) return fail(GSR_ERR_ALLOC, "fused_ssim: scratch allocation failed");
+    float* partial = reinterpret_cast<float*>(aligned_base(buf));
+    const size_t plane = (size_t)NC * H * W;
+    hipError_t e = launch_ssim_fwd(NC, H, W, valid, img1, img2, factors, factors ? factors + plane : nullptr,
+                                   factors ? factors + 2 * plane : nullptr, partial, out_mean, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "fused_ssim forward", e);
+}
+
+int gsr_fused_ssim_backward(int NC, int H, int W, int valid, const float* img1, const float* img2,
+                            const float* factors, const float* dL_dmean, float* dL_dimg1, void* stream_ptr) {
+    if (NC <= 0 || H <= 0 || W <= 0 || (valid && (H <= 10 || W <= 10)))
+        return fail(GSR_ERR_ARGS, "fused_ssim: invalid sizes");
+    if (!img1 || !img2 || !factors || !dL_dmean || !dL_dimg1) return fail(GSR_ERR_ARGS, "fused_ssim: missing buffer");
+    const size_t plane = (size_t)NC * H * W;
+    hipError_t e = launch_ssim_bwd(NC, H, W, valid, img1, img2, factors, factors + plane, factors + 2 * plane,
+                                   dL_dmean, dL_dimg1, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "fused_ssim backward", e);
+}
+
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream_ptr) {
     (void)projmatrix;

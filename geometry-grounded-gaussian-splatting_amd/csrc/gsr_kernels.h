@@ -153,6 +153,14 @@ struct NccParams {
 };
 hipError_t launch_ncc(const NccParams& q, hipStream_t stream);
 
+// ssim.hip: fused SSIM forward / backward
+size_t ssim_partials(int NC, int H, int W);
+hipError_t launch_ssim_fwd(int NC, int H, int W, int valid, const float* img1, const float* img2, float* fA,
+                           float* fB, float* fC, float* partial, float* out, hipStream_t stream);
+hipError_t launch_ssim_bwd(int NC, int H, int W, int valid, const float* img1, const float* img2, const float* fA,
+                           const float* fB, const float* fC, const float* dL_dloss, float* dL_dimg1,
+                           hipStream_t stream);
+
 // mark visible
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t stream);

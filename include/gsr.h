@@ -203,6 +203,23 @@ int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const i
                        float* grad_normals, uint8_t* valid, void* stream);
 
 /*
+ * D-SSIM term: replaces the external fused_ssim(img1,
+ * img2, padding) that utils/loss_utils.py:48-49 calls (padding "valid") with
+ * the SSIM of the reference's own _ssim (loss_utils.py:36-72): 11 x 11
+ * Gaussian window, sigma 1.5, C1 = 1e-4, C2 = 9e-4, zero padding.  Images
+ * are NC planes of H x W fp32 (e.g. [1,3,H,W]).  valid != 0 averages over
+ * the positions whose window lies inside the image (needs H, W > 10).
+ * *out_mean (device) receives the mean SSIM.  factors (device, 3*NC*H*W
+ * floats, may be NULL when no gradient is wanted) receives what the backward
+ * reads.  The backward writes dL/dimg1 (NC*H*W) for dL/dmean at dL_dmean
+ * (device scalar).
+ */
+int gsr_fused_ssim_forward(gsr_alloc_fn scratch_alloc, void* scratch_ctx, int NC, int H, int W, int valid,
+                           const float* img1, const float* img2, float* out_mean, float* factors, void* stream);
+int gsr_fused_ssim_backward(int NC, int H, int W, int valid, const float* img1, const float* img2,
+                            const float* factors, const float* dL_dmean, float* dL_dimg1, void* stream);
+
+/*
  * Per-stage GPU timing (no reference equivalent; SURVEY §5 "tracing").  While
  * enabled, every kernel stage of the calls above is bracketed by two hipEvents
  * on the call's stream.  gsr_timing_collect() waits for the recorded events,
