@@ -780,6 +780,24 @@ int gsr_fused_ssim_backward(int NC, int H, int W, int valid, const float* img1, 
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "fused_ssim backward", e);
 }
 
+int gsr_depth_to_normal_forward(const float* depth, int H, int W, float Fx, float Fy, float Cx, float Cy,
+                                float* normal, uint8_t* valid, void* stream_ptr) {
+    if (H < 0 || W < 0 || (H * W > 0 && (!depth || !normal || !valid)))
+        return fail(GSR_ERR_ARGS, "depth_to_normal: invalid arguments");
+    hipError_t e = launch_depth_normal(false, depth, H, W, Fx, Fy, Cx, Cy, nullptr, normal, valid,
+                                       (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "depth_to_normal", e);
+}
+
+int gsr_depth_to_normal_backward(const float* depth, int H, int W, float Fx, float Fy, float Cx, float Cy,
+                                 const float* dL_dnormal, float* dL_ddepth, void* stream_ptr) {
+    if (H < 0 || W < 0 || (H * W > 0 && (!depth || !dL_dnormal || !dL_ddepth)))
+        return fail(GSR_ERR_ARGS, "depth_to_normal backward: invalid arguments");
+    hipError_t e = launch_depth_normal(true, depth, H, W, Fx, Fy, Cx, Cy, dL_dnormal, dL_ddepth, nullptr,
+                                       (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "depth_to_normal backward", e);
+}
+
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream_ptr) {
     (void)projmatrix;

@@ -161,6 +161,10 @@ hipError_t launch_ssim_bwd(int NC, int H, int W, int valid, const float* img1, c
                            const float* fB, const float* fC, const float* dL_dloss, float* dL_dimg1,
                            hipStream_t stream);
 
+// depth_normal.hip: normal map of a depth map and its backward
+hipError_t launch_depth_normal(bool backward, const float* depth, int H, int W, float Fx, float Fy, float Cx, float Cy,
+                               const float* g, float* out, uint8_t* valid, hipStream_t stream);
+
 // mark visible
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t stream);

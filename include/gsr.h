@@ -220,6 +220,18 @@ int gsr_fused_ssim_backward(int NC, int H, int W, int valid, const float* img1, 
                             const float* factors, const float* dL_dmean, float* dL_dimg1, void* stream);
 
 /*
+ * Depth-normal consistency input: replaces the torch
+ * function depth_to_normal (utils/graphics_utils.py:103-119).  depth [H,W];
+ * forward: normal [3,H,W] (zero on the border), valid [H,W] uint8;
+ * backward: dL/ddepth [H,W] for dL/dnormal [3,H,W].  Fx, Fy, Cx, Cy are the
+ * camera's (scene/cameras.py).
+ */
+int gsr_depth_to_normal_forward(const float* depth, int H, int W, float Fx, float Fy, float Cx, float Cy,
+                                float* normal, uint8_t* valid, void* stream);
+int gsr_depth_to_normal_backward(const float* depth, int H, int W, float Fx, float Fy, float Cx, float Cy,
+                                 const float* dL_dnormal, float* dL_ddepth, void* stream);
+
+/*
  * Per-stage GPU timing (no reference equivalent; SURVEY §5 "tracing").  While
  * enabled, every kernel stage of the calls above is bracketed by two hipEvents
  * on the call's stream.  gsr_timing_collect() waits for the recorded events,

@@ -1,4 +1,4 @@
-"""TEST INFRASTRUCTURE ONLY — float64 torch restatement of the reference's
+"""TEST INFRASTRUCTURE ONLY — float64 torch restatements of the reference's
 SSIM (utils/loss_utils.py:36-72: gaussian(11, 1.5) window, _ssim with
 C1 = 0.01^2, C2 = 0.03^2, conv2d with zero padding 5), the checker of the
 fused SSIM kernel (csrc/ssim.hip).  "valid" padding (the mode loss_utils.ssim
@@ -35,3 +35,23 @@ def ssim(img1, img2, padding="same", window_size=11):
     if padding == "valid":
         m = m[:, :, p:-p, p:-p]
     return m.mean()
+
+
+def depth_to_normal(depth, Fx, Fy, Cx, Cy):
+    """float64 restatement of utils/graphics_utils.py:103-119 for a depth
+    [1,H,W]: back-projected points, central differences, normalize(dy x dx)
+    (eps 1e-12), zero border; valid = depth > 0 at the five taps."""
+    _, H, W = depth.shape
+    x = (torch.arange(W, dtype=torch.float32) - Cx) / Fx  # fp32 as the reference's arange
+    y = (torch.arange(H, dtype=torch.float32) - Cy) / Fy
+    x, y = x.to(depth.dtype), y.to(depth.dtype)
+    pts = torch.cat([depth * x[None, None], depth * y[None, :, None], depth], dim=0)
+    dy = pts[:, 2:, 1:-1] - pts[:, :-2, 1:-1]
+    dx = pts[:, 1:-1, 2:] - pts[:, 1:-1, :-2]
+    n = F.normalize(torch.cross(dy, dx, dim=0), dim=0)
+    out = F.pad(n, (1, 1, 1, 1))
+    v = depth > 0
+    vi = v[:, 2:, 1:-1] & v[:, :-2, 1:-1] & v[:, 1:-1, 2:] & v[:, 1:-1, :-2] & v[:, 1:-1, 1:-1]
+    valid = torch.zeros_like(depth, dtype=torch.bool)
+    valid[:, 1:-1, 1:-1] = vi
+    return out, valid
