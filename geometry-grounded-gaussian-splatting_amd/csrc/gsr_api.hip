@@ -129,6 +129,7 @@ size_t carve_points(void* base, int PN, PointState& s) {
     s.mdepth = c.take<float>(PN);
     s.dT = c.take<float>(PN);
     s.cached = c.take<uint8_t>(PN);
+    s.t = c.take<float>(PN);
     return c.off + 256;
 }
 
@@ -338,7 +339,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 5; }
+int gsr_abi_version(void) { return 6; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -541,16 +542,22 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
     return GSR_OK;
 }
 
-int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
-                             gsr_alloc_fn point_alloc, void* point_ctx, gsr_alloc_fn point_binning_alloc,
-                             void* point_binning_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
-                             gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P, int width, int height,
-                             const float* points3D, const float* means3D, const float* opacities,
-                             const float* scales, float scale_modifier, const float* rotations,
-                             const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
-                             const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size,
-                             int prefiltered, float* output, uint8_t* inside, int debug, void* stream_ptr,
-                             int* num_rendered, int* num_points, int* num_duplicated_tiles) {
+// The point-query forwards (sample_depth, integrate, evaluate_sdf) share
+// everything but the raster's mode and outputs: Rasterizer::sampleDepth
+// (rasterizer_impl.cu:1042-1261), evaluateTransmittance (:594-815) and
+// evaluateSDF (:817-1040) run the same preprocess, Gaussian binning, point
+// preprocess and point binning.
+static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc,
+                               void* binning_ctx, gsr_alloc_fn point_alloc, void* point_ctx,
+                               gsr_alloc_fn point_binning_alloc, void* point_binning_ctx, gsr_alloc_fn tile_alloc,
+                               void* tile_ctx, gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P,
+                               int width, int height, const float* points3D, const float* means3D,
+                               const float* opacities, const float* scales, float scale_modifier,
+                               const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                               const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                               float kernel_size, int prefiltered, float* output, float* output2, uint8_t* inside,
+                               int debug, void* stream_ptr, int* num_rendered, int* num_points,
+                               int* num_duplicated_tiles) {
     (void)prefiltered;
     hipStream_t stream = (hipStream_t)stream_ptr;
     if (num_rendered) *num_rendered = 0;
@@ -567,7 +574,7 @@ int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
     if (!means3D || !opacities || !viewmatrix || !projmatrix || !points3D) return fail(GSR_ERR_ARGS, "missing input");
     if ((scales && rotations) == (cov3D_precomp != nullptr))
         return fail(GSR_ERR_ARGS, "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
-    if (!output || !inside) return fail(GSR_ERR_ARGS, "missing output buffer");
+    if (!output || !inside || (query == kQuerySDF && !output2)) return fail(GSR_ERR_ARGS, "missing output buffer");
     if (!geom_alloc || !binning_alloc || !point_alloc || !point_binning_alloc || !tile_alloc || !dup_tile_alloc)
         return fail(GSR_ERR_ARGS, "missing allocator");
     const uint32_t tiles = p.grid_x * p.grid_y;
@@ -630,11 +637,68 @@ int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
         GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K_live, ts, (int)tiles, stream), "tile ranges");
     }
     GSR_STAGE(GSR_STAGE_SAMPLE_FWD,
-              launch_sample_fwd(p, gs, bs, ts, ps, pb, st, cs, n_chunks, output, inside, stream), "sample");
+              launch_point_fwd(query, p, gs, bs, ts, ps, pb, st, cs, n_chunks, output, output2, inside, stream),
+              "point query");
     if (num_rendered) *num_rendered = (int)K;
     if (num_points) *num_points = (int)totals[0];
     if (num_duplicated_tiles) *num_duplicated_tiles = (int)totals[1];
     return GSR_OK;
+}
+
+int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn point_alloc, void* point_ctx, gsr_alloc_fn point_binning_alloc,
+                             void* point_binning_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                             gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P, int width, int height,
+                             const float* points3D, const float* means3D, const float* opacities,
+                             const float* scales, float scale_modifier, const float* rotations,
+                             const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                             const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size,
+                             int prefiltered, float* output, uint8_t* inside, int debug, void* stream_ptr,
+                             int* num_rendered, int* num_points, int* num_duplicated_tiles) {
+    return point_query_forward(kQuerySample, geom_alloc, geom_ctx, binning_alloc, binning_ctx, point_alloc,
+                               point_ctx, point_binning_alloc, point_binning_ctx, tile_alloc, tile_ctx,
+                               dup_tile_alloc, dup_tile_ctx, PN, P, width, height, points3D, means3D, opacities,
+                               scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos,
+                               tan_fovx, tan_fovy, kernel_size, prefiltered, output, nullptr, inside, debug,
+                               stream_ptr, num_rendered, num_points, num_duplicated_tiles);
+}
+
+int gsr_integrate_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                          gsr_alloc_fn point_alloc, void* point_ctx, gsr_alloc_fn point_binning_alloc,
+                          void* point_binning_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                          gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P, int width, int height,
+                          const float* points3D, const float* means3D, const float* opacities, const float* scales,
+                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                          const float* view2gaussian_precomp, const float* viewmatrix, const float* projmatrix,
+                          const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
+                          float* out_transmittance, uint8_t* inside, int debug, void* stream_ptr,
+                          int* num_rendered) {
+    (void)view2gaussian_precomp;  // unused by the reference (rasterizer_impl.cu:610)
+    return point_query_forward(kQueryIntegrate, geom_alloc, geom_ctx, binning_alloc, binning_ctx, point_alloc,
+                               point_ctx, point_binning_alloc, point_binning_ctx, tile_alloc, tile_ctx,
+                               dup_tile_alloc, dup_tile_ctx, PN, P, width, height, points3D, means3D, opacities,
+                               scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos,
+                               tan_fovx, tan_fovy, kernel_size, prefiltered, out_transmittance, nullptr, inside,
+                               debug, stream_ptr, num_rendered, nullptr, nullptr);
+}
+
+int gsr_evaluate_sdf_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn point_alloc, void* point_ctx, gsr_alloc_fn point_binning_alloc,
+                             void* point_binning_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                             gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P, int width, int height,
+                             const float* points3D, const float* means3D, const float* opacities,
+                             const float* scales, float scale_modifier, const float* rotations,
+                             const float* cov3D_precomp, const float* view2gaussian_precomp,
+                             const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                             float tan_fovy, float kernel_size, int prefiltered, float* out_depth, float* out_sdf,
+                             uint8_t* inside, int debug, void* stream_ptr, int* num_rendered) {
+    (void)view2gaussian_precomp;  // unused by the reference (rasterizer_impl.cu:833)
+    return point_query_forward(kQuerySDF, geom_alloc, geom_ctx, binning_alloc, binning_ctx, point_alloc, point_ctx,
+                               point_binning_alloc, point_binning_ctx, tile_alloc, tile_ctx, dup_tile_alloc,
+                               dup_tile_ctx, PN, P, width, height, points3D, means3D, opacities, scales,
+                               scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx,
+                               tan_fovy, kernel_size, prefiltered, out_depth, out_sdf, inside, debug, stream_ptr,
+                               num_rendered, nullptr, nullptr);
 }
 
 int gsr_sample_depth_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int PN, int P, int RN, int R, int TN,

@@ -120,6 +120,7 @@ struct PointState {  // per point (point buffer)
     float* mdepth;     // median depth along the ray (the reference's pointState.median_depth)
     float* dT;         // dT/dt_m at mdepth, computed by the forward when `cached`
     uint8_t* cached;
+    float* t;          // |p_view| (preprocessPointsCUDA ts, sample_forward.cu:50; integrate / evaluate_sdf)
 };
 struct PointBinState {  // point binning buffer
     uint32_t* keys_unsorted;  // tile of each point (num_tiles when culled: sorts last)

@@ -96,10 +96,14 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
 hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const BwdState& ws, hipStream_t stream);
 
 // render_fwd.hip: the forward raster in SAMPLE mode (median depth at points)
-hipError_t launch_sample_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const TileState& ts,
-                             const PointState& ps, const PointBinState& pb, const SampleTiles& st,
-                             const ChunkState& cs, uint32_t num_chunks, float* out_points, uint8_t* out_inside,
-                             hipStream_t stream);
+// point queries answered by the forward raster in SAMPLE mode
+enum { kQuerySample = 0, kQueryIntegrate = 1, kQuerySDF = 2 };
+// sample_depth: out0 = points [PN][3]; integrate: out0 = transmittance [PN];
+// evaluate_sdf: out0 = median depth [PN], out1 = sdf [PN]
+hipError_t launch_point_fwd(int query, const FwdParams& p, const GeomState& gs, const BinningState& bs,
+                            const TileState& ts, const PointState& ps, const PointBinState& pb, const SampleTiles& st,
+                            const ChunkState& cs, uint32_t num_chunks, float* out0, float* out1, uint8_t* out_inside,
+                            hipStream_t stream);
 
 // sample.hip
 size_t point_sort_temp_bytes(int PN, uint32_t tiles);

@@ -57,6 +57,7 @@ struct RenderFwdArgs {
     float* out_normal;
     float* out_mdepth;
     int passes;  // bisection passes (kSplitIterations; fewer only for GSR_OPT_BISECT_PASSES timing runs)
+    float sample_range;  // half-width of the first bisection window (kSampleRange; 2 kSampleRange for evaluate_sdf)
     // SAMPLE mode (sample_depth, sample.hip): a workgroup is one chunk of
     // kTilePixels points of one tile instead of the tile's pixels
     uint32_t num_chunks;
@@ -64,7 +65,11 @@ struct RenderFwdArgs {
     const uint2* pt_ranges;     // [tiles] points of each tile in pt_list
     const uint32_t* pt_list;    // point indices grouped by tile
     const float2* pt_xy;        // projected point positions
-    float* out_points;          // [PN][3] camera-space point at the median depth
+    int query;                  // kQuerySample / kQueryIntegrate / kQuerySDF
+    const float* pt_t;          // [PN] |p_view| of each point
+    float* out_points;          // [PN][3] camera-space point at the median depth (sample_depth);
+                                // [PN] transmittance (integrate) or median depth (evaluate_sdf)
+    float* out_sdf;             // [PN] median depth - |p_view| (evaluate_sdf)
     uint8_t* out_inside;        // [PN]
     uint32_t* pt_last;          // [PN] last contributor
     float* pt_mdepth;           // [PN] median depth along the ray
@@ -150,10 +155,15 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
 // more than kFarDelta sigma from the splat's peak (exact-constant factors).
 __device__ unsigned long long g_render_stats[8];
 
-// SAMPLE: the median depth at arbitrary points (sampleDepthCUDA,
-// sample_forward.cu:430-657) — lanes hold points of one tile's chunk, the
-// composite keeps only T / last / m0 / blended set, and the outputs are the
-// per-point ones.  Everything else (batching, bisection) is shared.
+// SAMPLE: queries at arbitrary points — lanes hold points of one tile's
+// chunk and the outputs are per point.  Everything else (batching,
+// bisection) is shared with the render path.
+//  * GEOM (sample_depth, sampleDepthCUDA, sample_forward.cu:430-657; and
+//    evaluate_sdf, evaluateSDFCUDA, :171-427, which differs only in a twice
+//    as wide first window, one more pass and its outputs): the composite
+//    keeps only T / last / m0 / blended set, then the bisection runs.
+//  * !GEOM (integrate, evaluateTransmittanceCUDA, :55-169): the composite
+//    also carries the vacancy transmittance at the point's own distance.
 template <bool GEOM, bool SKIP, bool STATS = false, bool SAMPLE = false>
 __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 256 x 16 B = 16 KB) aliased with the
@@ -172,7 +182,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     uint32_t tile, chunk = 0, pid = 0;
     int px = 0, py = 0;
     bool inside;
-    float pixx, pixy;
+    float pixx, pixy, pt_t = 0.f;
     if constexpr (SAMPLE) {
         // chunks of one tile are consecutive: XCD-contiguous runs of chunks share Gaussian lists
         chunk = xcd_remap(blockIdx.x, a.num_chunks);
@@ -190,6 +200,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         const float2 xy = inside ? a.pt_xy[pid] : make_float2(0.f, 0.f);
         pixx = xy.x;
         pixy = xy.y;
+        if constexpr (!GEOM) pt_t = inside ? a.pt_t[pid] : 0.f;
     } else {
         tile = xcd_remap(blockIdx.x, a.num_tiles);
         const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
@@ -218,7 +229,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         for (int q = 0; q < kMaskWords; q++) my_mask[q * kTilePixels] = 0u;
     }
 
-    float T = 1.0f;
+    float T = 1.0f, T_pt = 1.0f;
     uint32_t contributor = 0, last = 0;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
     float N0 = 0.f, N1 = 0.f, N2 = 0.f, m_init = 0.f;
@@ -257,6 +268,15 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             }
             const float aT = alpha * T;
             const float4 w2 = s_w2[j];
+            if constexpr (SAMPLE && !GEOM) {
+                // vacancy transmittance at the point (sample_forward.cu:152-160)
+                const float t_peak = splat_tpeak(w1, w2, dx, dy);
+                const float rsigma = w2.y;
+                const float delta = (t_peak - pt_t) * rsigma;
+                const float g = rsigma > 0.f ? __expf(-0.5f * delta * delta) : 0.f;
+                const float omg = 1.f - alpha * g;
+                T_pt *= (pt_t > t_peak ? 1.f - alpha : omg) * __builtin_amdgcn_rsqf(omg);
+            }
             if constexpr (!SAMPLE) {
                 const float4 w3 = s_w3[j];
                 C0 = __builtin_fmaf(w2.z, aT, C0);
@@ -299,8 +319,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     if constexpr (GEOM) {
         unsigned long long st[4] = {0, 0, 0, 0};
         float Tp[kSplit + 1];
-        float dmin = fmaxf(m_init - kSampleRange, 0.f);
-        float dmax = fmaxf(m_init + kSampleRange, 0.f);
+        float dmin = fmaxf(m_init - a.sample_range, 0.f);
+        float dmax = fmaxf(m_init + a.sample_range, 0.f);
         bool in_range = T <= kMinTransmittance;
         const bool resident = max_contrib <= (uint32_t)kResident;
         float4* c_w0 = s_rec;
@@ -484,7 +504,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             mDepth_b = md_out * nrm;
         }
         float dT_dtm = 0.f;
-        if (resident && inside && mDepth_b != 0.f && last != 0) {
+        const bool want_dT = !SAMPLE || a.query == kQuerySample;
+        if (want_dT && resident && inside && mDepth_b != 0.f && last != 0) {
             const int nwords = (int)((last + 31) >> 5);
             for (int w = 0; w < nwords; w++) {
                 uint32_t bits = my_mask[w * kTilePixels];
@@ -507,8 +528,21 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         md_ok = resident;
     }
 
+    if constexpr (SAMPLE && !GEOM) {
+        if (inside) {  // sample_forward.cu:165-168
+            a.out_points[pid] = T_pt;
+            a.out_inside[pid] = 1;
+        }
+        if (tid == 0) a.chunk_max[chunk] = max_contrib;
+        return;
+    }
     if constexpr (SAMPLE) {
-        if (inside) {
+        if (inside && a.query == kQuerySDF) {
+            // sample_forward.cu:420-427
+            a.out_points[pid] = mDepth;
+            a.out_sdf[pid] = mDepth - a.pt_t[pid];
+            a.out_inside[pid] = (uint8_t)(md_in_range ? 1 : 0);
+        } else if (inside) {
             // sample_forward.cu:647-657
             const float pnx = (pixx - (float)(a.W - 1) / 2.f) / a.focal_x;
             const float pny = (pixy - (float)(a.H - 1) / 2.f) / a.focal_y;
@@ -575,6 +609,7 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.out_alpha = out_alpha;
     a.out_normal = out_normal;
     a.out_mdepth = out_mdepth;
+    a.sample_range = kSampleRange;
     {
         const int np = option(kOptBisectPasses);
         a.passes = (np > 0 && np < kSplitIterations) ? np : kSplitIterations;
@@ -594,10 +629,10 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     return hipGetLastError();
 }
 
-hipError_t launch_sample_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const TileState& ts,
-                             const PointState& ps, const PointBinState& pb, const SampleTiles& st,
-                             const ChunkState& cs, uint32_t num_chunks, float* out_points, uint8_t* out_inside,
-                             hipStream_t stream) {
+hipError_t launch_point_fwd(int query, const FwdParams& p, const GeomState& gs, const BinningState& bs,
+                            const TileState& ts, const PointState& ps, const PointBinState& pb, const SampleTiles& st,
+                            const ChunkState& cs, uint32_t num_chunks, float* out0, float* out1, uint8_t* out_inside,
+                            hipStream_t stream) {
     RenderFwdArgs a{};
     a.ranges = ts.ranges;
     a.point_list = bs.point_list;
@@ -608,13 +643,18 @@ hipError_t launch_sample_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.num_tiles = p.grid_x * p.grid_y;
     a.focal_x = p.focal_x;
     a.focal_y = p.focal_y;
-    a.passes = kSplitIterations;
+    // evaluateSDF: SPLIT_ITERATIONS + 1 passes over a +-2 SAMPLE_RANGE window (sample_forward.cu:319-320, 792)
+    a.passes = query == kQuerySDF ? kSplitIterations + 1 : kSplitIterations;
+    a.sample_range = query == kQuerySDF ? kSampleRange * 2.f : kSampleRange;
+    a.query = query;
+    a.pt_t = ps.t;
+    a.out_sdf = out1;
     a.num_chunks = num_chunks;
     a.chunk_off = st.chunk_off;
     a.pt_ranges = st.pt_ranges;
     a.pt_list = pb.pt_list;
     a.pt_xy = ps.xy;
-    a.out_points = out_points;
+    a.out_points = out0;
     a.out_inside = out_inside;
     a.pt_last = ps.last;
     a.pt_mdepth = ps.mdepth;
@@ -622,8 +662,12 @@ hipError_t launch_sample_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.pt_cached = ps.cached;
     a.chunk_max = cs.chunk_max;
     if (num_chunks == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_fwd_kernel<true, false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0, stream,
-                       a);
+    if (query == kQueryIntegrate)
+        hipLaunchKernelGGL((render_fwd_kernel<false, false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,
+                           stream, a);
+    else
+        hipLaunchKernelGGL((render_fwd_kernel<true, false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,
+                           stream, a);
     return hipGetLastError();
 }
 

@@ -51,7 +51,8 @@ __device__ inline float ndc2pix_d(float v, int S) { return (float)((((double)v +
 __global__ void __launch_bounds__(256)
     sample_points_kernel(int PN, const float* __restrict__ pts, const float* __restrict__ V,
                          const float* __restrict__ M, int W, int H, uint32_t gx, uint32_t gy,
-                         float2* __restrict__ xy_out, uint32_t* __restrict__ keys, uint32_t* __restrict__ counts) {
+                         float2* __restrict__ xy_out, float* __restrict__ t_out, uint32_t* __restrict__ keys,
+                         uint32_t* __restrict__ counts) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= PN) return;
     const uint32_t tiles = gx * gy;
@@ -59,6 +60,8 @@ __global__ void __launch_bounds__(256)
     const float x = pts[3 * idx], y = pts[3 * idx + 1], z = pts[3 * idx + 2];
     const float vz = V[2] * x + V[6] * y + V[10] * z + V[14];
     if (vz <= kNearPlane) return;  // in_frustum (auxiliary.h:133-153)
+    const float vx = V[0] * x + V[4] * y + V[8] * z + V[12];
+    const float vy = V[1] * x + V[5] * y + V[9] * z + V[13];
     const float hx = M[0] * x + M[4] * y + M[8] * z + M[12];
     const float hy = M[1] * x + M[5] * y + M[9] * z + M[13];
     const float hw = M[3] * x + M[7] * y + M[11] * z + M[15];
@@ -66,6 +69,7 @@ __global__ void __launch_bounds__(256)
     const float px = ndc2pix_d(hx * p_w, W), py = ndc2pix_d(hy * p_w, H);
     if (px < 0 || px > W - 1 || py < 0 || py > H - 1) return;
     xy_out[idx] = make_float2(px, py);
+    t_out[idx] = sqrtf(vx * vx + vy * vy + vz * vz);  // norm3df(p_view), sample_forward.cu:50
     const uint32_t tx = (uint32_t)min((int)gx - 1, max(0, (int)((px + 0.5f) / kTile)));
     const uint32_t ty = (uint32_t)min((int)gy - 1, max(0, (int)((py + 0.5f) / kTile)));
     const uint32_t t = ty * gx + tx;
@@ -88,7 +92,7 @@ hipError_t launch_sample_points(const FwdParams& p, int PN, const float* points3
     hipError_t e = hipMemsetAsync(st.counts, 0, sizeof(uint32_t) * tiles, stream);
     if (e != hipSuccess || PN == 0) return e;
     hipLaunchKernelGGL(sample_points_kernel, dim3((PN + 255) / 256), dim3(256), 0, stream, PN, points3D, p.view,
-                       p.proj, p.W, p.H, p.grid_x, p.grid_y, ps.xy, pb.keys_unsorted, st.counts);
+                       p.proj, p.W, p.H, p.grid_x, p.grid_y, ps.xy, ps.t, pb.keys_unsorted, st.counts);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     size_t bytes = pb.sort_tmp_bytes;
     return rocprim::radix_sort_pairs<PointSortConfig>(pb.sort_tmp, bytes, pb.keys_unsorted, pb.keys,

@@ -61,6 +61,12 @@ def _load():
     L.gsr_sample_depth_forward.restype = i
     L.gsr_sample_depth_forward.argtypes = ([_ALLOC, vp] * 6 + [i] * 4 + [vp] * 4 + [f] + [vp] * 5 + [f] * 3 + [i]
                                            + [vp, vp, i, vp] + [ctypes.POINTER(i)] * 3)
+    L.gsr_integrate_forward.restype = i
+    L.gsr_integrate_forward.argtypes = ([_ALLOC, vp] * 6 + [i] * 4 + [vp] * 4 + [f] + [vp] * 6 + [f] * 3 + [i]
+                                        + [vp, vp, i, vp, ctypes.POINTER(i)])
+    L.gsr_evaluate_sdf_forward.restype = i
+    L.gsr_evaluate_sdf_forward.argtypes = ([_ALLOC, vp] * 6 + [i] * 4 + [vp] * 4 + [f] + [vp] * 6 + [f] * 3 + [i]
+                                           + [vp, vp, vp, i, vp, ctypes.POINTER(i)])
     L.gsr_sample_depth_backward.restype = i
     L.gsr_sample_depth_backward.argtypes = ([_ALLOC, vp] + [i] * 7 + [vp] * 4 + [f] + [vp] * 5 + [f] * 3
                                             + [vp] * 6 + [vp] * 2 + [vp] * 6 + [i, vp])
@@ -307,6 +313,63 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         with torch.cuda.device(means3D.device):
             _check(L.gsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(means3D.device)))
     return present
+
+
+def _point_query(fn, points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                 view2gaussian_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, kernel_size, image_height,
+                 image_width, campos, prefiltered, debug):
+    """IntegrateGaussiansToPointsCUDA / evaluateSDFfromSingleView
+    (DGR/rasterize_points.cu:279-457): outputs zero-filled (torch::full 0),
+    the scratch buffers are local to the call."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    if points3D.ndimension() != 2 or points3D.size(1) != 3:
+        raise RuntimeError("points3D must have dimensions (num_points, 3)")
+    L = _load()
+    PN, P = points3D.size(0), means3D.size(0)
+    dev = means3D.device
+    out0 = torch.zeros(PN, dtype=torch.float32, device=dev)
+    out1 = torch.zeros(PN, dtype=torch.float32, device=dev)
+    inside = torch.zeros(PN, dtype=torch.bool, device=dev)
+    K = ctypes.c_int(0)
+    if P != 0 and PN != 0:
+        a = {k: _dev_contig(v, k) for k, v in dict(
+            points3D=points3D, means3D=means3D, opacity=opacity, scales=scales, rotations=rotations,
+            cov3D_precomp=cov3D_precomp, view2gaussian_precomp=view2gaussian_precomp, viewmatrix=viewmatrix,
+            projmatrix=projmatrix, campos=campos).items()}
+        bufs = [_ByteBuffer(dev) for _ in range(6)]
+        head = [bufs[0].cb, None, bufs[1].cb, None, bufs[2].cb, None, bufs[3].cb, None, bufs[4].cb, None,
+                bufs[5].cb, None, PN, P, int(image_width), int(image_height), _ptr(a["points3D"]),
+                _ptr(a["means3D"]), _ptr(a["opacity"]), _ptr(a["scales"]), float(scale_modifier),
+                _ptr(a["rotations"]), _ptr(a["cov3D_precomp"]), _ptr(a["view2gaussian_precomp"]),
+                _ptr(a["viewmatrix"]), _ptr(a["projmatrix"]), _ptr(a["campos"]), float(tan_fovx), float(tan_fovy),
+                float(kernel_size), int(bool(prefiltered))]
+        outs = [_ptr(out0)] if fn == "integrate" else [_ptr(out0), _ptr(out1)]
+        with torch.cuda.device(dev):
+            entry = L.gsr_integrate_forward if fn == "integrate" else L.gsr_evaluate_sdf_forward
+            rc = entry(*head, *outs, _ptr(inside), int(bool(debug)), _stream(dev), ctypes.byref(K))
+        _check(rc)
+    return K.value, out0, out1, inside
+
+
+def integrate_gaussians_to_points(points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                                  view2gaussian_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, kernel_size,
+                                  image_height, image_width, campos, prefiltered, debug):
+    """-> (num_rendered, transmittance [PN], inside [PN] bool), rasterize_points.cu:279-366."""
+    K, T, _, inside = _point_query("integrate", points3D, means3D, opacity, scales, rotations, scale_modifier,
+                                   cov3D_precomp, view2gaussian_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy,
+                                   kernel_size, image_height, image_width, campos, prefiltered, debug)
+    return K, T, inside
+
+
+def evaluate_sdf_from_signle_view(points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                                  view2gaussian_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, kernel_size,
+                                  image_height, image_width, campos, prefiltered, debug):
+    """-> (num_rendered, depth [PN], sdf [PN], inside [PN] bool), rasterize_points.cu:368-457
+    (the reference's spelling of the binding name, DGR/ext.cpp)."""
+    return _point_query("sdf", points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        view2gaussian_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, kernel_size,
+                        image_height, image_width, campos, prefiltered, debug)
 
 
 def sample_rasterized_depth(points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,

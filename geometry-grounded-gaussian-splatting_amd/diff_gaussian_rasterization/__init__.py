@@ -10,10 +10,8 @@ GaussianRasterizer` (gaussian_renderer/__init__.py:14) works unchanged once
 this directory's parent is on sys.path.  The compute lives in libgsr.so
 (hand-written HIP for gfx950) behind `_C`.
 
+  GaussianRasterizer.integrate / evaluate_sdf (forward-only)  (:338-468)
   GaussianRasterizer.sample_depth + _SampleDepth (autograd.Function)  (:470-655)
-The other point-query entry points of the reference (integrate,
-evaluate_sdf, DGR/__init__.py:338-468) are later rows of the build
-(SURVEY.md §8(f)); they raise NotImplementedError here.
 """
 from __future__ import annotations
 
@@ -140,11 +138,53 @@ class GaussianRasterizer(nn.Module):
         return rasterize_gaussians(means3D, means2D, shs, sg_axis, sg_sharpness, sg_color, colors_precomp,
                                    opacities, scales, rotations, cov3D_precomp, raster_settings)
 
-    def integrate(self, *args, **kwargs):
-        raise NotImplementedError("integrate (DGR/__init__.py:338-380) is a next-round row (SURVEY.md §8(f))")
+    def _query_args(self, points3D, means3D, opacities, scales, rotations, cov3D_precomp, view2gaussian_precomp):
+        """Argument checks and the 18-argument tuple of DGR/__init__.py:349-388
+        (kernel size 0.0 as the reference, whatever the settings hold)."""
+        s = self.raster_settings
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or (
+                (scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        if scales is None:
+            scales = torch.Tensor([])
+        if rotations is None:
+            rotations = torch.Tensor([])
+        if cov3D_precomp is None:
+            cov3D_precomp = torch.Tensor([])
+        if view2gaussian_precomp is None:
+            view2gaussian_precomp = torch.Tensor([])
+        return (points3D, means3D, opacities, scales, rotations, s.scale_modifier, cov3D_precomp,
+                view2gaussian_precomp, s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, 0.0, s.image_height,
+                s.image_width, s.campos, s.prefiltered, s.debug)
 
-    def evaluate_sdf(self, *args, **kwargs):
-        raise NotImplementedError("evaluate_sdf (DGR/__init__.py:382-440) is a next-round row (SURVEY.md §8(f))")
+    def _query(self, fn, args):
+        if self.raster_settings.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                return fn(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_fw.dump")
+                print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
+                raise ex
+        return fn(*args)
+
+    def integrate(self, points3D, means3D, opacities, scales=None, rotations=None, cov3D_precomp=None,
+                  view2gaussian_precomp=None):
+        """Opacity of the Gaussian field at world points seen from this camera
+        (DGR/__init__.py:338-402): returns (1 - transmittance [PN], inside [PN])."""
+        args = self._query_args(points3D, means3D, opacities, scales, rotations, cov3D_precomp,
+                                view2gaussian_precomp)
+        num_rendered, transmittance, inside = self._query(_C.integrate_gaussians_to_points, args)
+        return 1 - transmittance, inside
+
+    def evaluate_sdf(self, points3D, means3D, opacities, scales=None, rotations=None, cov3D_precomp=None,
+                     view2gaussian_precomp=None):
+        """Median depth along each point's ray and its signed distance to the
+        point (DGR/__init__.py:404-468): returns (depth, sdf, inside), [PN] each."""
+        args = self._query_args(points3D, means3D, opacities, scales, rotations, cov3D_precomp,
+                                view2gaussian_precomp)
+        num_rendered, depth, sdf, inside = self._query(_C.evaluate_sdf_from_signle_view, args)
+        return depth, sdf, inside
 
     def sample_depth(self, points3D, means3D, opacities, scales=None, rotations=None, cov3D_precomp=None):
         """Median depth of the Gaussians at world points seen from this camera

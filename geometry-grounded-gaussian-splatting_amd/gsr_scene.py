@@ -225,3 +225,21 @@ def upstream_grads(H: int, W: int, seed: int = 1, scale: float = 1e-3) -> dict:
         alpha=torch.zeros(1, H, W),
         normal=torch.randn(3, H, W, generator=g) * scale,
     )
+
+
+def tetra_points(inp):
+    """GaussianModel.get_tetra_points (scene/gaussian_model.py:496-519): per
+    Gaussian the 8 corners of its box at 1.5 scale and 6 axis points at 3
+    scale, rotated, then every centre: 15 points per Gaussian, the point set
+    mesh_extract_tetrahedra.py:75 integrates."""
+    q = torch.nn.functional.normalize(inp["rotations"], dim=1)
+    r, x, y, z = q.unbind(1)
+    Rm = torch.stack([torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y)], 1),
+                      torch.stack([2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x)], 1),
+                      torch.stack([2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], 1)], 1)
+    near = [[sx * 1.5, sy * 1.5, sz * 1.5] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]
+    far = [[3, 0, 0], [0, 3, 0], [0, 0, 3], [-3, 0, 0], [0, -3, 0], [0, 0, -3]]
+    verts = torch.tensor(near + far, dtype=torch.float32, device=q.device)
+    local = verts[None] * inp["scales"][:, None]
+    corners = (local @ Rm.transpose(1, 2) + inp["means3D"][:, None]).reshape(-1, 3)
+    return torch.cat([corners, inp["means3D"]], 0).contiguous()

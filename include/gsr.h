@@ -133,6 +133,49 @@ int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
                              int* num_rendered, int* num_points, int* num_duplicated_tiles);
 
 /*
+ * integrate / evaluate_sdf: forward-only queries of the
+ * Gaussian field at PN world points, used by the offline tetrahedral mesh
+ * extraction (mesh_extract_tetrahedra.py:75, gaussian_renderer/__init__.py:
+ * 101-222).  Same six resize callbacks, arguments and point binning as
+ * gsr_sample_depth_forward; view2gaussian_precomp is accepted and ignored, as
+ * in the reference.  Outputs are written for the points that project into
+ * the image and left untouched for the others (callers pass zeroed buffers,
+ * as the reference's torch::full(0)).  Synchronises `stream` once.
+ *
+ * gsr_integrate_forward replaces CudaRasterizer::Rasterizer::
+ * evaluateTransmittance (rasterizer.h:111-138, rasterizer_impl.cu:594-815),
+ * bound as _C.integrate_gaussians_to_points (DGR/rasterize_points.cu:279-366):
+ * out_transmittance [PN] = the vacancy transmittance at each point's distance
+ * from the camera (sample_forward.cu:55-169), inside [PN] = 1.
+ *
+ * gsr_evaluate_sdf_forward replaces Rasterizer::evaluateSDF (rasterizer.h:
+ * 140-168, rasterizer_impl.cu:817-1040), bound as
+ * _C.evaluate_sdf_from_signle_view (rasterize_points.cu:368-457):
+ * out_depth [PN] = the median depth along the point's ray (+-0.8 first
+ * window, 6 bisection passes, sample_forward.cu:171-427), out_sdf [PN] =
+ * out_depth - |p_view|, inside [PN] = whether the median is defined.
+ */
+int gsr_integrate_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                          gsr_alloc_fn point_alloc, void* point_ctx, gsr_alloc_fn point_binning_alloc,
+                          void* point_binning_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                          gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P, int width, int height,
+                          const float* points3D, const float* means3D, const float* opacities, const float* scales,
+                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                          const float* view2gaussian_precomp, const float* viewmatrix, const float* projmatrix,
+                          const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
+                          float* out_transmittance, uint8_t* inside, int debug, void* stream, int* num_rendered);
+int gsr_evaluate_sdf_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn point_alloc, void* point_ctx, gsr_alloc_fn point_binning_alloc,
+                             void* point_binning_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                             gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P, int width, int height,
+                             const float* points3D, const float* means3D, const float* opacities,
+                             const float* scales, float scale_modifier, const float* rotations,
+                             const float* cov3D_precomp, const float* view2gaussian_precomp,
+                             const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                             float tan_fovy, float kernel_size, int prefiltered, float* out_depth, float* out_sdf,
+                             uint8_t* inside, int debug, void* stream, int* num_rendered);
+
+/*
  * Replaces CudaRasterizer::Rasterizer::sampleDepthBackward (rasterizer.h:197-233,
  * rasterizer_impl.cu:1247-1394), bound as _C.sample_rasterized_depth_backward
  * (rasterize_points.cu:555-633).  The six buffers are the forward's; R, RN, TN

@@ -79,6 +79,9 @@ def lib():
         L.gsro_sample_get_points.argtypes = [ctypes.c_void_p, _f, _u32, _u32, _f]
         L.gsro_warp_patch_ncc.argtypes = ([ctypes.c_int, _f, _f, _i, _f, _f, _f, _f] + [ctypes.c_float] * 8
                                           + [ctypes.c_int] * 4 + [_f, _f, _f, _u8])
+        L.gsro_point_query.restype = ctypes.c_int
+        L.gsro_point_query.argtypes = ([ctypes.c_int] * 5 + [_f] * 4 + [ctypes.c_float] + [_f] * 5
+                                       + [ctypes.c_float] * 3 + [_f, _f, _u8, _i])
         L.gsro_sample_gaussians.restype = ctypes.c_void_p
         L.gsro_sample_gaussians.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -331,6 +334,43 @@ def sample_forward(points3D, means3D, opacity, scales, rotations, scale_modifier
     st = SampleState(ptr, P, PN, W, H, K.value)
     return dict(num_rendered=K.value, num_points=RN.value, num_duplicated_tiles=TN.value, output=output,
                 inside=inside.astype(bool), state=st)
+
+
+def _point_query(mode, points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                 view2gaussian_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, kernel_size, image_height,
+                 image_width, campos, prefiltered, debug):
+    del view2gaussian_precomp, prefiltered, debug  # unused by the reference (rasterizer_impl.cu:594-1040)
+    L = lib()
+    pts = _np(points3D)
+    PN = 0 if pts is None else pts.size // 3
+    means3D = _np(means3D)
+    P = 0 if means3D is None else means3D.shape[0]
+    out0, out1 = np.zeros(PN, np.float32), np.zeros(PN, np.float32)
+    inside = np.zeros(PN, np.uint8)
+    K = ctypes.c_int(0)
+    if P and PN:
+        keep = [pts, means3D, _np(opacity), _np(scales), _np(rotations), _np(cov3D_precomp), _np(viewmatrix),
+                _np(projmatrix), _np(campos)]
+        rc = L.gsro_point_query(mode, PN, P, int(image_width), int(image_height), _p(keep[0]), _p(keep[1]),
+                                _p(keep[2]), _p(keep[3]), float(scale_modifier), _p(keep[4]), _p(keep[5]),
+                                _p(keep[6]), _p(keep[7]), _p(keep[8]), float(tan_fovx), float(tan_fovy),
+                                float(kernel_size), _p(out0), _p(out1), _p(inside, _u8), ctypes.byref(K))
+        if rc != 0:
+            raise RuntimeError(f"oracle point query failed: {rc}")
+    return K.value, out0, out1, inside.astype(bool)
+
+
+def integrate(*args):
+    """Same 18 arguments and return tuple as _C.integrate_gaussians_to_points
+    (DGR/rasterize_points.cu:279-366): (num_rendered, transmittance, inside)."""
+    K, T, _, inside = _point_query(0, *args)
+    return K, T, inside
+
+
+def evaluate_sdf(*args):
+    """Same 18 arguments and return tuple as _C.evaluate_sdf_from_signle_view
+    (DGR/rasterize_points.cu:368-457): (num_rendered, depth, sdf, inside)."""
+    return _point_query(1, *args)
 
 
 def sample_backward(state: SampleState, points3D, means3D, opacity, scales, rotations, scale_modifier,

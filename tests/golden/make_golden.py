@@ -18,6 +18,9 @@ reference's CUDA rasterizer, which cannot build in this image):
   boundary_sample.json  DGR/diff_gaussian_rasterization/__init__.py:470-655 —
                    the same for GaussianRasterizer.sample_depth / _SampleDepth
                    (_C.sample_rasterized_depth{,_backward}).
+  boundary_query.json   DGR/diff_gaussian_rasterization/__init__.py:338-468 —
+                   the same for GaussianRasterizer.integrate / evaluate_sdf
+                   (_C.integrate_gaussians_to_points, _C.evaluate_sdf_from_signle_view).
 """
 from __future__ import annotations
 
@@ -187,10 +190,23 @@ def boundary_fixture():
         shapes = [(P, 1), (P, 3), (P, 6), (P, 3), (P, 4), PTS]
         return tuple(torch.full(s, float(i + 1)) for i, s in enumerate(shapes))
 
+    qcalls = {}
+    QN = 9
+
+    def integrate_gaussians_to_points(*args):
+        qcalls["integrate"] = [describe(a) for a in args]
+        return (13, torch.full((QN,), 0.25), torch.ones(QN, dtype=torch.bool))
+
+    def evaluate_sdf_from_signle_view(*args):
+        qcalls["evaluate_sdf"] = [describe(a) for a in args]
+        return (13, torch.full((QN,), 2.5), torch.full((QN,), -0.5), torch.ones(QN, dtype=torch.bool))
+
     _stub("diff_gaussian_rasterization._C", rasterize_gaussians=rasterize_gaussians,
           rasterize_gaussians_backward=rasterize_gaussians_backward, mark_visible=mark_visible,
           sample_rasterized_depth=sample_rasterized_depth,
-          sample_rasterized_depth_backward=sample_rasterized_depth_backward)
+          sample_rasterized_depth_backward=sample_rasterized_depth_backward,
+          integrate_gaussians_to_points=integrate_gaussians_to_points,
+          evaluate_sdf_from_signle_view=evaluate_sdf_from_signle_view)
     pkg = types.ModuleType("diff_gaussian_rasterization")
     pkg.__path__ = [os.path.join(REF, "submodules/diff-gaussian-rasterization/diff_gaussian_rasterization")]
     sys.modules["diff_gaussian_rasterization"] = pkg
@@ -256,6 +272,28 @@ def boundary_fixture():
     scalls["settings_kernel_size"] = 0.1
     with open(os.path.join(OUT, "boundary_sample.json"), "w") as f:
         json.dump(scalls, f, indent=1)
+
+    # integrate / evaluate_sdf (DGR/__init__.py:338-468): forward-only queries
+    qin = dict(points3D=torch.zeros(QN, 3), means3D=torch.zeros(P, 3), opacities=torch.zeros(P, 1),
+               scales=torch.zeros(P, 3), rotations=torch.zeros(P, 4))
+    a, ins = rz.integrate(**qin)
+    qcalls["integrate_outputs"] = [describe(a), describe(ins), float(a[0])]
+    d, s, ins = rz.evaluate_sdf(**qin)
+    qcalls["evaluate_sdf_outputs"] = [describe(d), describe(s), describe(ins), float(d[0]), float(s[0])]
+    errs = {}
+    for fn in ("integrate", "evaluate_sdf"):
+        for name, kw in [("no_cov", dict(scales=None)), ("both_cov", dict(cov3D_precomp=torch.zeros(P, 6)))]:
+            args = dict(qin)
+            args.update(kw)
+            try:
+                getattr(rz, fn)(**args)
+                errs[fn + "_" + name] = None
+            except Exception as e:  # noqa: BLE001 - record the reference's behaviour
+                errs[fn + "_" + name] = type(e).__name__ + ": " + str(e)
+    qcalls["errors"] = errs
+    qcalls["settings_kernel_size"] = 0.1
+    with open(os.path.join(OUT, "boundary_query.json"), "w") as f:
+        json.dump(qcalls, f, indent=1)
 
 
 def main():

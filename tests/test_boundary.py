@@ -21,6 +21,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "boundary.json")))
 GOLD_SAMPLE = json.load(open(os.path.join(ROOT, "tests", "golden", "boundary_sample.json")))
+GOLD_QUERY = json.load(open(os.path.join(ROOT, "tests", "golden", "boundary_query.json")))
 
 
 def _describe(a):
@@ -147,6 +148,62 @@ def test_sample_depth_no_cpu_fallback():
         _C.sample_rasterized_depth(torch.zeros(4, 2), torch.zeros(2, 3), *([None] * 15))
 
 
+def test_point_queries_marshal_reference_tuples(monkeypatch):
+    """GaussianRasterizer.integrate / evaluate_sdf: the reference's 18-argument
+    _C tuples (kernel size 0.0 whatever the settings hold, an empty
+    view2gaussian_precomp), the returned values (integrate returns
+    1 - transmittance) and the argument errors (tests/golden/boundary_query.json,
+    DGR/__init__.py:338-468)."""
+    import diff_gaussian_rasterization as dgr
+
+    calls = {}
+    P, H, W, QN = 5, 8, 12, 9
+
+    def integ(*args):
+        calls["integrate"] = [_describe(a) for a in args]
+        return (13, torch.full((QN,), 0.25), torch.ones(QN, dtype=torch.bool))
+
+    def sdf(*args):
+        calls["evaluate_sdf"] = [_describe(a) for a in args]
+        return (13, torch.full((QN,), 2.5), torch.full((QN,), -0.5), torch.ones(QN, dtype=torch.bool))
+
+    monkeypatch.setattr(dgr._C, "integrate_gaussians_to_points", integ)
+    monkeypatch.setattr(dgr._C, "evaluate_sdf_from_signle_view", sdf)
+    settings = dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=0.5, tanfovy=0.4, kernel_size=GOLD_QUERY["settings_kernel_size"],
+        bg=torch.zeros(3), scale_modifier=1.0, viewmatrix=torch.eye(4), projmatrix=torch.eye(4), sh_degree=3,
+        sg_degree=1, campos=torch.zeros(3), prefiltered=False, require_depth=True, debug=False)
+    rz = dgr.GaussianRasterizer(settings)
+    qin = dict(points3D=torch.zeros(QN, 3), means3D=torch.zeros(P, 3), opacities=torch.zeros(P, 1),
+               scales=torch.zeros(P, 3), rotations=torch.zeros(P, 4))
+    a, ins = rz.integrate(**qin)
+    assert [_describe(a), _describe(ins), float(a[0])] == GOLD_QUERY["integrate_outputs"]
+    d, s, ins = rz.evaluate_sdf(**qin)
+    assert [_describe(d), _describe(s), _describe(ins), float(d[0]), float(s[0])] == GOLD_QUERY["evaluate_sdf_outputs"]
+    assert calls["integrate"] == GOLD_QUERY["integrate"]
+    assert calls["evaluate_sdf"] == GOLD_QUERY["evaluate_sdf"]
+    for fn in ("integrate", "evaluate_sdf"):
+        for name, kw in [("no_cov", dict(scales=None)), ("both_cov", dict(cov3D_precomp=torch.zeros(P, 6)))]:
+            args = dict(qin)
+            args.update(kw)
+            with pytest.raises(Exception) as ei:
+                getattr(rz, fn)(**args)
+            assert type(ei.value).__name__ + ": " + str(ei.value) == GOLD_QUERY["errors"][fn + "_" + name]
+
+
+def test_point_queries_no_cpu_fallback():
+    from diff_gaussian_rasterization import _C
+
+    args = (torch.zeros(4, 3), torch.zeros(2, 3), torch.zeros(2, 1), torch.ones(2, 3), torch.zeros(2, 4), 1.0,
+            torch.Tensor([]), torch.Tensor([]), torch.eye(4), torch.eye(4), 0.5, 0.5, 0.0, 8, 8, torch.zeros(3),
+            False, False)
+    for fn in (_C.integrate_gaussians_to_points, _C.evaluate_sdf_from_signle_view):
+        with pytest.raises(RuntimeError, match="HIP device tensor"):
+            fn(*args)
+        with pytest.raises(RuntimeError, match="points3D must have dimensions"):
+            fn(torch.zeros(4, 2), *args[1:])
+
+
 def test_library_exports_header_symbols():
     header = open(os.path.join(ROOT, "include", "gsr.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(gsr_\w+)\s*\(", header, re.M)))
@@ -157,7 +214,7 @@ def test_library_exports_header_symbols():
     for n in names:
         assert hasattr(lib, n), n
     lib.gsr_abi_version.restype = ctypes.c_int
-    assert lib.gsr_abi_version() == 5
+    assert lib.gsr_abi_version() == 6
     lib.gsr_stage_name.restype = ctypes.c_char_p
     assert lib.gsr_stage_name(5) == b"render_fwd"
 

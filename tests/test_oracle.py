@@ -414,6 +414,114 @@ def test_sample_depth_at_pixel_centres_equals_render():
     assert s["inside"].mean() > 0.995
 
 
+# ------------------------------------------------- integrate / evaluate_sdf
+def query_args(c, pts, cov3D=None):
+    """The 18-argument tuple of _C.integrate_gaussians_to_points /
+    evaluate_sdf_from_signle_view (DGR/__init__.py:369-388)."""
+    inp = c["inp"]
+    scales, rots = (inp["scales"], inp["rotations"]) if cov3D is None else (None, None)
+    return (pts, inp["means3D"], inp["opacities"], scales, rots, 1.0, cov3D, None, c["cam"].world_view_transform,
+            c["cam"].full_proj_transform, c["tanx"], c["tany"], 0.0, c["H"], c["W"], c["cam"].camera_center, False,
+            False)
+
+
+def _ref_pre(c):
+    cam = c["cam"]
+    inp = {k: v.double() for k, v in c["inp"].items()}
+    pre = R.preprocess(inp["means3D"], inp["scales"], inp["rotations"], inp["opacities"], inp["shs"],
+                       inp["sg_axis"], inp["sg_sharpness"], inp["sg_color"],
+                       torch.zeros(inp["means3D"].shape[0], 3, dtype=torch.float64), cam.world_view_transform.double(),
+                       cam.full_proj_transform.double(), cam.camera_center.double(), c["W"], c["H"], c["tanx"],
+                       c["tany"], 0.0, 3, 0)
+    lists, _ = R.binning(pre, c["W"], c["H"])
+    return pre, lists
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_integrate_matches_float64(seed):
+    """integrate (evaluateTransmittanceCUDA, sample_forward.cu:55-169) against
+    the float64 restatement: inside flags exact, transmittance <= 1e-5."""
+    c = Hh.small_case(P=150, W=40, H=32, seed=seed)
+    pts = sample_points(c, 400, seed + 20)
+    K, T, inside = O.integrate(*query_args(c, pts))
+    assert K > 0 and inside.sum() > 200
+    pre, lists = _ref_pre(c)
+    cam = c["cam"]
+    ref = R.integrate(pre, lists, pts.double(), cam.world_view_transform.double(), cam.full_proj_transform.double(),
+                      c["W"], c["H"])
+    assert np.array_equal(inside, ref["inside"].numpy())
+    assert (T[~inside] == 0).all()  # culled points keep torch::full(0) (rasterize_points.cu:314)
+    Tr = ref["transmittance"].numpy()
+    assert 0.05 < Tr[inside].mean() < 0.95  # the scene occludes a fair share of the points
+    assert np.abs(T - Tr).max() <= 1e-5, np.abs(T - Tr).max()
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_evaluate_sdf_matches_float64(seed):
+    """evaluate_sdf (evaluateSDFCUDA, sample_forward.cu:171-427: a +-0.8 first
+    window and 6 bisection passes) against the float64 restatement: inside
+    exact, depth <= 5e-5 relative, sdf = depth - |p_view|."""
+    c = Hh.small_case(P=150, W=40, H=32, seed=seed)
+    pts = sample_points(c, 400, seed + 30)
+    K, depth, sdf, inside = O.evaluate_sdf(*query_args(c, pts))
+    assert inside.sum() > 50
+    pre, lists = _ref_pre(c)
+    cam = c["cam"]
+    out = R.sample(pre, lists, pts.double(), cam.world_view_transform.double(), cam.full_proj_transform.double(),
+                   c["W"], c["H"], iters=6, sample_range=0.8)
+    assert np.array_equal(inside, out["inside"].numpy())
+    md = out["mdepth"].numpy()
+    assert Hh.rel_err(depth, md) < 5e-5
+    dist = R.point_distance(pts.double(), cam.world_view_transform.double()).numpy()
+    in_view = out["tile"].numpy() >= 0
+    ref_sdf = np.where(in_view, md - dist, 0.0)
+    assert np.abs(sdf - ref_sdf).max() <= 5e-5 * np.abs(md).max()
+    # the 6-pass +-0.8 search differs from sample_depth's 5-pass +-0.4 one
+    s = O.sample_forward(*sample_args(c, pts))
+    assert not np.array_equal(s["inside"], inside) or Hh.rel_err(depth, s["state"].points()["median_depth"]) > 0
+
+
+def test_point_queries_against_render():
+    """Known answers linking the queries to the render path: a point on a
+    pixel centre's ray far behind every Gaussian (g = 0 for all of them) has
+    integrate's transmittance = the render's 1 - alpha; a point at the
+    rendered median depth has |sdf| ~ 0 where the median is defined."""
+    c = Hh.small_case(P=300, W=64, H=48, seed=1)
+    o = O.forward(*Hh.oracle_args(c))
+    md, alpha = o["mdepth"][0], o["alpha"][0]
+    W, H = c["W"], c["H"]
+    fx, fy = W / (2 * c["tanx"]), H / (2 * c["tany"])
+    ys, xs = np.mgrid[1:H - 1, 1:W - 1]
+    ys, xs = ys.ravel(), xs.ravel()
+    V = c["cam"].world_view_transform
+
+    def world(z):
+        z = torch.as_tensor(z, dtype=torch.float32)
+        cam_pts = torch.stack([(torch.tensor(xs, dtype=torch.float32) - (W - 1) / 2) / fx * z,
+                               (torch.tensor(ys, dtype=torch.float32) - (H - 1) / 2) / fy * z, z], 1)
+        return ((cam_pts - V[3, :3]) @ torch.linalg.inv(V[:3, :3])).float().contiguous()
+
+    K, T, inside = O.integrate(*query_args(c, world(np.full(xs.shape, 60.0))))
+    assert inside.all()
+    assert np.abs((1 - T) - alpha[ys, xs]).max() <= 1e-4
+    sel = md[ys, xs] > 0
+    z = np.where(sel, md[ys, xs], 3.0)
+    K, depth, sdf, inside = O.evaluate_sdf(*query_args(c, world(z)))
+    ok = sel & inside
+    assert ok.mean() > 0.5
+    # both bisections bracket the same root of T(t) = 1/2 (measured: 99th percentile 1.2e-6 at depth 2.5)
+    assert np.percentile(np.abs(sdf[ok]), 99) <= 1e-4 * np.median(md[ys, xs][ok])
+
+
+def test_point_queries_degenerate():
+    c = Hh.small_case(P=50, W=40, H=32, seed=3)
+    K, T, inside = O.integrate(*query_args(c, torch.zeros(0, 3)))
+    assert K == 0 and T.shape == (0,) and inside.shape == (0,)
+    pts = torch.tensor([[0.0, 0.0, -5.0], [100.0, 0.0, 3.0]])  # behind the camera / outside the image
+    K, depth, sdf, inside = O.evaluate_sdf(*query_args(c, pts))
+    assert not inside.any() and (depth == 0).all() and (sdf == 0).all()
+
+
 # ---------------------------------------------------------- warp_patch_ncc
 def ncc_case(P, seed, Wr=48, Hr=40, Wn=52, Hn=44):
     """Two smooth textured images, a relative pose (r to n) and random

@@ -465,6 +465,63 @@ def sample(pre, lists, points3D, view, proj, W, H, split=8, iters=5, sample_rang
                 n_contrib=last_all, tile=tile, _terms=terms, _pn=(pnx.detach(), pny.detach(), rln.detach()))
 
 
+def point_distance(points3D, view):
+    """|p_view| of world points (preprocessPointsCUDA ts, sample_forward.cu:50)."""
+    pts = points3D.reshape(-1, 3)
+    t = pts @ view[:3, :3] + view[3, :3]
+    return torch.sqrt((t * t).sum(1))
+
+
+def integrate(pre, lists, points3D, view, proj, W, H):
+    """Vacancy transmittance of the Gaussian field at world points
+    (evaluateTransmittanceCUDA, sample_forward.cu:55-169), float64, no
+    gradient: per point the tile's list front to back, the composite's
+    power / alpha / early-stop tests, and per blended Gaussian
+    T_point *= (t > t_peak ? 1 - a : 1 - a g) / sqrt(1 - a g),
+    g = exp(-((t_peak - t) rsigma)^2 / 2) (0 for rsigma <= 0)."""
+    dt = pre["xy"].dtype
+    pts = points3D.reshape(-1, 3).to(dt)
+    N = pts.shape[0]
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    tv = pts @ view[:3, :3] + view[3, :3]
+    p_hom = pts @ proj[:3] + proj[3]
+    ndc = p_hom[:, :2] / (p_hom[:, 3:4] + 1e-7)
+    xy = torch.stack([((ndc[:, 0] + 1.0) * W - 1.0) * 0.5, ((ndc[:, 1] + 1.0) * H - 1.0) * 0.5], 1)
+    valid = (tv[:, 2] > 0.2) & (xy[:, 0] >= 0) & (xy[:, 0] <= W - 1) & (xy[:, 1] >= 0) & (xy[:, 1] <= H - 1)
+    tx = torch.clamp(((xy[:, 0] + 0.5) / 16).floor().long(), 0, gx - 1)
+    ty = torch.clamp(((xy[:, 1] + 0.5) / 16).floor().long(), 0, gy - 1)
+    tile = torch.where(valid, ty * gx + tx, torch.full_like(tx, -1))
+    pt_t = torch.sqrt((tv * tv).sum(1))
+    T_out = torch.zeros(N, dtype=dt)
+    with torch.no_grad():
+        for tl in torch.unique(tile[tile >= 0]).tolist():
+            idx = torch.nonzero(tile == tl)[:, 0]
+            pxy, tpt = xy[idx], pt_t[idx]
+            n = idx.shape[0]
+            T = torch.ones(n, dtype=dt)
+            Tp = torch.ones(n, dtype=dt)
+            done = torch.zeros(n, dtype=torch.bool)
+            for g in lists[tl]:
+                d = pre["xy"][g][None] - pxy
+                co = pre["conic"][g]
+                power = -0.5 * (co[0] * d[:, 0] ** 2 + co[2] * d[:, 1] ** 2) - co[1] * d[:, 0] * d[:, 1]
+                al = torch.clamp(pre["opac"][g] * torch.exp(power), max=0.99)
+                ok = (~done) & (power <= 0) & (al >= 1.0 / 255.0)
+                test_T = T * (1 - al)
+                stop = ok & (test_T < 1e-4)
+                done = done | stop
+                ok = ok & ~stop
+                rp = pre["ray_plane"][g]
+                tp = rp[0] * d[:, 0] + rp[1] * d[:, 1] + rp[2]
+                gg = torch.exp(-0.5 * ((tp - tpt) * rp[3]) ** 2) if float(rp[3]) > 0 else torch.zeros_like(tp)
+                omg = 1 - al * gg
+                f = torch.where(tpt > tp, 1 - al, omg) / torch.sqrt(omg)
+                Tp = torch.where(ok, Tp * f, Tp)
+                T = torch.where(ok, test_T, T)
+            T_out[idx] = Tp
+    return dict(transmittance=T_out, inside=tile >= 0, tile=tile)
+
+
 def sample_surrogate(out, dL_doutput):
     """Scalar whose gradient is the reference's implicit median-depth gradient
     of the sampled points (sample_backward.cu:138-215, 289-301)."""
