@@ -862,6 +862,19 @@ int gsr_depth_to_normal_backward(const float* depth, int H, int W, float Fx, flo
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "depth_to_normal backward", e);
 }
 
+int gsr_knn_mean_dist(gsr_alloc_fn scratch_alloc, void* scratch_ctx, int P, const float* points,
+                      float* mean_dists, void* stream_ptr) {
+    if (P < 0) return fail(GSR_ERR_ARGS, "distCUDA2: P < 0");
+    if (P == 0) return GSR_OK;
+    if (!points || !mean_dists || !scratch_alloc) return fail(GSR_ERR_ARGS, "distCUDA2: missing buffer");
+    KnnState ks;
+    void* buf = scratch_alloc(scratch_ctx, carve_knn(nullptr, P, ks));
+    if (!buf) return fail(GSR_ERR_ALLOC, "distCUDA2: scratch allocation failed");
+    carve_knn(aligned_base(buf), P, ks);
+    hipError_t e = launch_knn(P, points, ks, mean_dists, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "distCUDA2", e);
+}
+
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream_ptr) {
     (void)projmatrix;

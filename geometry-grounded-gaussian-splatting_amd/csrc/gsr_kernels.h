@@ -173,4 +173,19 @@ hipError_t launch_depth_normal(bool backward, const float* depth, int H, int W, 
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t stream);
 
+// distCUDA2 (knn.hip): scratch carved from one caller buffer
+struct KnnState {
+    float* partials;
+    float* bounds;
+    uint32_t* codes;
+    uint32_t* codes_sorted;
+    uint32_t* order;
+    float4* sorted;
+    float4* boxes;
+    char* sort_tmp;
+    size_t sort_tmp_bytes;
+};
+size_t carve_knn(void* base, int P, KnnState& s);
+hipError_t launch_knn(int P, const float* pts, const KnnState& s, float* mean_dists, hipStream_t stream);
+
 }  // namespace gsr

@@ -275,6 +275,18 @@ int gsr_depth_to_normal_backward(const float* depth, int H, int W, float Fx, flo
                                  const float* dL_dnormal, float* dL_ddepth, void* stream);
 
 /*
+ * Initial scales: replaces distCUDA2 / SimpleKNN::knn
+ * (submodules/simple-knn/spatial.cu:15-25, simple_knn.cu:175-220), bound as
+ * simple_knn._C.distCUDA2 (scene/gaussian_model.py:20, 323).  points [P,3]
+ * fp32; mean_dists [P] = the mean of the squared distances to the 3 nearest
+ * other points (inf / FLT_MAX-based values when P < 4, as the reference).
+ * scratch_alloc is called once (about 48 B per point plus the sort's
+ * temporary).  No host synchronisation.
+ */
+int gsr_knn_mean_dist(gsr_alloc_fn scratch_alloc, void* scratch_ctx, int P, const float* points, float* mean_dists,
+                      void* stream);
+
+/*
  * Per-stage GPU timing (no reference equivalent; SURVEY §5 "tracing").  While
  * enabled, every kernel stage of the calls above is bracketed by two hipEvents
  * on the call's stream.  gsr_timing_collect() waits for the recorded events,

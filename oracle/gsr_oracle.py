@@ -82,6 +82,8 @@ def lib():
         L.gsro_point_query.restype = ctypes.c_int
         L.gsro_point_query.argtypes = ([ctypes.c_int] * 5 + [_f] * 4 + [ctypes.c_float] + [_f] * 5
                                        + [ctypes.c_float] * 3 + [_f, _f, _u8, _i])
+        L.gsro_knn_mean_dist.restype = ctypes.c_int
+        L.gsro_knn_mean_dist.argtypes = [ctypes.c_int, _f, _f, _u32]
         L.gsro_sample_gaussians.restype = ctypes.c_void_p
         L.gsro_sample_gaussians.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -420,3 +422,15 @@ def warp_patch_ncc(depths, normals, uvs, R, T, image_r, image_n, fx_r, fy_r, cx_
                               _p(out["ncc"]), _p(out["grad_depths"]), _p(out["grad_normals"]), _p(out["valid"], _u8))
     out["valid"] = out["valid"].astype(bool)
     return out
+
+
+def knn_mean_dist(points):
+    """distCUDA2 (submodules/simple-knn/spatial.cu:15-25): [P] mean squared
+    distance to the 3 nearest other points.  Returns (dists, Morton order)."""
+    pts = np.ascontiguousarray(_np(points), np.float32).reshape(-1, 3)
+    P = pts.shape[0]
+    out = np.zeros(P, np.float32)
+    order = np.zeros(P, np.uint32)
+    if P:
+        lib().gsro_knn_mean_dist(P, _p(pts), _p(out), _p(order, _u32))
+    return out, order

@@ -204,6 +204,15 @@ def test_point_queries_no_cpu_fallback():
             fn(torch.zeros(4, 2), *args[1:])
 
 
+def test_distcuda2_no_cpu_fallback():
+    """simple_knn._C.distCUDA2 (scene/gaussian_model.py:20) resolves to gsr
+    and refuses CPU tensors."""
+    from simple_knn._C import distCUDA2
+
+    with pytest.raises(RuntimeError, match="HIP device tensor"):
+        distCUDA2(torch.zeros(8, 3))
+
+
 def test_library_exports_header_symbols():
     header = open(os.path.join(ROOT, "include", "gsr.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(gsr_\w+)\s*\(", header, re.M)))

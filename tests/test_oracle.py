@@ -522,6 +522,37 @@ def test_point_queries_degenerate():
     assert not inside.any() and (depth == 0).all() and (sdf == 0).all()
 
 
+# ------------------------------------------------------------ simple_knn
+@pytest.mark.parametrize("P", [4, 5, 1000, 1023, 1025, 30000])
+def test_knn_matches_exact_kdtree(P):
+    """distCUDA2 restatement (submodules/simple-knn/simple_knn.cu:44-220):
+    the mean squared distance to the 3 nearest other points equals scipy's
+    exact k-d tree in float64 (the box pruning never drops a neighbour)."""
+    from scipy.spatial import cKDTree
+
+    rng = np.random.default_rng(P)
+    pts = rng.normal(size=(P, 3)).astype(np.float32)
+    pts[P // 2:] *= 0.01  # two scales
+    got, order = O.knn_mean_dist(pts)
+    d, _ = cKDTree(pts.astype(np.float64)).query(pts.astype(np.float64), k=4)
+    ref = (d[:, 1:] ** 2).mean(1)
+    assert np.abs(got - ref).max() <= 1e-6 * ref.max()
+    assert np.all(np.abs(got - ref) <= 1e-5 * ref + 1e-30)
+    assert sorted(order.tolist()) == list(range(P))
+
+
+def test_knn_small_counts_follow_reference():
+    """P < 4: the missing neighbours stay FLT_MAX in the sum (simple_knn.cu:146,
+    172): P = 1, 2 give inf (FLT_MAX + FLT_MAX overflows), P = 3 gives
+    (d1 + d2 + FLT_MAX) / 3."""
+    got, _ = O.knn_mean_dist(np.array([[0, 0, 0]], np.float32))
+    assert np.isinf(got).all()
+    got, _ = O.knn_mean_dist(np.array([[0, 0, 0], [1, 0, 0]], np.float32))
+    assert np.isinf(got).all()
+    got, _ = O.knn_mean_dist(np.array([[0, 0, 0], [1, 0, 0], [0, 2, 0]], np.float32))
+    assert np.allclose(got, np.float32(np.finfo(np.float32).max) / np.float32(3), rtol=1e-6)
+
+
 # ---------------------------------------------------------- warp_patch_ncc
 def ncc_case(P, seed, Wr=48, Hr=40, Wn=52, Hn=44):
     """Two smooth textured images, a relative pose (r to n) and random
