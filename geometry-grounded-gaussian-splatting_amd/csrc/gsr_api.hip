@@ -20,6 +20,37 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// The forward's one host synchronisation (K sizes the binning buffer, as
+// rasterizer_impl.cu:384) waits on an event recorded right after the counts
+// are copied into pinned host memory, not on the whole stream: work queued
+// behind the event (the depth sort) keeps the GPU busy while the host reads
+// K and allocates.  Per thread and device.
+struct HostReadback {
+    int device = -1;
+    uint32_t* pinned = nullptr;  // 8 words
+    hipEvent_t ev = nullptr;
+};
+thread_local HostReadback g_readback;
+
+hipError_t readback_slot(HostReadback*& rb) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    rb = &g_readback;
+    if (rb->device == dev) return hipSuccess;
+    if (rb->ev) (void)hipEventDestroy(rb->ev);
+    if (rb->pinned) (void)hipHostFree(rb->pinned);
+    rb->ev = nullptr;
+    rb->pinned = nullptr;
+    rb->device = -1;
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&rb->pinned), 8 * sizeof(uint32_t), hipHostMallocDefault)) !=
+        hipSuccess)
+        return e;
+    if ((e = hipEventCreateWithFlags(&rb->ev, hipEventDisableTiming)) != hipSuccess) return e;
+    rb->device = dev;
+    return hipSuccess;
+}
+
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
     char buf[512];
     if (e != hipSuccess)
@@ -436,16 +467,22 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     // also needs K_live, the instances that survive tile culling.
     uint2 Ks = make_uint2(0u, 0u);
     if (lists) {
-        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        // K depends on preprocess only: read it back while the depth sort runs
+        HostReadback* rb = nullptr;
+        GSR_TRY(readback_slot(rb), "pinned readback buffer");
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
-        GSR_TRY(hipMemcpyAsync(&Ks.x, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
+        GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
+        GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
+        Ks.x = rb->pinned[0];
     } else {
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_live_counts(p, gs, radii, stream), "live counts");
         GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
         GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
     }
-    {
+    if (!lists) {
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
     }
@@ -600,22 +637,31 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, gs.radii, stream), "preprocess");
     const bool lists = list_binning(p.grid_x, p.grid_y);
     uint2 Ks = make_uint2(0u, 0u);
-    GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+    uint32_t totals[4] = {0, 0, 0, 0};
     if (lists) {
+        // K and the point totals depend on preprocess and the points only:
+        // read them back while the depth sort runs (HostReadback)
+        HostReadback* rb = nullptr;
+        GSR_TRY(readback_slot(rb), "pinned readback buffer");
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
+        GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_points(p, PN, points3D, ps, pb, st, stream), "sample points");
+        GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_setup(PN, tiles, pb, st, stream), "sample setup");
+        GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
+        GSR_TRY(hipMemcpyAsync(rb->pinned + 4, st.totals, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
+                "memcpy totals");
+        GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
+        Ks.x = rb->pinned[0];
+        for (int k = 0; k < 4; k++) totals[k] = rb->pinned[4 + k];
     } else {
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_live_counts(p, gs, gs.radii, stream), "live counts");
         GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
-    }
-    GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_points(p, PN, points3D, ps, pb, st, stream), "sample points");
-    GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_setup(PN, tiles, pb, st, stream), "sample setup");
-    uint32_t totals[4] = {0, 0, 0, 0};
-    if (lists)
-        GSR_TRY(hipMemcpyAsync(&Ks.x, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
-    else
+        GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_points(p, PN, points3D, ps, pb, st, stream), "sample points");
+        GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_setup(PN, tiles, pb, st, stream), "sample setup");
         GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
-    GSR_TRY(hipMemcpyAsync(totals, st.totals, sizeof(totals), hipMemcpyDeviceToHost, stream), "memcpy totals");
-    {
+        GSR_TRY(hipMemcpyAsync(totals, st.totals, sizeof(totals), hipMemcpyDeviceToHost, stream), "memcpy totals");
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
     }
