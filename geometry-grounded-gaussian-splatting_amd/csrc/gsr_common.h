@@ -111,6 +111,7 @@ constexpr uint32_t kNoCache = 0x7fffffffu;
 struct TileState {
     uint2* ranges;
     uint32_t* max_contrib;
+    uint32_t* order;  // launch order of the tiles, heaviest first (tile_order_kernel)
 };
 // ---- sample_depth state (PointState / DuplicatedTileState, rasterizer_impl.h) ----
 constexpr uint32_t kNoTile = 0xffffffffu;
@@ -143,6 +144,7 @@ struct ChunkState {  // duplicated-tile buffer: one entry per 256-point chunk
 struct BwdState {
     float* acc;      // [P][16]
     float* acc_abs;  // [P]
+    uint32_t* tile_order;  // [tiles] backward launch order, heaviest first
 };
 
 // --------------------------------------------------------------------------

@@ -8,7 +8,7 @@ namespace gsr {
 
 // Run-time switches for A/B variants of one kernel in one process
 // (gsr_set_option in include/gsr.h); defaults are the shipped paths.
-enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kNumOptions = 8 };
+enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kNumOptions = 8 };
 int option(int which);
 hipError_t read_render_stats(unsigned long long* out, bool reset);
 
@@ -187,5 +187,12 @@ struct KnnState {
 };
 size_t carve_knn(void* base, int P, KnnState& s);
 hipError_t launch_knn(int P, const float* pts, const KnnState& s, float* mean_dists, hipStream_t stream);
+
+// Launch order of the per-tile raster kernels, heaviest tile first (longest-
+// processing-time-first list scheduling: the tail of a launch is then made
+// of short tiles).  Cost = the tile's list length (ranges, forward) or its
+// max contributor (backward); one 1024-lane workgroup.
+hipError_t launch_tile_order(uint32_t num_tiles, const uint2* ranges, const uint32_t* max_contrib, uint32_t* order,
+                             hipStream_t stream);
 
 }  // namespace gsr

@@ -40,6 +40,7 @@ struct RenderBwdArgs {
     float* acc;      // [P][16]
     float* acc_abs;  // [P]
     int skip_prepass;  // diagnostic (GSR_OPT_BWD_NO_PREPASS): time the kernel without the pre-pass
+    const uint32_t* tile_order;  // [tiles] launch order (heaviest first) or null: XCD-contiguous
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -119,7 +120,7 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const uint32_t tile = xcd_remap(blockIdx.x, a.num_tiles);
+    const uint32_t tile = a.tile_order ? a.tile_order[blockIdx.x] : xcd_remap(blockIdx.x, a.num_tiles);
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
     const uint2 range = a.ranges[tile];
     const int max_contrib = (int)a.max_contrib[tile];
@@ -352,6 +353,7 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.acc = ws.acc;
     a.acc_abs = ws.acc_abs;
     a.skip_prepass = option(kOptBwdNoPrepass);
+    a.tile_order = ws.tile_order;
     if (a.num_tiles == 0) return hipSuccess;
     if (p.require_depth)
         hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(a.num_tiles), dim3(kBwdThreads), 0, stream, a);

@@ -76,6 +76,7 @@ struct RenderFwdArgs {
     float* pt_dT;               // [PN] dT/dt_m at pt_mdepth (valid where pt_cached)
     uint8_t* pt_cached;         // [PN]
     uint32_t* chunk_max;        // [chunks] max contributor of the chunk
+    const uint32_t* tile_order; // [tiles] launch order (heaviest first) or null: XCD-contiguous
 };
 
 // One contributor's factor on the bisection samples (render_forward.cu:610-621):
@@ -202,7 +203,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         pixy = xy.y;
         if constexpr (!GEOM) pt_t = inside ? a.pt_t[pid] : 0.f;
     } else {
-        tile = xcd_remap(blockIdx.x, a.num_tiles);
+        tile = a.tile_order ? a.tile_order[blockIdx.x] : xcd_remap(blockIdx.x, a.num_tiles);
         const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
         px = tx * kTile + (tid & 15);
         py = ty * kTile + (tid >> 4);
@@ -605,6 +606,7 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.dT_dtm = is.dT_dtm;
     a.md_check = is.md_check;
     a.max_contrib = ts.max_contrib;
+    a.tile_order = ts.order;
     a.out_color = out_color;
     a.out_alpha = out_alpha;
     a.out_normal = out_normal;
@@ -668,6 +670,51 @@ hipError_t launch_point_fwd(int query, const FwdParams& p, const GeomState& gs, 
     else
         hipLaunchKernelGGL((render_fwd_kernel<true, false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,
                            stream, a);
+    return hipGetLastError();
+}
+
+// LPT order: the tiles bucketed by cost (1024 buckets over [0, max cost]),
+// heaviest bucket first.  The order within a bucket is whatever the LDS
+// atomics give: a tile's outputs do not depend on when it runs.
+__global__ void __launch_bounds__(1024) tile_order_kernel(uint32_t n, const uint2* __restrict__ ranges,
+                                                          const uint32_t* __restrict__ max_contrib,
+                                                          uint32_t* __restrict__ order) {
+    constexpr uint32_t kB = 1024;
+    __shared__ uint32_t s_cnt[kB];
+    __shared__ uint32_t s_max[kB / 64];
+    const uint32_t tid = threadIdx.x;
+    auto cost = [&](uint32_t t) { return ranges ? ranges[t].y - ranges[t].x : max_contrib[t]; };
+    uint32_t m = 0;
+    for (uint32_t t = tid; t < n; t += kB) m = max(m, cost(t));
+    m = wave_max_u(m);
+    if ((tid & 63) == 0) s_max[tid >> 6] = m;
+    s_cnt[tid] = 0u;
+    __syncthreads();
+    m = 0;
+    for (uint32_t w = 0; w < kB / 64; w++) m = max(m, s_max[w]);
+    const unsigned long long scale = (unsigned long long)m + 1ull;
+    auto bucket = [&](uint32_t c) { return kB - 1u - (uint32_t)(((unsigned long long)c * kB) / scale); };
+    for (uint32_t t = tid; t < n; t += kB) atomicAdd(&s_cnt[bucket(cost(t))], 1u);
+    __syncthreads();
+    // exclusive scan of the bucket counts (Hillis-Steele in LDS)
+    const uint32_t own = s_cnt[tid];
+    uint32_t v = own;
+    for (uint32_t o = 1; o < kB; o <<= 1) {
+        const uint32_t u = tid >= o ? s_cnt[tid - o] : 0u;
+        __syncthreads();
+        v += u;
+        s_cnt[tid] = v;
+        __syncthreads();
+    }
+    s_cnt[tid] = v - own;
+    __syncthreads();
+    for (uint32_t t = tid; t < n; t += kB) order[atomicAdd(&s_cnt[bucket(cost(t))], 1u)] = t;
+}
+
+hipError_t launch_tile_order(uint32_t num_tiles, const uint2* ranges, const uint32_t* max_contrib, uint32_t* order,
+                             hipStream_t stream) {
+    if (num_tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, num_tiles, ranges, max_contrib, order);
     return hipGetLastError();
 }
 

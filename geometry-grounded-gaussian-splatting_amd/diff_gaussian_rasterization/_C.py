@@ -105,6 +105,7 @@ OPT_BISECT_SKIP = 0
 OPT_RENDER_STATS = 1
 OPT_BISECT_PASSES = 2
 OPT_BWD_NO_PREPASS = 3
+OPT_NO_TILE_ORDER = 4
 
 
 def debug_render_stats(reset: bool = True) -> list:

@@ -324,13 +324,16 @@ const char* gsr_stage_name(int stage);
  */
 /* GSR_OPT_BISECT_PASSES (diagnostic, default 0 = all 5): run only n median-depth
  * bisection passes (n < 0: none) to time them; median depth is then wrong. */
+/* GSR_OPT_NO_TILE_ORDER (A/B, default 0): launch the per-tile raster kernels in
+ * XCD-contiguous tile order instead of heaviest-tile-first (backward). */
 /* GSR_OPT_BWD_NO_PREPASS (diagnostic): skip the backward's median-depth pre-pass
  * (its gradient terms are then wrong), to time it. */
 enum gsr_option {
     GSR_OPT_BISECT_SKIP = 0,
     GSR_OPT_RENDER_STATS = 1,
     GSR_OPT_BISECT_PASSES = 2,
-    GSR_OPT_BWD_NO_PREPASS = 3
+    GSR_OPT_BWD_NO_PREPASS = 3,
+    GSR_OPT_NO_TILE_ORDER = 4
 };
 int gsr_set_option(int opt, int value);
 /* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (8 values, see render_fwd.hip). */
