@@ -32,8 +32,14 @@
 
 namespace gsr {
 
-constexpr int kRowSeg = 256;   // Gaussians per row-pass segment
-constexpr int kTileSeg = 512;  // row entries per tile-pass segment
+#ifndef GSR_ROW_SEG
+#define GSR_ROW_SEG 128  // measured at C3: 0.29 ms tile_lists vs 0.31 (256), 0.39 (512)
+#endif
+#ifndef GSR_TILE_SEG
+#define GSR_TILE_SEG 512
+#endif
+constexpr int kRowSeg = GSR_ROW_SEG;    // Gaussians per row-pass segment
+constexpr int kTileSeg = GSR_TILE_SEG;  // row entries per tile-pass segment
 
 bool list_binning(uint32_t gx, uint32_t gy) { return gx <= (uint32_t)kMaxGrid && gy <= (uint32_t)kMaxGrid; }
 

@@ -30,7 +30,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgsr.so")
+LIB_PATH = os.environ.get("GSR_LIB") or os.path.join(_HERE, "libgsr.so")  # GSR_LIB: development A/B builds
 
 _ALLOC = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 _lib = None
