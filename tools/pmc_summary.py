@@ -40,6 +40,8 @@ def stage_of(name: str) -> str | None:
         return "render_fwd"
     if "render_bwd_kernel" in n:
         return "render_bwd"
+    if "tile_order_kernel" in n:
+        return "bwd_clear"
     if "gather_counts_kernel" in n or "live_tiles_kernel" in n:
         return "depth_order"
     if "radix_sort" in n or "onesweep" in n or "merge_sort" in n:
@@ -76,7 +78,7 @@ def launches(path: str, counter: str) -> dict:
     bwd = calls.get("preprocess_bwd", 1)
     out = {}
     for k in calls:
-        out[k] = bwd if k in ("render_bwd", "preprocess_bwd") else fwd
+        out[k] = bwd if k in ("render_bwd", "preprocess_bwd", "bwd_clear") else fwd
     return out
 
 
@@ -115,7 +117,7 @@ def main():
             ncalls_trace["bwd"] += 1
     for st, lst in dur.items():
         lst.sort()
-        n = ncalls_trace["bwd" if st in ("render_bwd", "preprocess_bwd") else "fwd"]
+        n = ncalls_trace["bwd" if st in ("render_bwd", "preprocess_bwd", "bwd_clear") else "fwd"]
         per_call = max(1, len(lst) // max(1, n))
         calls = [sum(d for _, d in lst[i:i + per_call]) for i in range(0, len(lst), per_call)]
         calls.sort()
