@@ -680,7 +680,7 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, bs));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
     carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, bs);
-    ChunkState cs;
+    ChunkState cs{};
     void* cbuf = dup_tile_alloc(dup_tile_ctx, carve_chunks(nullptr, n_chunks, cs));
     if (!cbuf) return fail(GSR_ERR_ALLOC, "duplicated-tile buffer allocation failed");
     carve_chunks(aligned_base(cbuf), n_chunks, cs);
@@ -692,6 +692,8 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
         GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K_live, tile_bits, stream), "sort");
         GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K_live, ts, (int)tiles, stream), "tile ranges");
     }
+    // (heaviest-first chunk order with the tile's list length as the cost
+    // was measured for this forward: no change, 1.52 vs 1.51 ms at 1.27M points)
     GSR_STAGE(GSR_STAGE_SAMPLE_FWD,
               launch_point_fwd(query, p, gs, bs, ts, ps, pb, st, cs, n_chunks, output, output2, inside, stream),
               "point query");
@@ -807,12 +809,18 @@ int gsr_sample_depth_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
         cs.chunk_max = c.take<uint32_t>(1);  // first in the buffer (carve_chunks)
     }
     BwdState ws{};
-    const size_t wbytes = carve_bwd(nullptr, P, ws);
+    const uint32_t bound = PN > 0 ? sample_chunk_bound(PN, tiles) : 0u;
+    const size_t wbytes = carve_bwd(nullptr, P, ws, (int)bound);
     void* wbuf = geom_bwd_alloc(geom_bwd_ctx, wbytes + 256);
     if (!wbuf) return fail(GSR_ERR_ALLOC, "backward buffer allocation failed");
     void* wb = aligned_base(wbuf);
-    carve_bwd(wb, P, ws);
+    carve_bwd(wb, P, ws, (int)bound);
     GSR_STAGE(GSR_STAGE_BWD_CLEAR, hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
+    if (!option(kOptNoTileOrder) && bound)  // heaviest chunks first (cost: the forward's chunk max contributor)
+        GSR_STAGE(GSR_STAGE_BWD_CLEAR, launch_chunk_order(bound, st.totals + 2, cs.chunk_max, ws.tile_order, stream),
+                  "chunk order");
+    else
+        ws.tile_order = nullptr;
     GSR_STAGE(GSR_STAGE_SAMPLE_BWD, launch_sample_bwd(b, gs, bs, ts, ps, pb, st, cs, ws, stream), "sample backward");
     BwdParams pbw{};
     pbw.f = b.f;

@@ -676,10 +676,12 @@ hipError_t launch_point_fwd(int query, const FwdParams& p, const GeomState& gs, 
 // LPT order: the tiles bucketed by cost (1024 buckets over [0, max cost]),
 // heaviest bucket first.  The order within a bucket is whatever the LDS
 // atomics give: a tile's outputs do not depend on when it runs.
-__global__ void __launch_bounds__(1024) tile_order_kernel(uint32_t n, const uint2* __restrict__ ranges,
+__global__ void __launch_bounds__(1024) tile_order_kernel(uint32_t n, const uint32_t* __restrict__ n_dev,
+                                                          const uint2* __restrict__ ranges,
                                                           const uint32_t* __restrict__ max_contrib,
                                                           uint32_t* __restrict__ order) {
     constexpr uint32_t kB = 1024;
+    if (n_dev) n = min(n, *n_dev);  // chunk counts known on the device only
     __shared__ uint32_t s_cnt[kB];
     __shared__ uint32_t s_max[kB / 64];
     const uint32_t tid = threadIdx.x;
@@ -714,7 +716,16 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(uint32_t n, const uint
 hipError_t launch_tile_order(uint32_t num_tiles, const uint2* ranges, const uint32_t* max_contrib, uint32_t* order,
                              hipStream_t stream) {
     if (num_tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, num_tiles, ranges, max_contrib, order);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, num_tiles, (const uint32_t*)nullptr, ranges,
+                       max_contrib, order);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_order(uint32_t bound, const uint32_t* n_dev, const uint32_t* chunk_max, uint32_t* order,
+                              hipStream_t stream) {
+    if (bound == 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, bound, n_dev, (const uint2*)nullptr,
+                       chunk_max, order);
     return hipGetLastError();
 }
 

@@ -201,6 +201,7 @@ struct SampleBwdArgs {
     float focal_x, focal_y;
     float* acc;  // [P][16] (gsr_common.h AccField): mean2D, conic, ray-plane
     int diag;    // diagnostic timing switches (GSR_OPT_BWD_NO_PREPASS: bit 0 no pre-pass, bit 1 no reduction)
+    const uint32_t* chunk_order;  // launch order of the chunks (heaviest first) or null
 };
 
 // sampleDepthCUDA backward (sample_backward.cu:77-359), one 256-lane
@@ -216,8 +217,8 @@ __global__ void __launch_bounds__(256) sample_bwd_kernel(SampleBwdArgs a) {
     __shared__ float4 s_w0[kTilePixels], s_w1[kTilePixels], s_w2[kTilePixels];
     __shared__ uint32_t s_id[kTilePixels];
 
-    const uint32_t chunk = xcd_remap(blockIdx.x, gridDim.x);
-    if (chunk >= a.totals[2]) return;  // uniform over the block
+    if (blockIdx.x >= a.totals[2]) return;  // uniform over the block
+    const uint32_t chunk = a.chunk_order ? a.chunk_order[blockIdx.x] : xcd_remap(blockIdx.x, a.totals[2]);
     const int tid = threadIdx.x, lane = tid & 63;
     uint32_t lo = 0, hi = a.num_tiles;
     while (hi - lo > 1) {
@@ -385,6 +386,11 @@ __global__ void __launch_bounds__(256) sample_bwd_kernel(SampleBwdArgs a) {
     }
 }
 
+// chunks <= ceil(points / 256) + tiles holding points
+uint32_t sample_chunk_bound(int PN, uint32_t tiles) {
+    return (uint32_t)((PN + kTilePixels - 1) / kTilePixels) + min(tiles, (uint32_t)PN);
+}
+
 hipError_t launch_sample_bwd(const SampleBwdParams& b, const GeomState& gs, const BinningState& bs,
                              const TileState& ts, const PointState& ps, const PointBinState& pb,
                              const SampleTiles& st, const ChunkState& cs, const BwdState& ws, hipStream_t stream) {
@@ -417,8 +423,8 @@ hipError_t launch_sample_bwd(const SampleBwdParams& b, const GeomState& gs, cons
     a.focal_y = p.focal_y;
     a.acc = ws.acc;
     a.diag = option(kOptBwdNoPrepass);
-    // chunks <= ceil(points / 256) + tiles holding points
-    const uint32_t bound = (uint32_t)((b.PN + kTilePixels - 1) / kTilePixels) + min(tiles, (uint32_t)b.PN);
+    a.chunk_order = ws.tile_order;
+    const uint32_t bound = sample_chunk_bound(b.PN, tiles);
     hipLaunchKernelGGL(sample_bwd_kernel, dim3(bound), dim3(kTilePixels), 0, stream, a);
     return hipGetLastError();
 }

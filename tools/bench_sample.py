@@ -14,6 +14,8 @@ import gsr_scene as S
 from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, _C
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+for kv in sys.argv[2:]:  # OPT=VALUE pairs (gsr_set_option), for A/B runs
+    _C.set_option(*map(int, kv.split("=")))
 dev = torch.device("cuda")
 W, H, P = 1920, 1080, 1_000_000
 cam0 = S.make_camera(W, H).to(dev)
