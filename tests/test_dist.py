@@ -53,13 +53,25 @@ def _worker(rank, world, port, outdir):
 
     inp = _view_grads(rank)
     params = [inp[k] for k in ("means3D", "shs", "opacities", "scales", "rotations")]
-    red = ViewParallelGrads([p.float().detach().requires_grad_(True) for p in params], bucket_mb=0.002)
+    red = ViewParallelGrads([p.float().detach().requires_grad_(True) for p in params], bucket_mb=0.002,
+                            inplace=False)
     for p, src in zip(red.params, params):
         p.grad = src.grad.float().clone()
     assert len(red.buckets) >= 2  # small buckets exercise the bucketing path
     red.all_reduce(async_op=(rank == 0))
     if rank == 0:
         red.finish() if red._work else None
+    # the default: .grad tensors summed in place by one coalesced all-reduce
+    ipl = ViewParallelGrads([p.float().detach().requires_grad_(True) for p in params])
+    for p, src in zip(ipl.params, params):
+        p.grad = src.grad.float().clone()
+    ptrs = [p.grad.data_ptr() for p in ipl.params]
+    ipl.all_reduce(async_op=(rank == 1))
+    if rank == 1:
+        ipl.finish()
+    assert [p.grad.data_ptr() for p in ipl.params] == ptrs  # no copies
+    for a, b in zip(ipl.params, red.params):
+        assert torch.equal(a.grad, b.grad)
     gn = torch.arange(30, dtype=torch.float32) * (rank + 1)
     den = torch.ones(30) * (rank + 1)
     mr = torch.arange(30, dtype=torch.int32) * (1 if rank == 0 else -1) + rank * 100
