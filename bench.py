@@ -18,8 +18,11 @@ ranks, time = max over ranks.
 
 Rank 0 prints one JSON line: the contract fields, a `roofline` object for the
 dominant kernel (algorithmic bytes per launch / its HIP-event-timed average
-duration, vs 8 TB/s HBM peak; `traffic` from the committed rocprofv3 PMC
-summary when present) and a `cpu_baseline` object (the C oracle on the host
+duration in the timed region, vs 8 TB/s HBM peak; `traffic` from the
+committed rocprofv3 PMC summary when present).  Inside the timed region only
+the dominant stage is bracketed by hipEvents (each recorded event idles the
+stream ~10 us); the other stages' times come from --stage-steps untimed steps
+with every stage bracketed and a `cpu_baseline` object (the C oracle on the host
 cores, bounded sample, rank 0 at N = 1 only).
 """
 from __future__ import annotations
@@ -60,6 +63,11 @@ def parse():
     ap.add_argument("--no-depth", action="store_true", help="require_depth=False (iterations < 7000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-tile-stride", type=int, default=0, help="0 = auto")
+    ap.add_argument("--stage-steps", type=int, default=5,
+                    help="untimed steps with every stage bracketed by hipEvents (the per-stage table)")
+    ap.add_argument("--all-stage-events", action="store_true",
+                    help="bracket every stage with hipEvents inside the timed region too (each event pair "
+                         "idles the stream ~10 us; default: only the dominant stage)")
     a = ap.parse_args()
     preset = {"C3": (1_000_000, 0), "C5": (5_000_000, 7)}[a.config]
     a.P = preset[0] if a.P is None else a.P
@@ -209,7 +217,19 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    # per-stage table: a few untimed steps with every stage bracketed by events
     _C.timing_collect()  # discard
+    _C.timing_stages(None)
+    _C.timing_enable(True)
+    for _ in range(max(1, args.stage_steps)):
+        step()
+    torch.cuda.synchronize(dev)
+    _C.timing_enable(False)
+    table = _C.timing_collect()
+    table_ms = {k: (ms / n if n else 0.0) for k, (ms, n) in table.items()}
+    dom = max(table_ms, key=lambda k: table_ms[k])
+    # timed region: events only around the dominant stage (the roofline kernel)
+    _C.timing_stages(None if args.all_stage_events else [dom])
     _C.timing_enable(True)
     if world > 1:
         dist.barrier()
@@ -222,6 +242,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     _C.timing_enable(False)
+    _C.timing_stages(None)
     stages = _C.timing_collect()
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -248,7 +269,8 @@ def main():
     shm = (args.sh_degree + 1) ** 2
     algo = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom)
     per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in stages.items()}
-    dom = max(per_launch, key=lambda k: per_launch[k])
+    if not args.all_stage_events:  # the other stages from the untimed table
+        per_launch = {k: (per_launch[k] if k == dom else v) for k, v in table_ms.items()}
     achieved = algo[dom] / (per_launch[dom] * 1e-3) / 1e9
     traffic, valu = load_pmc_traffic(dom) if args.default_workload else (None, None)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,

@@ -263,6 +263,7 @@ struct TimingRec {
 };
 std::mutex g_tmu;
 bool g_timing = false;
+unsigned g_stage_mask = ~0u;
 std::vector<TimingRec> g_recs;
 std::vector<hipEvent_t> g_pool;
 
@@ -283,7 +284,7 @@ struct StageTimer {
     hipEvent_t e0 = nullptr;
     StageTimer(int st, hipStream_t s) : stream(s), stage(st) {
         std::lock_guard<std::mutex> lk(g_tmu);
-        if (!g_timing) return;
+        if (!g_timing || !((g_stage_mask >> st) & 1u)) return;
         e0 = pool_event();
         if (e0) (void)hipEventRecord(e0, stream);
     }
@@ -372,11 +373,17 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 6; }
+int gsr_abi_version(void) { return 7; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
     g_timing = on != 0;
+    return GSR_OK;
+}
+
+int gsr_timing_stage_mask(unsigned int mask) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_stage_mask = mask;
     return GSR_OK;
 }
 

@@ -82,6 +82,7 @@ def _load():
     L.gsr_debug_sample_points.argtypes = [vp, i, vp, vp, vp]
     L.gsr_debug_render_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i]
     L.gsr_timing_enable.argtypes = [i]
+    L.gsr_timing_stage_mask.argtypes = [ctypes.c_uint]
     L.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i)]
     L.gsr_stage_name.restype = ctypes.c_char_p
     L.gsr_stage_name.argtypes = [i]
@@ -155,6 +156,17 @@ def set_option(opt: int, value: int) -> None:
 def timing_enable(on: bool = True) -> None:
     """Bracket every kernel stage with hipEvents on its stream (gsr_timing_enable)."""
     _load().gsr_timing_enable(int(bool(on)))
+
+
+def timing_stages(names=None) -> None:
+    """Time only the named stages (None: all), gsr_timing_stage_mask."""
+    L = _load()
+    if names is None:
+        mask = 0xFFFFFFFF
+    else:
+        idx = {L.gsr_stage_name(k).decode(): k for k in range(NUM_STAGES)}
+        mask = sum(1 << idx[n] for n in set(names))
+    _check(L.gsr_timing_stage_mask(mask))
 
 
 def timing_collect() -> dict:

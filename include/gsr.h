@@ -312,6 +312,10 @@ enum gsr_stage {
     GSR_NUM_STAGES
 };
 int gsr_timing_enable(int on);
+/* Restrict the timing to the stages whose bit (1 << enum gsr_stage) is set
+ * (default: all).  Each recorded event costs the stream ~10 us of idle time,
+ * so a throughput measurement times only the stage it reports. */
+int gsr_timing_stage_mask(unsigned int mask);
 int gsr_timing_collect(double* ms, int* launches);
 const char* gsr_stage_name(int stage);
 

@@ -283,6 +283,14 @@ def test_timing_api():
     st = _C.timing_collect()
     for k in ("preprocess", "depth_order", "scan", "tile_lists", "render_fwd"):
         assert st[k][1] == 1 and st[k][0] > 0, k
+    _C.timing_stages(["render_fwd"])
+    _C.timing_enable(True)
+    _C.rasterize_gaussians(*ga)
+    _C.timing_enable(False)
+    _C.timing_stages(None)
+    st = _C.timing_collect()
+    assert st["render_fwd"][1] == 1 and st["render_fwd"][0] > 0
+    assert all(n == 0 for k, (_, n) in st.items() if k != "render_fwd")
 
 
 # ------------------------------------------------------------- full size
