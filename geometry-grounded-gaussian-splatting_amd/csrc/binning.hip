@@ -58,8 +58,24 @@ size_t scan_temp_bytes(int P) {
 
 // rocPRIM picks a merge sort below 1M items for 32-bit keys (10 merge passes
 // at P = 1M); a merge-sort limit of 0 keeps the 4-pass onesweep radix sort.
+#ifndef GSR_DSORT_BITS
+#define GSR_DSORT_BITS 8  // 0: rocPRIM's tuned onesweep config; measured at C3: 8 / 512 x 16 0.127 ms vs tuned 0.147 (11 bits: 0.145-0.173, 7: 0.177)
+#endif
+#ifndef GSR_DSORT_BLOCK
+#define GSR_DSORT_BLOCK 512
+#endif
+#ifndef GSR_DSORT_ITEMS
+#define GSR_DSORT_ITEMS 16
+#endif
+#if GSR_DSORT_BITS
+using DepthOnesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>,
+                                                          rocprim::kernel_config<GSR_DSORT_BLOCK, GSR_DSORT_ITEMS>,
+                                                          GSR_DSORT_BITS, rocprim::block_radix_rank_algorithm::match>;
+#else
+using DepthOnesweep = rocprim::default_config;
+#endif
 using DepthSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                   rocprim::default_config, 0>;
+                                                   DepthOnesweep, 0>;
 
 size_t depth_sort_temp_bytes(int P) {
     size_t bytes = 0;
