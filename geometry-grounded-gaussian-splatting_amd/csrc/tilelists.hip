@@ -41,6 +41,160 @@ namespace gsr {
 constexpr int kRowSeg = GSR_ROW_SEG;    // Gaussians per row-pass segment
 constexpr int kTileSeg = GSR_TILE_SEG;  // row entries per tile-pass segment
 
+// ------------------------------------------- exclusive scan, device-sized
+// The counting passes' [bucket][segment] count arrays are scanned by a
+// three-kernel reduce-then-scan whose length n is read on the device (the
+// tile pass's segment count, gx * segbase[gy], is known there only): the
+// grid covers the host's upper bound, blocks past n exit at once, no input
+// beyond n is read (so the count array needs no clearing) and out[n] gets
+// the total.  (rocPRIM's lookback scan over the host bound scanned ~6x the
+// live length at C3 behind a memset: 46 us of the tile-list stage.)
+constexpr int kScanThreads = 256, kScanItems = 16, kScanTile = kScanThreads * kScanItems;
+
+__device__ __forceinline__ uint32_t scan_len(uint32_t n_host, const uint32_t* n_dev, uint32_t mul) {
+    return n_dev ? mul * *n_dev : n_host;
+}
+
+// exclusive scan of one value per thread over the block; *total = block sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; w++) {
+        const uint32_t t = s_w[w];
+        before += w < wave ? t : 0u;
+        all += t;
+    }
+    *total = all;
+    return before + x - v;
+}
+
+__device__ __forceinline__ void scan_load(const uint32_t* in, uint32_t i0, uint32_t n, uint32_t (&v)[kScanItems]) {
+    if (i0 + kScanItems <= n) {
+        const uint4* q = reinterpret_cast<const uint4*>(in + i0);  // i0 is a multiple of 16: 16-B aligned
+#pragma unroll
+        for (int k = 0; k < kScanItems / 4; k++) {
+            const uint4 u = q[k];
+            v[4 * k] = u.x;
+            v[4 * k + 1] = u.y;
+            v[4 * k + 2] = u.z;
+            v[4 * k + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanItems; k++) v[k] = i0 + k < n ? in[i0 + k] : 0u;
+    }
+}
+
+__global__ void __launch_bounds__(kScanThreads)
+    scan_sums_kernel(const uint32_t* __restrict__ in, uint32_t n_host, const uint32_t* __restrict__ n_dev, uint32_t mul,
+                     uint32_t* __restrict__ sums) {
+    __shared__ uint32_t s_w[kScanThreads / 64];
+    const uint32_t n = scan_len(n_host, n_dev, mul);
+    const uint32_t base = blockIdx.x * (uint32_t)kScanTile;
+    if (base >= n) {
+        if (threadIdx.x == 0) sums[blockIdx.x] = 0u;
+        return;
+    }
+    uint32_t v[kScanItems];
+    scan_load(in, base + threadIdx.x * kScanItems, n, v);
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) t += v[k];
+    uint32_t total;
+    (void)block_excl_scan(t, s_w, &total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(1024) scan_block_sums_kernel(uint32_t nb, uint32_t* __restrict__ sums) {
+    __shared__ uint32_t s_w[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
+        const uint32_t i = c0 + tid;
+        const uint32_t v = i < nb ? sums[i] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[wave] = x;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int w = 0; w < 16; w++) {
+            const uint32_t t = s_w[w];
+            before += w < wave ? t : 0u;
+            all += t;
+        }
+        if (i < nb) sums[i] = carry + before + x - v;
+        carry += all;
+        __syncthreads();  // s_w reused by the next chunk
+    }
+}
+
+__global__ void __launch_bounds__(kScanThreads)
+    scan_out_kernel(const uint32_t* __restrict__ in, uint32_t n_host, const uint32_t* __restrict__ n_dev, uint32_t mul,
+                    const uint32_t* __restrict__ sums, uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_w[kScanThreads / 64];
+    const uint32_t n = scan_len(n_host, n_dev, mul);
+    const uint32_t base = blockIdx.x * (uint32_t)kScanTile;
+    if (base > n) return;  // (the block holding index n writes the total there)
+    const uint32_t i0 = base + threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    scan_load(in, i0, n, v);
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) t += v[k];
+    uint32_t total;
+    uint32_t run = sums[blockIdx.x] + block_excl_scan(t, s_w, &total);
+    if (i0 + kScanItems <= n) {
+        uint4* q = reinterpret_cast<uint4*>(out + i0);
+#pragma unroll
+        for (int k = 0; k < kScanItems / 4; k++) {
+            uint4 u;
+            u.x = run;
+            run += v[4 * k];
+            u.y = run;
+            run += v[4 * k + 1];
+            u.z = run;
+            run += v[4 * k + 2];
+            u.w = run;
+            run += v[4 * k + 3];
+            q[k] = u;
+        }
+        if (i0 + kScanItems == n) out[n] = run;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanItems; k++) {
+            if (i0 + k <= n) out[i0 + k] = run;
+            run += v[k];
+        }
+    }
+}
+
+// exclusive scan of in[0, n) into out[0, n], n = n_dev ? mul * *n_dev : n;
+// cap >= n is the host's bound, sums holds scan_sums_count(cap) words
+uint32_t scan_sums_count(size_t cap) { return (uint32_t)(cap / kScanTile + 1); }
+
+hipError_t launch_scan_excl(const uint32_t* in, uint32_t* out, size_t cap, uint32_t n_host, const uint32_t* n_dev,
+                            uint32_t mul, uint32_t* sums, hipStream_t stream) {
+    const uint32_t nb = scan_sums_count(cap);
+    hipLaunchKernelGGL(scan_sums_kernel, dim3(nb), dim3(kScanThreads), 0, stream, in, n_host, n_dev, mul, sums);
+    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(1024), 0, stream, nb, sums);
+    hipLaunchKernelGGL(scan_out_kernel, dim3(nb), dim3(kScanThreads), 0, stream, in, n_host, n_dev, mul,
+                       (const uint32_t*)sums, out);
+    return hipGetLastError();
+}
+
 bool list_binning(uint32_t gx, uint32_t gy) { return gx <= (uint32_t)kMaxGrid && gy <= (uint32_t)kMaxGrid; }
 
 ListLayout list_layout(int P, int K, uint32_t gx, uint32_t gy) {
@@ -56,6 +210,9 @@ ListLayout list_layout(int P, int K, uint32_t gx, uint32_t gy) {
                           rocprim::plus<uint32_t>());
     L.tmp_bytes = a > b ? a : b;
     L.tmp_bytes = L.tmp_bytes > c ? L.tmp_bytes : c;
+    // the device-sized scans' block sums
+    const size_t d = 4 * (size_t)scan_sums_count((size_t)gx * L.nseg_tiles_max + (size_t)gy * L.nseg_rows);
+    L.tmp_bytes = L.tmp_bytes > d ? L.tmp_bytes : d;
     return L;
 }
 
@@ -332,10 +489,12 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
                        p.cull_pad, gs.order,
                        gs.splats, radii, bs.rows_count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    size_t bytes = L.tmp_bytes;
-    e = rocprim::exclusive_scan(bs.list_tmp, bytes, bs.rows_count, bs.rows_off, 0u, (size_t)gy * L.nseg_rows,
-                                rocprim::plus<uint32_t>(), stream);
-    if (e != hipSuccess) return e;
+    uint32_t* sums = reinterpret_cast<uint32_t*>(bs.list_tmp);
+    const size_t nrows = (size_t)gy * L.nseg_rows;
+    // (rows_off holds gy * nseg_rows words: the scan writes the total at [n] only up to n - 1 here)
+    if ((e = launch_scan_excl(bs.rows_count, bs.rows_off, nrows - 1, (uint32_t)(nrows - 1), nullptr, 1u, sums,
+                              stream)) != hipSuccess)
+        return e;
     hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, gx, gy,
                        p.cull_pad, gs.order,
                        gs.splats, radii, bs.rows_off, bs.rows);
@@ -345,15 +504,13 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     hipLaunchKernelGGL(tiles_setup_kernel, dim3(1), dim3(1024), 0, stream, gy, L.nseg_rows, bs.rows_off, last,
                        bs.segbase);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const size_t mt = (size_t)gx * L.nseg_tiles_max + 1;
-    if ((e = hipMemsetAsync(bs.tiles_count, 0, sizeof(uint32_t) * mt, stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(tiles_count_kernel, dim3(kTileBlocks), dim3(64), 4 * gx, stream, gx, gy, L.nseg_rows,
                        bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    bytes = L.tmp_bytes;
-    e = rocprim::exclusive_scan(bs.list_tmp, bytes, bs.tiles_count, bs.tiles_off, 0u, mt, rocprim::plus<uint32_t>(),
-                                stream);
-    if (e != hipSuccess) return e;
+    // counts of the live segments only: gx * segbase[gy] of them (tiles_count_kernel writes every one)
+    if ((e = launch_scan_excl(bs.tiles_count, bs.tiles_off, (size_t)gx * L.nseg_tiles_max, 0u, bs.segbase + gy, gx,
+                              sums, stream)) != hipSuccess)
+        return e;
     hipLaunchKernelGGL(tiles_emit_kernel, dim3(kTileBlocks), dim3(64), 24 * gx, stream, gx, gy, L.nseg_rows,
                        bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
     if ((e = hipGetLastError()) != hipSuccess) return e;
