@@ -72,7 +72,15 @@ __device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
     }
 }
 
+#ifndef GSR_PBWD_WAVES
+#define GSR_PBWD_WAVES 0
+#endif
+#if GSR_PBWD_WAVES
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_PBWD_WAVES, 8)))
+preprocess_bwd_kernel(PreprocessBwdArgs a) {
+#else
 __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a) {
+#endif
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
     const float* acc = a.acc + (size_t)idx * kAccFields;

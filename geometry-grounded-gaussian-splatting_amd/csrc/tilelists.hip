@@ -43,7 +43,7 @@ constexpr int kTileSeg = GSR_TILE_SEG;  // row entries per tile-pass segment
 
 // ------------------------------------------- exclusive scan, device-sized
 // The counting passes' [bucket][segment] count arrays are scanned by a
-// three-kernel reduce-then-scan whose length n is read on the device (the
+// two-kernel reduce-then-scan whose length n is read on the device (the
 // tile pass's segment count, gx * segbase[gy], is known there only): the
 // grid covers the host's upper bound, blocks past n exit at once, no input
 // beyond n is read (so the count array needs no clearing) and out[n] gets
@@ -75,6 +75,19 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
     }
     *total = all;
     return before + x - v;
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* s_w) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s_w[wave] = v;
+    __syncthreads();
+    uint32_t all = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; w++) all += s_w[w];
+    __syncthreads();  // s_w is reused
+    return all;
 }
 
 __device__ __forceinline__ void scan_load(const uint32_t* in, uint32_t i0, uint32_t n, uint32_t (&v)[kScanItems]) {
@@ -114,33 +127,6 @@ __global__ void __launch_bounds__(kScanThreads)
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-__global__ void __launch_bounds__(1024) scan_block_sums_kernel(uint32_t nb, uint32_t* __restrict__ sums) {
-    __shared__ uint32_t s_w[16];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t carry = 0;
-    for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
-        const uint32_t i = c0 + tid;
-        const uint32_t v = i < nb ? sums[i] : 0u;
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_w[wave] = x;
-        __syncthreads();
-        uint32_t before = 0, all = 0;
-        for (int w = 0; w < 16; w++) {
-            const uint32_t t = s_w[w];
-            before += w < wave ? t : 0u;
-            all += t;
-        }
-        if (i < nb) sums[i] = carry + before + x - v;
-        carry += all;
-        __syncthreads();  // s_w reused by the next chunk
-    }
-}
-
 __global__ void __launch_bounds__(kScanThreads)
     scan_out_kernel(const uint32_t* __restrict__ in, uint32_t n_host, const uint32_t* __restrict__ n_dev, uint32_t mul,
                     const uint32_t* __restrict__ sums, uint32_t* __restrict__ out) {
@@ -154,8 +140,13 @@ __global__ void __launch_bounds__(kScanThreads)
     uint32_t t = 0;
 #pragma unroll
     for (int k = 0; k < kScanItems; k++) t += v[k];
+    // this block's offset: the sum of the earlier blocks' sums (<= a few
+    // thousand words from L2; cheaper than a separate launch scanning them)
+    uint32_t pre = 0;
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += kScanThreads) pre += sums[j];
+    pre = block_sum(pre, s_w);
     uint32_t total;
-    uint32_t run = sums[blockIdx.x] + block_excl_scan(t, s_w, &total);
+    uint32_t run = pre + block_excl_scan(t, s_w, &total);
     if (i0 + kScanItems <= n) {
         uint4* q = reinterpret_cast<uint4*>(out + i0);
 #pragma unroll
@@ -189,7 +180,6 @@ hipError_t launch_scan_excl(const uint32_t* in, uint32_t* out, size_t cap, uint3
                             uint32_t mul, uint32_t* sums, hipStream_t stream) {
     const uint32_t nb = scan_sums_count(cap);
     hipLaunchKernelGGL(scan_sums_kernel, dim3(nb), dim3(kScanThreads), 0, stream, in, n_host, n_dev, mul, sums);
-    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(1024), 0, stream, nb, sums);
     hipLaunchKernelGGL(scan_out_kernel, dim3(nb), dim3(kScanThreads), 0, stream, in, n_host, n_dev, mul,
                        (const uint32_t*)sums, out);
     return hipGetLastError();
