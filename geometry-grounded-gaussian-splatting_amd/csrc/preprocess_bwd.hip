@@ -72,6 +72,54 @@ __device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
     }
 }
 
+#ifndef GSR_SG_UNROLL
+#define GSR_SG_UNROLL 1
+#endif
+// SG degree 7 (the configuration with SG lobes, BASELINE C5), all lobes of
+// a Gaussian at once: its axis / colour / sharpness rows (21 + 21 + 7
+// consecutive floats) are loaded and its gradient rows stored as wide
+// contiguous accesses issued together, instead of 7 dependent iterations of
+// 3-float pieces.  Same arithmetic in the same order as the generic loop.
+constexpr int kSG7 = 7;
+__device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, float x, float y, float z, float dR0,
+                                        float dR1, float dR2, float& ddx, float& ddy, float& ddz) {
+    const size_t o0 = (size_t)idx * kSG7;
+    float ax[3 * kSG7], gc[3 * kSG7], sharp[kSG7];
+#pragma unroll
+    for (int k = 0; k < 3 * kSG7; k++) ax[k] = a.sg_axis[3 * o0 + k];
+#pragma unroll
+    for (int k = 0; k < 3 * kSG7; k++) gc[k] = a.sg_color[3 * o0 + k];
+#pragma unroll
+    for (int k = 0; k < kSG7; k++) sharp[k] = a.sg_sharpness[o0 + k];
+    float dcol[3 * kSG7], dax[3 * kSG7], dsh[kSG7];
+#pragma unroll
+    for (int sg = 0; sg < kSG7; sg++) {
+        const float* axs = ax + 3 * sg;
+        const float* gcs = gc + 3 * sg;
+        const float auxs = (axs[0] * x + axs[1] * y + axs[2] * z) - 1.0f;
+        const float gs = expf(sharp[sg] * auxs);
+        dcol[3 * sg + 0] = dR0 * gs;
+        dcol[3 * sg + 1] = dR1 * gs;
+        dcol[3 * sg + 2] = dR2 * gs;
+        const float dL_dgs = gcs[0] * dR0 + gcs[1] * dR1 + gcs[2] * dR2;
+        const float dL_dexp = dL_dgs * gs;
+        dsh[sg] = dL_dexp * auxs;
+        const float dL_daux = dL_dexp * sharp[sg];
+        dax[3 * sg + 0] = dL_daux * x;
+        dax[3 * sg + 1] = dL_daux * y;
+        dax[3 * sg + 2] = dL_daux * z;
+        ddx += dL_daux * axs[0];
+        ddy += dL_daux * axs[1];
+        ddz += dL_daux * axs[2];
+    }
+#pragma unroll
+    for (int k = 0; k < 3 * kSG7; k++) a.dL_dsg_color[3 * o0 + k] = dcol[k];
+#pragma unroll
+    for (int k = 0; k < kSG7; k++) a.dL_dsg_sharpness[o0 + k] = dsh[k];
+#pragma unroll
+    for (int k = 0; k < 3 * kSG7; k++) a.dL_dsg_axis[3 * o0 + k] = dax[k];
+}
+
 #ifndef GSR_PBWD_WAVES
 #define GSR_PBWD_WAVES 0
 #endif
@@ -474,6 +522,11 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         float ddx = gdx[0] * dR0 + gdx[1] * dR1 + gdx[2] * dR2;
         float ddy = gdy[0] * dR0 + gdy[1] * dR1 + gdy[2] * dR2;
         float ddz = gdz[0] * dR0 + gdz[1] * dR1 + gdz[2] * dR2;
+#if GSR_SG_UNROLL
+        if (a.SGM == kSG7 && a.SGD == kSG7) {
+            sg7_bwd(a, idx, x, y, z, dR0, dR1, dR2, ddx, ddy, ddz);
+        } else
+#endif
         for (int sg = 0; sg < a.SGM; sg++) {
             const size_t o = (size_t)idx * a.SGM + sg;
             if (sg >= a.SGD) {
