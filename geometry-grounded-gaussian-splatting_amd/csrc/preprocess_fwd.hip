@@ -221,6 +221,27 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
                 col[2] += Y[kk] * sh[3 * kk + 2];
             }
         }
+        if (a.SGM == 7 && a.SGD == 7) {
+            // SG degree 7 (C5): every lobe's axis / colour / sharpness rows
+            // loaded at once as wide contiguous accesses (preprocess_bwd.hip
+            // sg7_bwd); same arithmetic and order as the loop below
+            const size_t o0 = (size_t)idx * 7;
+            float ax[21], sc[21], sh7[7];
+#pragma unroll
+            for (int k = 0; k < 21; k++) ax[k] = a.sg_axis[3 * o0 + k];
+#pragma unroll
+            for (int k = 0; k < 21; k++) sc[k] = a.sg_color[3 * o0 + k];
+#pragma unroll
+            for (int k = 0; k < 7; k++) sh7[k] = a.sg_sharpness[o0 + k];
+#pragma unroll
+            for (int sg = 0; sg < 7; sg++) {
+                const float gs =
+                    expf(sh7[sg] * ((ax[3 * sg] * dx + ax[3 * sg + 1] * dy + ax[3 * sg + 2] * dz) - 1.0f));
+                col[0] += sc[3 * sg] * gs;
+                col[1] += sc[3 * sg + 1] * gs;
+                col[2] += sc[3 * sg + 2] * gs;
+            }
+        } else
         for (int sg = 0; sg < a.SGD; sg++) {
             const size_t o = (size_t)idx * a.SGM + sg;
             const float* ax = a.sg_axis + 3 * o;
