@@ -585,12 +585,17 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
     if (!wbuf) return fail(GSR_ERR_ALLOC, "backward buffer allocation failed");
     void* wb = aligned_base(wbuf);
     carve_bwd(wb, P, ws, tiles);
-    GSR_STAGE(GSR_STAGE_BWD_CLEAR, hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
-    if (!option(kOptNoTileOrder))  // heaviest tiles first: the forward's per-tile max contributor is the cost
-        GSR_STAGE(GSR_STAGE_BWD_CLEAR, launch_tile_order((uint32_t)tiles, nullptr, ts.max_contrib, ws.tile_order, stream),
-                  "tile order");
-    else
+    if (!option(kOptNoTileOrder) && tiles > 0) {
+        // heaviest tiles first (cost: the forward's per-tile max contributor),
+        // ordered by one workgroup while the others clear the accumulators
+        const size_t zbytes = (size_t)(reinterpret_cast<char*>(ws.tile_order) - static_cast<char*>(wb));
+        GSR_STAGE(GSR_STAGE_BWD_CLEAR,
+                  launch_bwd_prepare(wb, zbytes, (uint32_t)tiles, ts.max_contrib, ws.tile_order, stream),
+                  "clear accumulators + tile order");
+    } else {
+        GSR_STAGE(GSR_STAGE_BWD_CLEAR, hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
         ws.tile_order = nullptr;
+    }
     GSR_STAGE(GSR_STAGE_RENDER_BWD, launch_render_bwd(b, gs, bs, is, ts, ws, stream), "render backward");
     GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_bwd(b, gs, ws, stream), "preprocess backward");
     return GSR_OK;

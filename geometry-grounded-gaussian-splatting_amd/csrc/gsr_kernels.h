@@ -194,6 +194,10 @@ hipError_t launch_knn(int P, const float* pts, const KnnState& s, float* mean_di
 // max contributor (backward); one 1024-lane workgroup.
 hipError_t launch_tile_order(uint32_t num_tiles, const uint2* ranges, const uint32_t* max_contrib, uint32_t* order,
                              hipStream_t stream);
+// the tile order (workgroup 0) and the clearing of [zero, zero + zero_bytes)
+// (16-B aligned and sized) in one launch
+hipError_t launch_bwd_prepare(void* zero, size_t zero_bytes, uint32_t num_tiles, const uint32_t* max_contrib,
+                              uint32_t* order, hipStream_t stream);
 // the same for sample_depth's point chunks (count *n_dev <= bound, cost = chunk max contributor)
 hipError_t launch_chunk_order(uint32_t bound, const uint32_t* n_dev, const uint32_t* chunk_max, uint32_t* order,
                               hipStream_t stream);

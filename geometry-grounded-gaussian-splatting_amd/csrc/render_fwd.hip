@@ -31,6 +31,8 @@
 
 #include <type_traits>
 
+#include <algorithm>
+
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -676,10 +678,10 @@ hipError_t launch_point_fwd(int query, const FwdParams& p, const GeomState& gs, 
 // LPT order: the tiles bucketed by cost (1024 buckets over [0, max cost]),
 // heaviest bucket first.  The order within a bucket is whatever the LDS
 // atomics give: a tile's outputs do not depend on when it runs.
-__global__ void __launch_bounds__(1024) tile_order_kernel(uint32_t n, const uint32_t* __restrict__ n_dev,
-                                                          const uint2* __restrict__ ranges,
-                                                          const uint32_t* __restrict__ max_contrib,
-                                                          uint32_t* __restrict__ order) {
+__device__ __forceinline__ void tile_order_body(uint32_t n, const uint32_t* __restrict__ n_dev,
+                                                const uint2* __restrict__ ranges,
+                                                const uint32_t* __restrict__ max_contrib,
+                                                uint32_t* __restrict__ order) {
     constexpr uint32_t kB = 1024;
     if (n_dev) n = min(n, *n_dev);  // chunk counts known on the device only
     __shared__ uint32_t s_cnt[kB];
@@ -713,11 +715,43 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(uint32_t n, const uint
     for (uint32_t t = tid; t < n; t += kB) order[atomicAdd(&s_cnt[bucket(cost(t))], 1u)] = t;
 }
 
+__global__ void __launch_bounds__(1024) tile_order_kernel(uint32_t n, const uint32_t* __restrict__ n_dev,
+                                                          const uint2* __restrict__ ranges,
+                                                          const uint32_t* __restrict__ max_contrib,
+                                                          uint32_t* __restrict__ order) {
+    tile_order_body(n, n_dev, ranges, max_contrib, order);
+}
+
+// The backward's preparation in one launch: workgroup 0 builds the LPT tile
+// order while the others clear the accumulators (a memset and the
+// single-workgroup ordering kernel were two serial launches, ~23 us).
+__global__ void __launch_bounds__(1024) bwd_prepare_kernel(uint4* __restrict__ zero, size_t n16, uint32_t n_tiles,
+                                                           const uint32_t* __restrict__ max_contrib,
+                                                           uint32_t* __restrict__ order) {
+    if (blockIdx.x == 0) {
+        tile_order_body(n_tiles, nullptr, nullptr, max_contrib, order);
+        return;
+    }
+    const size_t stride = (size_t)(gridDim.x - 1) * blockDim.x;
+    for (size_t i = (size_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < n16; i += stride)
+        zero[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 hipError_t launch_tile_order(uint32_t num_tiles, const uint2* ranges, const uint32_t* max_contrib, uint32_t* order,
                              hipStream_t stream) {
     if (num_tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, num_tiles, (const uint32_t*)nullptr, ranges,
                        max_contrib, order);
+    return hipGetLastError();
+}
+
+hipError_t launch_bwd_prepare(void* zero, size_t zero_bytes, uint32_t num_tiles, const uint32_t* max_contrib,
+                              uint32_t* order, hipStream_t stream) {
+    if (zero_bytes % 16 != 0 || ((uintptr_t)zero & 15u) != 0) return hipErrorInvalidValue;
+    const size_t n16 = zero_bytes / 16;
+    const uint32_t zblocks = (uint32_t)std::min<size_t>((n16 + 1023) / 1024, 1024);
+    hipLaunchKernelGGL(bwd_prepare_kernel, dim3(1 + zblocks), dim3(1024), 0, stream, reinterpret_cast<uint4*>(zero),
+                       n16, num_tiles, max_contrib, order);
     return hipGetLastError();
 }
 
