@@ -40,7 +40,7 @@ def stage_of(name: str) -> str | None:
         return "render_fwd"
     if "render_bwd_kernel" in n:
         return "render_bwd"
-    if "tile_order_kernel" in n:
+    if "tile_order_kernel" in n or "bwd_prepare_kernel" in n:
         return "bwd_clear"
     if "gather_counts_kernel" in n or "live_tiles_kernel" in n:
         return "depth_order"
