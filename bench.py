@@ -51,8 +51,8 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", choices=["C3", "C5"], default="C3",
                     help="C3: 1M Gaussians, SH 3 (the metric's config); C5: 5M Gaussians, SH 3 + SG 7")
     ap.add_argument("--P", type=int, default=None)
