@@ -33,7 +33,7 @@
 namespace gsr {
 
 #ifndef GSR_ROW_SEG
-#define GSR_ROW_SEG 128  // measured at C3: 0.29 ms tile_lists vs 0.31 (256), 0.39 (512)
+#define GSR_ROW_SEG 64  // measured at C3: tile_lists 0.248 ms vs 0.256 (128), 0.277 (96), 0.31 (256), 0.39 (512)
 #endif
 #ifndef GSR_TILE_SEG
 #define GSR_TILE_SEG 512
