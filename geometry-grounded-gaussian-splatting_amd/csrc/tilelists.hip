@@ -260,6 +260,12 @@ __global__ void __launch_bounds__(64)
     for (uint32_t y = lane; y < gy; y += 64) M[(size_t)y * nseg + seg] = s_cnt[y];
 }
 
+#ifndef GSR_SPAN_CACHE
+#define GSR_SPAN_CACHE 4
+#endif
+constexpr int kSpanCache = GSR_SPAN_CACHE;  // tile rows whose spans rows_emit keeps in registers
+constexpr uint32_t kNoSpan = 0xffffffffu;   // (spans are lo | hi << 16 with hi < 1024)
+
 // Ranking within a 64-entry chunk: every entry ORs its lane bit into its
 // bucket's mask; its slot is the bucket's running slot plus the popcount of
 // the lower lanes' bits, and the bucket's lowest lane advances the running
@@ -292,18 +298,34 @@ __global__ void __launch_bounds__(64)
         }
         const QGauss G = load_q(c0 + lane, q1, order, splats, radii, gx, gy, pad);
         uint32_t lo, hi;
+        // the spans of the first kSpanCache rows are computed once and kept
+        // in registers for the write phase (constant indices: no scratch)
+        uint32_t span[kSpanCache];
+#pragma unroll
+        for (int k = 0; k < kSpanCache; k++) {
+            const uint32_t y = G.R.y0 + (uint32_t)k;
+            span[k] = kNoSpan;
+            if (G.on && y < G.R.y1 && row_span(G.E, G.R, y, &lo, &hi)) {
+                span[k] = lo | (hi << 16);
+                atomicOr(&cov[y], bit);
+            }
+        }
         if (G.on)
-            for (uint32_t y = G.R.y0; y < G.R.y1; y++)
+            for (uint32_t y = G.R.y0 + kSpanCache; y < G.R.y1; y++)
                 if (row_span(G.E, G.R, y, &lo, &hi)) atomicOr(&cov[y], bit);
         __syncthreads();  // one wave: orders the LDS phases for the compiler
+        auto emit = [&](uint32_t y, uint32_t sp) {
+            const unsigned long long m = cov[y];
+            const uint32_t r0 = run[y];
+            rows[r0 + (uint32_t)__popcll(m & below)] = make_uint2(G.g, sp);
+            if ((m & below) == 0ull) run_next[y] = r0 + (uint32_t)__popcll(m);
+        };
+#pragma unroll
+        for (int k = 0; k < kSpanCache; k++)
+            if (span[k] != kNoSpan) emit(G.R.y0 + (uint32_t)k, span[k]);
         if (G.on)
-            for (uint32_t y = G.R.y0; y < G.R.y1; y++)
-                if (row_span(G.E, G.R, y, &lo, &hi)) {
-                    const unsigned long long m = cov[y];
-                    const uint32_t r0 = run[y];
-                    rows[r0 + (uint32_t)__popcll(m & below)] = make_uint2(G.g, lo | (hi << 16));
-                    if ((m & below) == 0ull) run_next[y] = r0 + (uint32_t)__popcll(m);
-                }
+            for (uint32_t y = G.R.y0 + kSpanCache; y < G.R.y1; y++)
+                if (row_span(G.E, G.R, y, &lo, &hi)) emit(y, lo | (hi << 16));
         __syncthreads();
     }
 }
