@@ -109,6 +109,7 @@ size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, Binning
     if (b.use_lists) {
         b.lists = list_layout(P, K, gx, gy);
         b.rows = c.take<uint2>(K);
+        b.qrec = c.take<uint4>((size_t)2 * P);
         b.rows_count = c.take<uint32_t>((size_t)gy * b.lists.nseg_rows);
         b.rows_off = c.take<uint32_t>((size_t)gy * b.lists.nseg_rows);
         b.segbase = c.take<uint32_t>(gy + 1);

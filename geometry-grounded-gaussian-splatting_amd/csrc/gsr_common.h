@@ -92,6 +92,7 @@ struct BinningState {
     bool use_lists;        // tilelists.hip path (else emit + tile-id sort)
     ListLayout lists;
     uint2* rows;           // (Gaussian, column span) per tile row, q order
+    uint4* qrec;           // [P][2] per Gaussian in q order: id, rows y0 | y1 << 16, spans of rows y0 .. y0 + 5
     uint32_t *rows_count, *rows_off, *segbase, *tiles_count, *tiles_off;
     void* list_tmp;
     int key_bytes;        // 2 or 4 (tile_key_bytes)

@@ -240,9 +240,19 @@ __device__ __forceinline__ QGauss load_q(int q, int q1, const uint32_t* order, c
     return G;
 }
 
+// rows_count writes, per Gaussian in q order, a 32-B record: its id (or
+// kNoSpan when it has no live tile), its rect rows y0 | y1 << 16 and the
+// column spans of rows y0 .. y0 + kRecSpans - 1 (kNoSpan where not live).
+// rows_emit streams the records instead of gathering the splat by id and
+// recomputing the spans; it falls back to both only for rows past the
+// record's (Gaussians taller than kRecSpans tile rows).
+constexpr int kRecSpans = 6;
+constexpr uint32_t kNoSpan = 0xffffffffu;  // (spans are lo | hi << 16 with hi < 1024)
+
 __global__ void __launch_bounds__(64)
     rows_count_kernel(int P, int nseg, uint32_t gx, uint32_t gy, float pad, const uint32_t* __restrict__ order,
-                      const Splat* __restrict__ splats, const int* __restrict__ radii, uint32_t* __restrict__ M) {
+                      const Splat* __restrict__ splats, const int* __restrict__ radii, uint32_t* __restrict__ M,
+                      uint4* __restrict__ qrec) {
     extern __shared__ unsigned long long s_dyn[];
     uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
     const int seg = (int)xcd_remap(blockIdx.x, gridDim.x), lane = threadIdx.x;  // XCD-contiguous segments
@@ -251,20 +261,28 @@ __global__ void __launch_bounds__(64)
     const int q0 = seg * kRowSeg, q1 = min(P, q0 + kRowSeg);
     for (int q = q0 + lane; q < q1; q += 64) {
         const QGauss G = load_q(q, q1, order, splats, radii, gx, gy, pad);
-        if (!G.on) continue;
         uint32_t lo, hi;
-        for (uint32_t y = G.R.y0; y < G.R.y1; y++)
+        // the record rows_emit reads instead of re-gathering and re-spanning
+        uint32_t sp[kRecSpans];
+#pragma unroll
+        for (int k = 0; k < kRecSpans; k++) {
+            const uint32_t y = G.R.y0 + (uint32_t)k;
+            sp[k] = kNoSpan;
+            if (G.on && y < G.R.y1 && row_span(G.E, G.R, y, &lo, &hi)) {
+                sp[k] = lo | (hi << 16);
+                atomicAdd(&s_cnt[y], 1u);
+            }
+        }
+        qrec[2 * (size_t)q] = make_uint4(G.on ? G.g : kNoSpan, G.R.y0 | (G.R.y1 << 16), sp[0], sp[1]);
+        qrec[2 * (size_t)q + 1] = make_uint4(sp[2], sp[3], sp[4], sp[5]);
+        if (!G.on) continue;
+        for (uint32_t y = G.R.y0 + kRecSpans; y < G.R.y1; y++)
             if (row_span(G.E, G.R, y, &lo, &hi)) atomicAdd(&s_cnt[y], 1u);
     }
     __syncthreads();
     for (uint32_t y = lane; y < gy; y += 64) M[(size_t)y * nseg + seg] = s_cnt[y];
 }
 
-#ifndef GSR_SPAN_CACHE
-#define GSR_SPAN_CACHE 4
-#endif
-constexpr int kSpanCache = GSR_SPAN_CACHE;  // tile rows whose spans rows_emit keeps in registers
-constexpr uint32_t kNoSpan = 0xffffffffu;   // (spans are lo | hi << 16 with hi < 1024)
 
 // Ranking within a 64-entry chunk: every entry ORs its lane bit into its
 // bucket's mask; its slot is the bucket's running slot plus the popcount of
@@ -275,7 +293,7 @@ constexpr uint32_t kNoSpan = 0xffffffffu;   // (spans are lo | hi << 16 with hi 
 __global__ void __launch_bounds__(64)
     rows_emit_kernel(int P, int nseg, uint32_t gx, uint32_t gy, float pad, const uint32_t* __restrict__ order,
                      const Splat* __restrict__ splats, const int* __restrict__ radii, const uint32_t* __restrict__ O,
-                     uint2* __restrict__ rows) {
+                     const uint4* __restrict__ qrec, uint2* __restrict__ rows) {
     extern __shared__ unsigned long long s_dyn[];  // 2 x [gy] masks, then 2 x [gy] running slots
     unsigned long long* s_cov = s_dyn;
     uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * gy);
@@ -296,35 +314,38 @@ __global__ void __launch_bounds__(64)
             run_next[y] = run[y];
             s_cov[(cur ^ 1u) * gy + y] = 0ull;
         }
-        const QGauss G = load_q(c0 + lane, q1, order, splats, radii, gx, gy, pad);
-        uint32_t lo, hi;
-        // the spans of the first kSpanCache rows are computed once and kept
-        // in registers for the write phase (constant indices: no scratch)
-        uint32_t span[kSpanCache];
-#pragma unroll
-        for (int k = 0; k < kSpanCache; k++) {
-            const uint32_t y = G.R.y0 + (uint32_t)k;
-            span[k] = kNoSpan;
-            if (G.on && y < G.R.y1 && row_span(G.E, G.R, y, &lo, &hi)) {
-                span[k] = lo | (hi << 16);
-                atomicOr(&cov[y], bit);
-            }
+        const int q = c0 + lane;
+        uint4 r0 = make_uint4(kNoSpan, 0u, kNoSpan, kNoSpan), r1 = make_uint4(kNoSpan, kNoSpan, kNoSpan, kNoSpan);
+        if (q < q1) {
+            r0 = qrec[2 * (size_t)q];
+            r1 = qrec[2 * (size_t)q + 1];
         }
-        if (G.on)
-            for (uint32_t y = G.R.y0 + kSpanCache; y < G.R.y1; y++)
+        const bool on = r0.x != kNoSpan;
+        const uint32_t y0 = r0.y & 0xffffu, y1 = r0.y >> 16;
+        const uint32_t span[kRecSpans] = {r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        // rows past the record: the splat's ellipse, as rows_count had it
+        const bool tall = on && y1 > y0 + kRecSpans;
+        QGauss G{};
+        if (tall) G = load_q(q, q1, order, splats, radii, gx, gy, pad);
+        uint32_t lo, hi;
+#pragma unroll
+        for (int k = 0; k < kRecSpans; k++)
+            if (span[k] != kNoSpan) atomicOr(&cov[y0 + (uint32_t)k], bit);
+        if (tall)
+            for (uint32_t y = y0 + kRecSpans; y < y1; y++)
                 if (row_span(G.E, G.R, y, &lo, &hi)) atomicOr(&cov[y], bit);
         __syncthreads();  // one wave: orders the LDS phases for the compiler
         auto emit = [&](uint32_t y, uint32_t sp) {
             const unsigned long long m = cov[y];
-            const uint32_t r0 = run[y];
-            rows[r0 + (uint32_t)__popcll(m & below)] = make_uint2(G.g, sp);
-            if ((m & below) == 0ull) run_next[y] = r0 + (uint32_t)__popcll(m);
+            const uint32_t rs = run[y];
+            rows[rs + (uint32_t)__popcll(m & below)] = make_uint2(r0.x, sp);
+            if ((m & below) == 0ull) run_next[y] = rs + (uint32_t)__popcll(m);
         };
 #pragma unroll
-        for (int k = 0; k < kSpanCache; k++)
-            if (span[k] != kNoSpan) emit(G.R.y0 + (uint32_t)k, span[k]);
-        if (G.on)
-            for (uint32_t y = G.R.y0 + kSpanCache; y < G.R.y1; y++)
+        for (int k = 0; k < kRecSpans; k++)
+            if (span[k] != kNoSpan) emit(y0 + (uint32_t)k, span[k]);
+        if (tall)
+            for (uint32_t y = y0 + kRecSpans; y < y1; y++)
                 if (row_span(G.E, G.R, y, &lo, &hi)) emit(y, lo | (hi << 16));
         __syncthreads();
     }
@@ -499,7 +520,7 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     // rows pass
     hipLaunchKernelGGL(rows_count_kernel, dim3(L.nseg_rows), dim3(64), 4 * gy, stream, p.P, L.nseg_rows, gx, gy,
                        p.cull_pad, gs.order,
-                       gs.splats, radii, bs.rows_count);
+                       gs.splats, radii, bs.rows_count, bs.qrec);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     uint32_t* sums = reinterpret_cast<uint32_t*>(bs.list_tmp);
     const size_t nrows = (size_t)gy * L.nseg_rows;
@@ -509,7 +530,7 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
         return e;
     hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, gx, gy,
                        p.cull_pad, gs.order,
-                       gs.splats, radii, bs.rows_off, bs.rows);
+                       gs.splats, radii, bs.rows_off, bs.qrec, bs.rows);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // tiles pass
     const uint32_t* last = bs.rows_count + (size_t)gy * L.nseg_rows - 1;
