@@ -59,6 +59,7 @@ struct RenderFwdArgs {
     float* out_normal;
     float* out_mdepth;
     int passes;  // bisection passes (kSplitIterations; fewer only for GSR_OPT_BISECT_PASSES timing runs)
+    int refine;  // root refinement after pass 2 (GSR_OPT_NO_REFINE = 0 for the reference's passes only)
     float sample_range;  // half-width of the first bisection window (kSampleRange; 2 kSampleRange for evaluate_sdf)
     // SAMPLE mode (sample_depth, sample.hip): a workgroup is one chunk of
     // kTilePixels points of one tile instead of the tile's pixels
@@ -152,10 +153,56 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
     }
 }
 
+// Root refinement (after the reference's first two passes).  The vacancy
+// transmittance T(t) is continuous and non-increasing in t (each factor is
+// sqrt(1 - a g) in front of the splat's peak and (1 - a) / sqrt(1 - a g)
+// behind it), so the reference's 8-way bisection converges on the root of
+// T(t) = 1/2 and returns it within its final cell (0.8 / 8^5 = 2.4e-5 wide,
+// linearly interpolated: ~1e-8 from the root where T is smooth).  Where T is
+// smooth on the pass-2 cell (every contributor that can reach the cell spans
+// it with at most kSmoothCells of its sigmas; wave-uniform test) the root is
+// found instead by bracketed Halley steps on H(t) = log2 T(t) + 1:
+//   H'  = -sum x sc |u|,                    x = a g / (1 - a g)
+//   H'' = sum (+-) x sc^2 (1 - 2 ln2 u^2 (1 + x))   (+ in front of the peak)
+// with u = (t - t_peak) sc and g = exp2(-u^2) as in bisect_step.  A lane is
+// done when the Newton step |H / H'| <= kRefineTol max(t, 1), and keeps the
+// result when the root is well conditioned (|H'| kRefineTol max(t, 1) >=
+// kHNoise); lanes not done after kRefineWalks walks, ill-conditioned lanes
+// and waves that fail the smoothness test run the reference's passes 3-5
+// from the unchanged pass-2 cell (the root of a T that stays within rounding
+// of 1/2 over a stretch is decided by rounding: there only the reference's
+// own sample grid reproduces its answer).  Measured on C3 contributor sets
+// (tools/sim/median_sim.c): 2.0 walks per lane on average, max |refined -
+// bisected| = 2.4e-7, 1 lane in 50k left to the passes.
+constexpr int kRefineWalks = 3;
+constexpr float kRefineTol = 1e-6f;
+constexpr float kSmoothCells = 4.f;  // max rsigma * (pass-2 cell width) for the refinement
+constexpr float kTwoLn2 = 1.38629436111989061883f;
+constexpr float kHNoise = 1e-5f;  // rounding noise assumed in log2 T (~10x a 64-factor product's)
+
+__device__ __forceinline__ void refine_step(float& A, float& B, float& D, float& E, float t, float alpha,
+                                            float t_peak, float sc, float bm) {
+    const float om = 1.f - alpha;
+    const float u = __builtin_fmaf(t, sc, -t_peak * sc);
+    const float u2 = u * u;
+    const float ag = (alpha * bm) * __builtin_amdgcn_exp2f(-u2);
+    const float omg = 1.f - ag;
+    const bool behind = t > t_peak;
+    A *= behind ? om : omg;
+    B *= omg;
+    const float x = ag * __builtin_amdgcn_rcpf(omg);
+    const float xs = x * sc;
+    D = __builtin_fmaf(xs, fabsf(u), D);
+    const float e = (xs * sc) * __builtin_fmaf(-kTwoLn2 * u2, 1.f + x, 1.f);
+    E += behind ? -e : e;
+}
+
 // Diagnostic counters (STATS builds only, option GSR_OPT_RENDER_STATS):
 // [0] bisection wave-steps and [1] active lanes on the per-lane (resident)
 // walk; [2] active lanes in passes 2-5 and [3] those whose whole window is
-// more than kFarDelta sigma from the splat's peak (exact-constant factors).
+// more than kFarDelta sigma from the splat's peak (exact-constant factors);
+// [4] waves refined, [5] resident waves failing the smoothness test,
+// [6] refinement lane-walks, [7] lanes left to passes 3-5 after refining.
 __device__ unsigned long long g_render_stats[8];
 
 // SAMPLE: queries at arbitrary points — lanes hold points of one tile's
@@ -320,7 +367,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     float mDepth = 0.f, md_out = 0.f, md_dT = 0.f;
     bool md_ok = false, md_in_range = false;
     if constexpr (GEOM) {
-        unsigned long long st[4] = {0, 0, 0, 0};
+        unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float Tp[kSplit + 1];
         float dmin = fmaxf(m_init - a.sample_range, 0.f);
         float dmax = fmaxf(m_init + a.sample_range, 0.f);
@@ -354,6 +401,9 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         // from the lane's mask and folds the (1 - a) of those behind the
         // window into far_A, the starting value of A in passes 3-5.
         float far_A = 1.f;
+        float smax = 0.f;       // (pass 2) largest rsigma among the contributors kept for passes 3-5
+        bool refined = false;   // median depth found by the refinement (passes 3-5 skipped)
+        float t_ref = 0.f;
         auto pass = [&](auto first_c, auto prune_c) {
             constexpr bool FIRST = decltype(first_c)::value;
             constexpr bool prune = decltype(prune_c)::value;
@@ -378,7 +428,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             if (resident) {
                 // per-lane walk over the blended contributors, increasing index
                 // (same multiplication order as the reference's c = 1..last loop)
-                const int nwords = in_range ? (int)((last + 31) >> 5) : 0;
+                const int nwords = (in_range && !refined) ? (int)((last + 31) >> 5) : 0;
                 int w = 0;
                 uint32_t bits = nwords ? my_mask[0] : 0u;
                 uint32_t keep = 0u;  // (prune) near contributors of word w
@@ -425,6 +475,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                         const bool front = ball && (ts[kSplit] - t_peak) * w2.y < -kFarDelta;
                         far_A *= behind ? 1.f - alpha : 1.f;
                         keep |= (behind || front) ? 0u : jbit;
+                        // steepest contributor that can reach the window (a non-ball splat is a step)
+                        if (!(behind || front)) smax = fmaxf(smax, ball ? w2.y : __builtin_inff());
                     }
                     bisect_step<NP, HAS1, SKIP>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
                 }
@@ -479,16 +531,74 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         };
         if (a.passes > 0) pass(std::true_type{}, std::false_type{});
         if (a.passes > 1) pass(std::false_type{}, std::integral_constant<bool, kPruneAfterPass2>{});
+        static_assert(kPruneAfterPass2, "the refinement's smoothness test is computed by the pruning pass");
+        if (a.refine && a.passes > 2 && resident) {
+            const bool smooth = !in_range || smax * (dmax - dmin) <= kSmoothCells;
+            if (__all(smooth)) {
+                if constexpr (STATS) {
+                    if ((tid & 63) == 0) st[4] += 1;
+                }
+                // bracket: the pass-2 cell, H(lo) >= 0 >= H(hi); start at the secant root of H
+                float lo = dmin, hi = dmax;
+                const float Hlo = __builtin_amdgcn_logf(Tp[0]) + 1.f;
+                const float Hhi = __builtin_amdgcn_logf(Tp[kSplit]) + 1.f;
+                float wsec = Hlo / (Hlo - Hhi);
+                wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
+                float t = __builtin_fmaf(wsec, hi - lo, lo);
+                const float tol = kRefineTol * fmaxf(t, 1.f);
+                bool live = in_range;
+                for (int k = 0; k < kRefineWalks; k++) {
+                    if (__ballot(live) == 0ull) break;
+                    float A = far_A, B = 1.f, D = 0.f, E = 0.f;
+                    const int nwords = live ? (int)((last + 31) >> 5) : 0;
+                    for (int w = 0; w < nwords; w++) {
+                        uint32_t bits = my_mask[w * kTilePixels];
+                        while (bits) {
+                            const int j = (w << 5) + __builtin_ctz(bits);
+                            bits &= bits - 1u;
+                            const float4 w0 = c_w0[j];
+                            const float dx = w0.x - pixx, dy = w0.y - pixy;
+                            const float4 w1 = c_w1[j];
+                            const float alpha = fminf(0.99f, w1.y * __expf(splat_power(w0, w1, dx, dy)));
+                            const float4 w2 = c_w2[j];
+                            refine_step(A, B, D, E, t, alpha, splat_tpeak(w1, w2, dx, dy), w2.z, w2.w);
+                        }
+                    }
+                    if (live) {
+                        if constexpr (STATS) st[6] += 1;
+                        const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
+                        if (H >= 0.f) lo = t;
+                        else hi = t;
+                        // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
+                        float tn = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
+                        if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
+                        const bool done = (D > 0.f && fabsf(H) <= tol * D) || hi - lo <= tol;
+                        t = tn;
+                        if (done) {
+                            // accepted only where the root is well conditioned: rounding noise of
+                            // ~kHNoise in log2 T moves it by less than tol (T flat near 1/2 — a
+                            // pixel between two splats' peaks — leaves it to the reference's passes)
+                            refined = D * tol >= kHNoise;
+                            t_ref = tn;
+                            live = false;
+                        }
+                    }
+                }
+                if constexpr (STATS) st[7] += live ? 1 : 0;
+            } else if constexpr (STATS) {
+                if ((tid & 63) == 0) st[5] += 1;
+            }
+        }
 #pragma unroll 1
         for (int it = 2; it < a.passes; it++) pass(std::false_type{}, std::false_type{});
         if constexpr (STATS) {
-            for (int q = 0; q < 4; q++)
+            for (int q = 0; q < 8; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
         }
         float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
         w_max = fminf(fmaxf(w_max, 0.f), 1.f);  // __saturatef (NaN -> 0)
         const float w_min = 1.f - w_max;
-        mDepth = in_range ? __builtin_fmaf(w_max, dmax, w_min * dmin) : 0.f;
+        mDepth = in_range ? (refined ? t_ref : __builtin_fmaf(w_max, dmax, w_min * dmin)) : 0.f;
         md_in_range = in_range;
 
         // The backward's median-depth pre-pass (render_backward.cu:835-880),
@@ -614,6 +724,7 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.out_normal = out_normal;
     a.out_mdepth = out_mdepth;
     a.sample_range = kSampleRange;
+    a.refine = option(kOptNoRefine) ? 0 : 1;
     {
         const int np = option(kOptBisectPasses);
         a.passes = (np > 0 && np < kSplitIterations) ? np : kSplitIterations;
@@ -651,6 +762,7 @@ hipError_t launch_point_fwd(int query, const FwdParams& p, const GeomState& gs, 
     a.passes = query == kQuerySDF ? kSplitIterations + 1 : kSplitIterations;
     a.sample_range = query == kQuerySDF ? kSampleRange * 2.f : kSampleRange;
     a.query = query;
+    a.refine = option(kOptNoRefine) ? 0 : 1;
     a.pt_t = ps.t;
     a.out_sdf = out1;
     a.num_chunks = num_chunks;

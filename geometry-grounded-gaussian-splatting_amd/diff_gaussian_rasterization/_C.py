@@ -42,6 +42,9 @@ class AdamGroup(ctypes.Structure):
                 ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_longlong), ("lr", ctypes.c_double)]
 
 
+# include/gsr.h ABI these bindings are written for (gsr_abi_version)
+ABI_VERSION = 8
+
 
 def _load():
     global _lib
@@ -52,6 +55,10 @@ def _load():
                            "or __graft_entry__.build()")
     L = ctypes.CDLL(LIB_PATH)
     vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    L.gsr_abi_version.restype = i
+    if L.gsr_abi_version() != ABI_VERSION:  # the argtypes below are written for this ABI
+        raise RuntimeError(f"{LIB_PATH}: ABI {L.gsr_abi_version()}, expected {ABI_VERSION} (stale build? "
+                           "run `make -C geometry-grounded-gaussian-splatting_amd`)")
     L.gsr_rasterize_forward.restype = i
     L.gsr_rasterize_forward.argtypes = ([_ALLOC, vp] * 4 + [i] * 5 + [vp, i, i] + [vp] * 10 + [f] + [vp] * 3
                                         + [f] * 3 + [i] + [vp] * 5 + [i, i, vp, ctypes.POINTER(i)])
@@ -87,7 +94,6 @@ def _load():
     L.gsr_stage_name.restype = ctypes.c_char_p
     L.gsr_stage_name.argtypes = [i]
     L.gsr_last_error.restype = ctypes.c_char_p
-    L.gsr_abi_version.restype = i
     _lib = L
     return L
 
@@ -107,6 +113,7 @@ OPT_RENDER_STATS = 1
 OPT_BISECT_PASSES = 2
 OPT_BWD_NO_PREPASS = 3
 OPT_NO_TILE_ORDER = 4
+OPT_NO_REFINE = 5
 
 
 def debug_render_stats(reset: bool = True) -> list:

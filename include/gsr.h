@@ -321,8 +321,8 @@ const char* gsr_stage_name(int stage);
 
 /*
  * Process-wide switches selecting A/B variants of a kernel, for measuring one
- * against the other in the same process (all variants give bit-identical
- * results).  GSR_OPT_BISECT_SKIP (default 0): exact shortcut for bisection
+ * against the other in the same process (all variants but GSR_OPT_NO_REFINE
+ * give bit-identical results).  GSR_OPT_BISECT_SKIP (default 0): exact shortcut for bisection
  * samples far from a Gaussian's ray peak (render_fwd.hip; slower on the
  * fog-like benchmark scene, where most samples are near a peak).
  */
@@ -332,12 +332,16 @@ const char* gsr_stage_name(int stage);
  * XCD-contiguous tile order instead of heaviest-tile-first (backward). */
 /* GSR_OPT_BWD_NO_PREPASS (diagnostic): skip the backward's median-depth pre-pass
  * (its gradient terms are then wrong), to time it. */
+/* GSR_OPT_NO_REFINE (A/B, default 0): find the median depth with the reference's
+ * five bisection passes only, instead of two passes plus the bracketed Halley
+ * refinement (render_fwd.hip; results agree to ~1e-7 of the depth, not bitwise). */
 enum gsr_option {
     GSR_OPT_BISECT_SKIP = 0,
     GSR_OPT_RENDER_STATS = 1,
     GSR_OPT_BISECT_PASSES = 2,
     GSR_OPT_BWD_NO_PREPASS = 3,
-    GSR_OPT_NO_TILE_ORDER = 4
+    GSR_OPT_NO_TILE_ORDER = 4,
+    GSR_OPT_NO_REFINE = 5
 };
 int gsr_set_option(int opt, int value);
 /* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (8 values, see render_fwd.hip). */

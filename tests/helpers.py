@@ -11,7 +11,7 @@ import gsr_scene as S
 
 def small_case(P=40, W=40, H=24, seed=0, sh_degree=3, sg_degree=0, sgm=None, log_scale=math.log(0.12),
                opacity_max_logit=2.0, z_range=(2.0, 4.0), kernel_size=0.0, require_depth=True, cam=None,
-               bg=(0.0, 0.0, 0.0)):
+               bg=(0.0, 0.0, 0.0), flat=1.0):
     """A small random scene plus every argument of _C.rasterize_gaussians.
 
     Opacity logits are capped (sigmoid(2) = 0.88) so o*G < 0.99 and the
@@ -21,6 +21,8 @@ def small_case(P=40, W=40, H=24, seed=0, sh_degree=3, sg_degree=0, sgm=None, log
                            aspect=H / W, z_range=z_range, log_scale_mean=log_scale, log_scale_std=0.3,
                            opacity_std=1.0)
     raw.opacity.clamp_(max=opacity_max_logit)
+    if flat != 1.0:  # surfel-like Gaussians: one axis `flat` times thinner (steep vacancy steps)
+        raw.scaling[:, 2] -= math.log(flat)
     inp = S.activated_inputs(raw)
     inp = {k: v.detach().contiguous() for k, v in inp.items()}
     return dict(

@@ -1,0 +1,325 @@
+/*
+ * median_sim.c — development tool (not product, not the oracle): simulates
+ * median-depth root-finding strategies on real per-pixel contributor sets and
+ * compares them with the reference's 5 x 8-way bisection
+ * (render_forward.cu:549-645), counting per-wave walk steps so the GPU cost
+ * of each strategy can be estimated before writing it in HIP.
+ *
+ * Input: the oracle's geometry (means2D, conic_opacity, ray_planes) and
+ * binning (point_list, ranges) for the sampled tiles.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+
+#define SPLIT 8
+#define PASSES 5
+#define RANGE 0.4f
+
+typedef struct { float a, tp, rs; } contrib_t;
+
+/* vacancy transmittance at t (reference formula, fp32) */
+static float vac(const contrib_t* c, int n, float t) {
+    float T = 1.f;
+    for (int i = 0; i < n; i++) {
+        const int ball = c[i].rs > 0;
+        const float d = (t - c[i].tp) * c[i].rs;
+        const float g = ball ? expf(-0.5f * d * d) : 0.f;
+        const float omg = 1.f - c[i].a * g;
+        T *= (t > c[i].tp ? 1.f - c[i].a : omg) * (1.f / sqrtf(omg));
+    }
+    return T;
+}
+
+/* log T and d log T / dt (h' as in the backward's dT/dtm / T, render_backward.cu:866-877) */
+static void vac_d(const contrib_t* c, int n, float t, float* logT, float* dlog) {
+    float A = 1.f, B = 1.f, D = 0.f;
+    for (int i = 0; i < n; i++) {
+        const int ball = c[i].rs > 0;
+        const float d = (t - c[i].tp) * c[i].rs;
+        const float g = ball ? expf(-0.5f * d * d) : 0.f;
+        const float ag = c[i].a * g;
+        const float omg = 1.f - ag;
+        A *= t > c[i].tp ? 1.f - c[i].a : omg;
+        B *= omg;
+        if (ball) D += -0.5f * ag / omg * fabsf(d) * c[i].rs;
+    }
+    *logT = logf(A) - 0.5f * logf(B);
+    *dlog = D;
+}
+
+static float ref_bisect(const contrib_t* c, int n, float m0, float Tfinal, int* in_range_out) {
+    float Tp[SPLIT + 1];
+    float lo = fmaxf(m0 - RANGE, 0.f), hi = fmaxf(m0 + RANGE, 0.f);
+    int in_range = Tfinal <= 0.45f;
+    for (int it = 0; it < PASSES; it++) {
+        const int first = it == 0;
+        const float iv = (hi - lo) * (1.f / SPLIT);
+        for (int s = first ? 0 : 1; s < (first ? SPLIT + 1 : SPLIT); s++) Tp[s] = vac(c, n, lo + iv * s);
+        if (first) in_range = Tp[0] >= 0.5f && Tp[SPLIT] <= 0.5f && in_range;
+        int sid = 0;
+        for (int p = 1; p < SPLIT; p++) sid = Tp[p] >= 0.5f ? p : sid;
+        hi = lo + (sid + 1) * iv;
+        lo = lo + sid * iv;
+        Tp[0] = Tp[sid];
+        Tp[SPLIT] = Tp[sid + 1];
+    }
+    float w = (Tp[0] - 0.5f) / (Tp[0] - Tp[SPLIT]);
+    w = (w != w) ? 0.f : fminf(fmaxf(w, 0.f), 1.f);
+    *in_range_out = in_range;
+    return in_range ? w * hi + (1.f - w) * lo : 0.f;
+}
+
+/* Strategy: `npass` reference 8-way passes, then bracketed Newton on log T.
+ * Returns the depth; *walks = Newton walks used; counts per-walk contributor
+ * counts into wk[] (0 when the lane is done). */
+static int g_halley = 0;
+int g_dbg = 0;
+static float g_sa, g_sb;
+static int g_sel = 0;
+static float g_smax = 1e30f;
+static float g_hnoise = 0.f;
+void sim_set_hnoise(float v) { g_hnoise = v; }
+void sim_set_pred(int sel, float smax) { g_sel = sel; g_smax = smax; }
+void sim_set_halley(int v) { g_halley = v; }
+/* h, h', h'' of h = log T + ln 2 */
+static void vac_d2(const contrib_t* c, int n, float t, float* hv, float* d1, float* d2) {
+    float A = 1.f, B = 1.f, D = 0.f, E = 0.f;
+    for (int i = 0; i < n; i++) {
+        const int ball = c[i].rs > 0;
+        const float d = (t - c[i].tp) * c[i].rs;
+        const float g = ball ? expf(-0.5f * d * d) : 0.f;
+        const float ag = c[i].a * g;
+        const float omg = 1.f - ag;
+        const int before = !(t > c[i].tp);
+        A *= before ? omg : 1.f - c[i].a;
+        B *= omg;
+        if (ball) {
+            const float x = ag / omg;
+            D += -0.5f * x * fabsf(d) * c[i].rs;
+            const float e = 0.5f * c[i].rs * c[i].rs * x * (1.f - d * d * (1.f + x));
+            E += before ? e : -e;
+        }
+    }
+    *hv = logf(A) - 0.5f * logf(B) + 0.69314718f;
+    *d1 = D;
+    *d2 = E;
+}
+static float newton_strategy(const contrib_t* c, int n, float m0, float Tfinal, int npass, float tol_rel,
+                             int maxit, int* walks, int* in_range_out, int* fell_back) {
+    float Tp[SPLIT + 1];
+    float lo = fmaxf(m0 - RANGE, 0.f), hi = fmaxf(m0 + RANGE, 0.f);
+    int in_range = Tfinal <= 0.45f;
+    *walks = 0;
+    *fell_back = 0;
+    for (int it = 0; it < npass; it++) {
+        const int first = it == 0;
+        const float iv = (hi - lo) * (1.f / SPLIT);
+        for (int s = first ? 0 : 1; s < (first ? SPLIT + 1 : SPLIT); s++) Tp[s] = vac(c, n, lo + iv * s);
+        if (first) in_range = Tp[0] >= 0.5f && Tp[SPLIT] <= 0.5f && in_range;
+        int sid = 0;
+        for (int p = 1; p < SPLIT; p++) sid = Tp[p] >= 0.5f ? p : sid;
+        hi = lo + (sid + 1) * iv;
+        lo = lo + sid * iv;
+        Tp[0] = Tp[sid];
+        Tp[SPLIT] = Tp[sid + 1];
+    }
+    *in_range_out = in_range;
+    {
+        float sa = 0.f, sb = 0.f;
+        const float wl = lo - (hi - lo) * 3.5f, wh = hi + (hi - lo) * 3.5f; /* pass-2 window */
+        for (int i = 0; i < n; i++) {
+            if (c[i].rs <= 0.f) continue;
+            const int near_cell = !((lo - c[i].tp) * c[i].rs > 6.f || (hi - c[i].tp) * c[i].rs < -6.f);
+            const int near_win = !((wl - c[i].tp) * c[i].rs > 6.f || (wh - c[i].tp) * c[i].rs < -6.f);
+            if (near_cell && c[i].rs > sa) sa = c[i].rs;
+            if (near_win && c[i].rs > sb) sb = c[i].rs;
+        }
+        g_sa = sa * (hi - lo);
+        g_sb = sb * (hi - lo);
+    }
+    if (!in_range) return 0.f;
+    const float lo2 = lo, hi2 = hi;
+    /* bracket [lo, hi]: T(lo) >= 0.5 >= T(hi) (h = log T + ln 2) */
+    float t;
+    if (npass == 0) {
+        /* walk 1 also gives T at the window ends (in_range) */
+        Tp[0] = vac(c, n, lo);
+        Tp[SPLIT] = vac(c, n, hi);
+        in_range = Tp[0] >= 0.5f && Tp[SPLIT] <= 0.5f && in_range;
+        *in_range_out = in_range;
+        if (!in_range) return 0.f;
+        t = fminf(fmaxf(m0, lo), hi);
+    } else {
+        float hlo = logf(Tp[0]) + 0.69314718f, hhi = logf(Tp[SPLIT]) + 0.69314718f;
+        float w = hlo / (hlo - hhi);
+        w = (w != w) ? 0.5f : fminf(fmaxf(w, 0.f), 1.f);
+        t = lo + w * (hi - lo);
+    }
+    const float tol = tol_rel * fmaxf(t, 1.f);
+    for (int k = 0; k < maxit; k++) {
+        float h, dh, d2 = 0.f;
+        vac_d2(c, n, t, &h, &dh, &d2);
+        (*walks)++;
+        if (h >= 0.f) lo = t; else hi = t;
+        float tn;
+        if (g_halley) {
+            const float den = 2.f * dh * dh - h * d2;
+            tn = den != 0.f ? t - 2.f * h * dh / den : 0.5f * (lo + hi);
+        } else {
+            tn = dh < 0.f ? t - h / dh : 0.5f * (lo + hi);
+        }
+        int bis = 0;
+        if (!(tn >= lo && tn <= hi)) { tn = 0.5f * (lo + hi); bis = 1; }
+        const float step = fabsf(tn - t);
+        t = tn;
+        if (bis) *fell_back += 1;
+        if (g_dbg) fprintf(stderr, "walk %d t=%.7f h=%g d1=%g d2=%g tn=%.7f lo=%.7f hi=%.7f\n", k, t, h, dh, d2, tn, lo, hi);
+        if ((dh < 0.f && fabsf(h) <= tol * -dh) || hi - lo <= tol) {
+            /* well-conditioned root only: ulp noise in log2 T (~kHNoise) must move it by < tol */
+            if (-dh / 0.69314718f * tol >= g_hnoise) return t;
+            break;
+        }
+    }
+    lo = lo2; hi = hi2; /* fallback: the reference's remaining passes from the pass-2 cell */
+    /* not converged: 8-way passes on the bracket down to the reference's final width */
+    {
+        const float wfinal = 2.f * RANGE / 32768.f;
+        float Tlo = Tp[0], Thi = Tp[SPLIT];
+        for (int it = npass; it < PASSES; it++) {
+            const float iv = (hi - lo) * (1.f / SPLIT);
+            float Tp[SPLIT + 1];
+            Tp[0] = Tlo; Tp[SPLIT] = Thi;
+            for (int s2 = 1; s2 < SPLIT; s2++) Tp[s2] = vac(c, n, lo + iv * s2);
+            int sid = 0;
+            for (int p = 1; p < SPLIT; p++) sid = Tp[p] >= 0.5f ? p : sid;
+            hi = lo + (sid + 1) * iv;
+            lo = lo + sid * iv;
+            Tlo = Tp[sid]; Thi = Tp[sid + 1];
+            if (g_dbg) fprintf(stderr, "fb sid %d lo=%.7f hi=%.7f Tlo=%g Thi=%g\n", sid, lo, hi, Tlo, Thi);
+            *walks += 100;
+        }
+        float w = (Tlo - 0.5f) / (Tlo - Thi);
+        w = (w != w) ? 0.f : fminf(fmaxf(w, 0.f), 1.f);
+        return w * hi + (1.f - w) * lo;
+    }
+}
+
+/* per-pixel composite over the tile list: blended set, T, m0 */
+static int composite(const uint32_t* list, int cnt, const float* xy, const float* co, const float* rp, float px,
+                     float py, contrib_t* out, float* Tfin, float* m0) {
+    float T = 1.f, mi = 0.f;
+    int n = 0;
+    for (int k = 0; k < cnt; k++) {
+        const uint32_t g = list[k];
+        const float dx = xy[2 * g] - px, dy = xy[2 * g + 1] - py;
+        const float* c4 = co + 4 * g;
+        const float power = -0.5f * (c4[0] * dx * dx + c4[2] * dy * dy) - c4[1] * dx * dy;
+        if (power > 0.f) continue;
+        const float alpha = fminf(0.99f, c4[3] * expf(power));
+        if (alpha < 1.f / 255.f) continue;
+        const float tT = T * (1.f - alpha);
+        if (tT < 1e-4f) break;
+        const float* r = rp + 4 * g;
+        const float t = r[0] * dx + r[1] * dy + r[2];
+        mi = T > 0.5f ? t : mi;
+        out[n].a = alpha;
+        out[n].tp = t;
+        out[n].rs = r[3];
+        n++;
+        T = tT;
+    }
+    *Tfin = T;
+    *m0 = mi;
+    return n;
+}
+
+/* stats: [0] pixels, [1] in_range, [2] max |d|, [4] sum walks, [5] ref cost, [6] strategy cost,
+ * [7] bisect fallbacks inside the walk loop, [8] in_range mismatches, [9] lanes needing the pass fallback,
+ * [10] sum blended, [11] non-ball, [12..27] walk histogram.
+ * Cost model per contributor-step: first pass 1.2, later pass 1.0, walk `wcost`. */
+void sim_run(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+             const uint32_t* point_list, const float* xy, const float* co, const float* rp, int npass,
+             float tol_rel, int maxit, float wcost, double* stats, float* md_ref_out, float* md_new_out) {
+    contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const uint32_t tx = tile % gx, ty = tile / gx;
+        const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
+        for (int wv = 0; wv < 4; wv++) {
+            int lane_n[64], lane_walks[64], lane_fb[64];
+            float lane_s[64];
+            int nmax = 0;
+            for (int l = 0; l < 64; l++) {
+                const int px = tx * 16 + (l & 15), py = ty * 16 + wv * 4 + (l >> 4);
+                lane_n[l] = lane_walks[l] = lane_fb[l] = 0;
+                lane_s[l] = 0.f;
+                const int pidx = ti * 256 + wv * 64 + l;
+                md_ref_out[pidx] = 0.f;
+                md_new_out[pidx] = 0.f;
+                if (px >= W || py >= H) continue;
+                float Tf, m0;
+                const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf,
+                                        &Tf, &m0);
+                stats[0] += 1;
+                stats[10] += n;
+                for (int i = 0; i < n; i++) stats[11] += buf[i].rs <= 0.f;
+                int ir1, ir2, walks, fb;
+                const float mr = ref_bisect(buf, n, m0, Tf, &ir1);
+                g_dbg = (px == 394 && py == 792);
+                const float mn = newton_strategy(buf, n, m0, Tf, npass, tol_rel, maxit, &walks, &ir2, &fb);
+                md_ref_out[pidx] = mr;
+                md_new_out[pidx] = mn;
+                stats[1] += ir1;
+                stats[8] += ir1 != ir2;
+                const double d = fabs((double)mr - mn);
+                if (d > stats[2]) stats[2] = d;
+                stats[4] += walks % 100;
+                stats[7] += fb;
+                stats[9] += walks >= 100;
+                stats[12 + (walks % 100 < 15 ? walks % 100 : 15)] += 1;
+                if (ir1) {
+                    const float sv = g_sel ? g_sb : g_sa;
+                    int b = sv <= 0.25f ? 0 : sv <= 0.5f ? 1 : sv <= 1.f ? 2 : sv <= 2.f ? 3 : sv <= 4.f ? 4 : 5;
+                    stats[32 + b * 3] += 1;
+                    stats[32 + b * 3 + 1] += walks >= 100;
+                    stats[32 + b * 3 + 2] += walks % 100;
+                    lane_s[l] = sv;
+                }
+                if (ir1) {
+                    lane_n[l] = n;
+                    lane_walks[l] = walks % 100;
+                    lane_fb[l] = walks / 100;
+                }
+                if (lane_n[l] > nmax) nmax = lane_n[l];
+            }
+            stats[5] += nmax * (1.2 + (PASSES - 1));
+            {
+                int smooth = 1;
+                for (int l = 0; l < 64; l++) smooth &= lane_s[l] <= g_smax;
+                stats[50] += smooth;
+                stats[51] += 1;
+                if (!smooth) {
+                    stats[6] += nmax * (1.2 + (PASSES - 1));
+                    continue;
+                }
+            }
+            stats[6] += npass > 0 ? nmax * (1.2 + (npass - 1)) : 0;
+            for (int k = 0; k < maxit; k++) {
+                int m = 0;
+                for (int l = 0; l < 64; l++)
+                    if (lane_walks[l] > k && lane_n[l] > m) m = lane_n[l];
+                stats[6] += m * wcost;
+            }
+            for (int k = 0; k < 4; k++) {
+                int m = 0;
+                for (int l = 0; l < 64; l++)
+                    if (lane_fb[l] > k && lane_n[l] > m) m = lane_n[l];
+                stats[6] += m;
+            }
+        }
+    }
+    free(buf);
+}
