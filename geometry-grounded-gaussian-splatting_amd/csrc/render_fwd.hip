@@ -404,6 +404,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         float smax = 0.f;       // (pass 2) largest rsigma among the contributors kept for passes 3-5
         bool refined = false;   // median depth found by the refinement (passes 3-5 skipped)
         float t_ref = 0.f;
+        float ref_t = 0.f, ref_D = 0.f, ref_E = 0.f;  // the last refinement walk's depth, -H', H''
         auto pass = [&](auto first_c, auto prune_c) {
             constexpr bool FIRST = decltype(first_c)::value;
             constexpr bool prune = decltype(prune_c)::value;
@@ -573,7 +574,6 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                         float tn = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
                         if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
                         const bool done = (D > 0.f && fabsf(H) <= tol * D) || hi - lo <= tol;
-                        t = tn;
                         if (done) {
                             // accepted only where the root is well conditioned: rounding noise of
                             // ~kHNoise in log2 T moves it by less than tol (T flat near 1/2 — a
@@ -581,7 +581,11 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                             refined = D * tol >= kHNoise;
                             t_ref = tn;
                             live = false;
+                            ref_t = t;
+                            ref_D = D;
+                            ref_E = E;
                         }
+                        t = tn;
                     }
                 }
                 if constexpr (STATS) st[7] += live ? 1 : 0;
@@ -618,7 +622,13 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         }
         float dT_dtm = 0.f;
         const bool want_dT = !SAMPLE || a.query == kQuerySample;
-        if (want_dT && resident && inside && mDepth_b != 0.f && last != 0) {
+        if (refined) {
+            // the reference's dT/dt_m (render_backward.cu:876) is T H' ln2 = H' ln2 / 2 at T = 1/2;
+            // continued to mDepth_b from the last walk: H'(t) = -D + E (t - ref_t) (|t - ref_t| <= a
+            // Newton step of kRefineTol max(t, 1); the next term is ~(step / sigma)^2 relative)
+            if (mDepth_b != 0.f)
+                dT_dtm = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(ref_E, mDepth_b - ref_t, -ref_D);
+        } else if (want_dT && resident && inside && mDepth_b != 0.f && last != 0) {
             const int nwords = (int)((last + 31) >> 5);
             for (int w = 0; w < nwords; w++) {
                 uint32_t bits = my_mask[w * kTilePixels];
