@@ -307,6 +307,29 @@ __global__ void __launch_bounds__(256)
     present[idx] = (V[2] * x + V[6] * y + V[10] * z + V[14]) > kNearPlane;
 }
 
+// prefiltered = true promises that every Gaussian passes the near-plane test
+// (in_frustum, CR/auxiliary.h:144-149, traps otherwise).  flag |= 1 when one
+// does not; the host reads it with K and reports the reference's message.
+__global__ void __launch_bounds__(256)
+    near_violation_kernel(int P, const float* __restrict__ means3D, const float* __restrict__ V,
+                          uint32_t* __restrict__ flag) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    bool culled = false;
+    if (idx < P) {
+        const float x = means3D[3 * idx], y = means3D[3 * idx + 1], z = means3D[3 * idx + 2];
+        culled = !((V[2] * x + V[6] * y + V[10] * z + V[14]) > kNearPlane);
+    }
+    if (__ballot(culled) != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+hipError_t launch_near_violation(int P, const float* means3D, const float* view, uint32_t* flag,
+                                 hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess || P == 0) return e;
+    hipLaunchKernelGGL(near_violation_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, P, means3D, view, flag);
+    return hipGetLastError();
+}
+
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t stream) {
     if (P == 0) return hipSuccess;

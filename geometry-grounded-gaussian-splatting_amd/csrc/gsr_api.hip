@@ -24,30 +24,33 @@ thread_local std::string g_last_error;
 // rasterizer_impl.cu:384) waits on an event recorded right after the counts
 // are copied into pinned host memory, not on the whole stream: work queued
 // behind the event (the depth sort) keeps the GPU busy while the host reads
-// K and allocates.  Per thread and device.
+// K and allocates.  One slot per (thread, device), created on first use and
+// kept: a thread that alternates devices never frees and re-allocates pinned
+// memory (hipHostFree / hipHostMalloc both synchronise).
 struct HostReadback {
-    int device = -1;
     uint32_t* pinned = nullptr;  // 8 words
     hipEvent_t ev = nullptr;
 };
-thread_local HostReadback g_readback;
+constexpr int kMaxReadbackDevices = 64;
+thread_local HostReadback g_readback[kMaxReadbackDevices];
 
 hipError_t readback_slot(HostReadback*& rb) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    rb = &g_readback;
-    if (rb->device == dev) return hipSuccess;
-    if (rb->ev) (void)hipEventDestroy(rb->ev);
-    if (rb->pinned) (void)hipHostFree(rb->pinned);
-    rb->ev = nullptr;
-    rb->pinned = nullptr;
-    rb->device = -1;
-    if ((e = hipHostMalloc(reinterpret_cast<void**>(&rb->pinned), 8 * sizeof(uint32_t), hipHostMallocDefault)) !=
-        hipSuccess)
+    if (dev < 0 || dev >= kMaxReadbackDevices) return hipErrorInvalidDevice;
+    rb = &g_readback[dev];
+    if (rb->pinned && rb->ev) return hipSuccess;
+    if (!rb->pinned &&
+        (e = hipHostMalloc(reinterpret_cast<void**>(&rb->pinned), 8 * sizeof(uint32_t), hipHostMallocDefault)) !=
+            hipSuccess) {
+        rb->pinned = nullptr;
         return e;
-    if ((e = hipEventCreateWithFlags(&rb->ev, hipEventDisableTiming)) != hipSuccess) return e;
-    rb->device = dev;
+    }
+    if (!rb->ev && (e = hipEventCreateWithFlags(&rb->ev, hipEventDisableTiming)) != hipSuccess) {
+        rb->ev = nullptr;
+        return e;
+    }
     return hipSuccess;
 }
 
@@ -89,6 +92,7 @@ size_t carve_geom(void* base, int P, GeomState& g) {
     g.radii = c.take<int>(P);
     g.clamped = c.take<uint8_t>(P);
     g.offsets_K = c.take<uint32_t>(1);
+    g.near_flag = c.take<uint32_t>(1);
     g.scan_tmp_bytes = scan_temp_bytes(P) > reduce_temp_bytes(P) ? scan_temp_bytes(P) : reduce_temp_bytes(P);
     g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
     g.dsort_tmp_bytes = depth_sort_temp_bytes(P);
@@ -421,6 +425,9 @@ const char* gsr_stage_name(int stage) {
 
 const char* gsr_last_error(void) { return g_last_error.c_str(); }
 
+// CR/auxiliary.h:146-148 (the reference traps the kernel)
+static const char* kPrefilteredMsg = "Point is filtered although prefiltered is set. This shouldn't happen!";
+
 int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
                           gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
                           int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
@@ -431,7 +438,6 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
                           const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
                           float* out_color, float* out_mdepth, float* out_alpha, float* out_normal, int* radii,
                           int require_depth, int debug, void* stream_ptr, int* num_rendered) {
-    (void)prefiltered;
     hipStream_t stream = (hipStream_t)stream_ptr;
     if (num_rendered) *num_rendered = 0;
     FwdParams p = make_params(P, sh_degree, SHM, sg_degree, SGM, background, width, height, means3D, colors_precomp,
@@ -471,6 +477,8 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     }
 
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, radii, stream), "preprocess");
+    if (prefiltered) GSR_TRY(launch_near_violation(P, means3D, viewmatrix, gs.near_flag, stream), "prefiltered check");
+    uint32_t near_flag = 0;
     const bool lists = list_binning(p.grid_x, p.grid_y);
     // K = the reference's instance count (rect tiles): returned as
     // num_rendered and the capacity of the binning buffer.  The sort path
@@ -482,20 +490,26 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
         GSR_TRY(readback_slot(rb), "pinned readback buffer");
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
         GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
+        if (prefiltered)
+            GSR_TRY(hipMemcpyAsync(rb->pinned + 1, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
+                    "memcpy prefiltered flag");
         GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
         Ks.x = rb->pinned[0];
+        if (prefiltered) near_flag = rb->pinned[1];
     } else {
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_live_counts(p, gs, radii, stream), "live counts");
         GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
         GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
-    }
-    if (!lists) {
+        if (prefiltered)
+            GSR_TRY(hipMemcpyAsync(&near_flag, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
+                    "memcpy prefiltered flag");
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
     }
+    if (near_flag) return fail(GSR_ERR_ARGS, kPrefilteredMsg);
     const uint32_t K = Ks.x, K_live = Ks.y;
     BinningState bs;
     void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, bs));
@@ -618,7 +632,6 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
                                float kernel_size, int prefiltered, float* output, float* output2, uint8_t* inside,
                                int debug, void* stream_ptr, int* num_rendered, int* num_points,
                                int* num_duplicated_tiles) {
-    (void)prefiltered;
     hipStream_t stream = (hipStream_t)stream_ptr;
     if (num_rendered) *num_rendered = 0;
     if (num_points) *num_points = 0;
@@ -658,6 +671,8 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     carve_point_binning(aligned_base(pbbuf), PN, tiles, pb);
 
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, gs.radii, stream), "preprocess");
+    if (prefiltered) GSR_TRY(launch_near_violation(P, means3D, viewmatrix, gs.near_flag, stream), "prefiltered check");
+    uint32_t near_flag = 0;
     const bool lists = list_binning(p.grid_x, p.grid_y);
     uint2 Ks = make_uint2(0u, 0u);
     uint32_t totals[4] = {0, 0, 0, 0};
@@ -672,10 +687,14 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
         GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
         GSR_TRY(hipMemcpyAsync(rb->pinned + 4, st.totals, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
                 "memcpy totals");
+        if (prefiltered)
+            GSR_TRY(hipMemcpyAsync(rb->pinned + 1, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
+                    "memcpy prefiltered flag");
         GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
         Ks.x = rb->pinned[0];
+        if (prefiltered) near_flag = rb->pinned[1];
         for (int k = 0; k < 4; k++) totals[k] = rb->pinned[4 + k];
     } else {
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
@@ -685,9 +704,13 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
         GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_setup(PN, tiles, pb, st, stream), "sample setup");
         GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
         GSR_TRY(hipMemcpyAsync(totals, st.totals, sizeof(totals), hipMemcpyDeviceToHost, stream), "memcpy totals");
+        if (prefiltered)
+            GSR_TRY(hipMemcpyAsync(&near_flag, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
+                    "memcpy prefiltered flag");
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "stream sync", e);
     }
+    if (near_flag) return fail(GSR_ERR_ARGS, kPrefilteredMsg);
     const uint32_t K = Ks.x, K_live = Ks.y, n_chunks = totals[2];
     BinningState bs;
     void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, bs));

@@ -71,6 +71,7 @@ struct GeomState {
     uint2* counts;                // per Gaussian in depth order: (tiles_touched, live tiles)
     uint2* offsets;               // inclusive scan of counts: .x -> K (reference count), .y -> live instances
     uint32_t* offsets_K;          // (tile-list path) K = sum of tiles_touched
+    uint32_t* near_flag;          // prefiltered check: 1 if a Gaussian fails the near-plane test
     int* radii;                   // internal copy when the caller passes radii == NULL
     uint8_t* clamped;             // bit c set: colour channel c was clamped at 0
     void* scan_tmp;

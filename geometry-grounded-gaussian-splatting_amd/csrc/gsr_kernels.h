@@ -170,6 +170,8 @@ hipError_t launch_depth_normal(bool backward, const float* depth, int H, int W, 
                                const float* g, float* out, uint8_t* valid, hipStream_t stream);
 
 // mark visible
+hipError_t launch_near_violation(int P, const float* means3D, const float* view, uint32_t* flag,
+                                 hipStream_t stream);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t stream);
 

@@ -29,7 +29,8 @@ def warp_patch_ncc(depths, normals, uvs, R, T, image_r, image_n, fx_r, fy_r, cx_
     dev = depths.device
     fopt = dict(dtype=torch.float32, device=dev)
     ncc = torch.empty(P, **fopt)
-    grad_depths = torch.empty_like(depths, dtype=torch.float32)
+    # contiguous, whatever the strides of `depths`: the kernel writes P floats in order
+    grad_depths = torch.empty(depths.shape, **fopt)
     grad_normals = torch.empty(P, 3, **fopt)
     valid = torch.empty(P, dtype=torch.bool, device=dev)
     if P == 0:

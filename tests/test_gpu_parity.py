@@ -240,6 +240,24 @@ def test_degenerate_scenes():
     _run(Hh.small_case(P=1, W=32, H=32, seed=3, z_range=(2.0, 2.5)))
 
 
+def test_prefiltered_contract():
+    """prefiltered=True promises no Gaussian fails the near-plane test; the
+    reference traps when one does (CR/auxiliary.h:146-149), here the call
+    raises with the reference's message.  A kept promise renders as usual."""
+    from diff_gaussian_rasterization import _C
+
+    c = Hh.small_case(P=300, W=64, H=48, seed=1)
+    ga = [_gpu(x) for x in Hh.oracle_args(c)] + [False]
+    ref = _C.rasterize_gaussians(*ga)
+    ga[22] = True  # prefiltered, every mean in front of the camera
+    out = _C.rasterize_gaussians(*ga)
+    assert out[0] == ref[0] and torch.equal(out[1], ref[1])
+    ga[1] = ga[1].clone()
+    ga[1][7, 2] = -1.0  # one Gaussian behind the camera
+    with pytest.raises(RuntimeError, match="prefiltered is set"):
+        _C.rasterize_gaussians(*ga)
+
+
 def test_mark_visible_matches_oracle():
     from diff_gaussian_rasterization import _C
 
