@@ -38,7 +38,6 @@
 namespace gsr {
 
 constexpr int kResident = 384;
-constexpr bool kPruneAfterPass2 = true;  // measured: 1.98 vs 2.18 ms render_fwd at C3
 constexpr int kMaskWords = kResident / 32;
 constexpr int kRecSlots = 3 * kResident > 4 * kTilePixels ? 3 * kResident : 4 * kTilePixels;
 
@@ -119,8 +118,11 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
     const f32x2 om2 = {om, om};
     if constexpr (SKIP) {
         const bool ball = rsig > 0.f;
-        const float d_lo = (TS[0].x - t_peak) * rsig;
-        const float d_hi = ((HAS1 ? T1 : TS[NP - 1].y) - t_peak) * rsig;
+        // the samples' extremes (T1 is the last sample of a pass, the middle probe of walk 1)
+        const float s_lo = HAS1 ? fminf(TS[0].x, T1) : TS[0].x;
+        const float s_hi = HAS1 ? fmaxf(TS[NP - 1].y, T1) : TS[NP - 1].y;
+        const float d_lo = (s_lo - t_peak) * rsig;
+        const float d_hi = (s_hi - t_peak) * rsig;
         if (ball && d_lo > kFarDelta) {
 #pragma unroll
             for (int k = 0; k < NP; k++) A[k] *= om2;
@@ -153,30 +155,39 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
     }
 }
 
-// Root refinement (after the reference's first two passes).  The vacancy
-// transmittance T(t) is continuous and non-increasing in t (each factor is
-// sqrt(1 - a g) in front of the splat's peak and (1 - a) / sqrt(1 - a g)
-// behind it), so the reference's 8-way bisection converges on the root of
-// T(t) = 1/2 and returns it within its final cell (0.8 / 8^5 = 2.4e-5 wide,
-// linearly interpolated: ~1e-8 from the root where T is smooth).  Where T is
-// smooth on the pass-2 cell (every contributor that can reach the cell spans
-// it with at most kSmoothCells of its sigmas; wave-uniform test) the root is
-// found instead by bracketed Halley steps on H(t) = log2 T(t) + 1:
-//   H'  = -sum x sc |u|,                    x = a g / (1 - a g)
-//   H'' = sum (+-) x sc^2 (1 - 2 ln2 u^2 (1 + x))   (+ in front of the peak)
-// with u = (t - t_peak) sc and g = exp2(-u^2) as in bisect_step.  A lane is
-// done when the Newton step |H / H'| <= kRefineTol max(t, 1), and keeps the
-// result when the root is well conditioned (|H'| kRefineTol max(t, 1) >=
-// kHNoise); lanes not done after kRefineWalks walks, ill-conditioned lanes
-// and waves that fail the smoothness test run the reference's passes 3-5
-// from the unchanged pass-2 cell (the root of a T that stays within rounding
-// of 1/2 over a stretch is decided by rounding: there only the reference's
-// own sample grid reproduces its answer).  Measured on C3 contributor sets
-// (tools/sim/median_sim.c): 2.0 walks per lane on average, max |refined -
-// bisected| = 2.4e-7, 1 lane in 50k left to the passes.
-constexpr int kRefineWalks = 3;
-constexpr float kRefineTol = 1e-6f;
-constexpr float kSmoothCells = 4.f;  // max rsigma * (pass-2 cell width) for the refinement
+// Root refinement.  The vacancy transmittance T(t) is continuous and
+// non-increasing in t (each factor is sqrt(1 - a g) in front of the splat's
+// peak and (1 - a) / sqrt(1 - a g) behind it), so the reference's 5-pass
+// 8-way bisection converges on the root of T(t) = 1/2 and returns it within
+// its final cell (0.8 / 8^5 = 2.4e-5 wide, linearly interpolated: ~1e-8 from
+// the root where T is smooth).  Here the root is found directly:
+//  1. one walk evaluates T at kProbes depths: the reference's window ends
+//     (its in_range test) and m0 + kProbeOffsets * SAMPLE_RANGE, which
+//     bracket the root tightly (on C3 the root is within 0.05 of m0 for 97%
+//     of pixels, within 0.2 for all);
+//  2. bracketed Halley steps on H(t) = log2 T(t) + 1 from the secant root of
+//     H in that bracket:
+//       H'  = -sum x sc |u|,                    x = a g / (1 - a g)
+//       H'' = sum (+-) x sc^2 (1 - 2 ln2 u^2 (1 + x))   (+ in front of the peak)
+//     with u = (t - t_peak) sc and g = exp2(-u^2) as in bisect_step.  A lane
+//     is done when the Newton step |H / H'| <= kRefineTol max(t, 1) (the
+//     Halley iterate after it is then ~(step / sigma)^2 closer still), and
+//     keeps the result where the root is well conditioned (|H'| kCondTol
+//     max(t, 1) >= kHNoise).
+// Lanes not done after kRefineWalks walks and ill-conditioned lanes run the
+// reference's 5 passes from its first window (the root of a T that stays
+// within rounding of 1/2 over a stretch is decided by rounding: there only
+// the reference's own sample grid reproduces its answer).  Measured on C3
+// contributor sets (tools/sim/s2_sim.py): 2.0 walks per lane, 2.27 per wave
+// (the slowest lane), max |refined - bisected| = 2.4e-7, no lane left to the
+// passes.  (The previous scheme ran the reference's first two passes and
+// refined from the pass-2 cell: one more 7-sample walk per contributor.)
+constexpr int kProbes = 11;
+__constant__ constexpr float kProbeOffsets[kProbes] = {0.f,    -0.5f,   -0.25f, -0.125f, -0.0625f, 0.f,
+                                                        0.0625f, 0.125f, 0.25f,  0.5f,    0.f};
+constexpr int kRefineWalks = 4;
+constexpr float kRefineTol = 3e-5f;
+constexpr float kCondTol = 1e-6f;   // conditioning threshold (as the previous scheme's tolerance)
 constexpr float kTwoLn2 = 1.38629436111989061883f;
 constexpr float kHNoise = 1e-5f;  // rounding noise assumed in log2 T (~10x a 64-factor product's)
 
@@ -198,11 +209,9 @@ __device__ __forceinline__ void refine_step(float& A, float& B, float& D, float&
 }
 
 // Diagnostic counters (STATS builds only, option GSR_OPT_RENDER_STATS):
-// [0] bisection wave-steps and [1] active lanes on the per-lane (resident)
-// walk; [2] active lanes in passes 2-5 and [3] those whose whole window is
-// more than kFarDelta sigma from the splat's peak (exact-constant factors);
-// [4] waves refined, [5] resident waves failing the smoothness test,
-// [6] refinement lane-walks, [7] lanes left to passes 3-5 after refining.
+// [0] per-lane walk wave-steps and [1] their active lanes; [2], [3] unused;
+// [4] waves running the refinement, [5] waves sending a lane to the
+// reference's passes, [6] refinement lane-walks, [7] lanes left to the passes.
 __device__ unsigned long long g_render_stats[8];
 
 // SAMPLE: queries at arbitrary points — lanes hold points of one tile's
@@ -369,8 +378,10 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     if constexpr (GEOM) {
         unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float Tp[kSplit + 1];
-        float dmin = fmaxf(m_init - a.sample_range, 0.f);
-        float dmax = fmaxf(m_init + a.sample_range, 0.f);
+        // the reference's first window (render_forward.cu:560-562)
+        const float win_lo = fmaxf(m_init - a.sample_range, 0.f);
+        const float win_hi = fmaxf(m_init + a.sample_range, 0.f);
+        float dmin = win_lo, dmax = win_hi;
         bool in_range = T <= kMinTransmittance;
         const bool resident = max_contrib <= (uint32_t)kResident;
         float4* c_w0 = s_rec;
@@ -393,26 +404,45 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             stage(0);
             __syncthreads();
         }
-        // one bisection pass; FIRST evaluates all 9 samples, later passes
-        // reuse the bracketing ends (render_forward.cu:560-645)
-        // Contributors whose whole pass-2 window lies more than 6 sigma from
-        // their peak have exactly constant factors in passes 3-5 (their
-        // windows nest inside it; see bisect_step SKIP): pass 2 drops them
-        // from the lane's mask and folds the (1 - a) of those behind the
-        // window into far_A, the starting value of A in passes 3-5.
-        float far_A = 1.f;
-        float smax = 0.f;       // (pass 2) largest rsigma among the contributors kept for passes 3-5
-        bool refined = false;   // median depth found by the refinement (passes 3-5 skipped)
+        // Per-lane walk over the LDS-resident records of the contributors the
+        // lane blended, in increasing index order (the reference's c = 1..last
+        // multiplication order); each lane advances through its own mask words.
+        auto lane_walk = [&](bool active, auto&& body) {
+            const int nwords = active ? (int)((last + 31) >> 5) : 0;
+            int w = 0;
+            uint32_t bits = nwords ? my_mask[0] : 0u;
+            while (true) {
+                while (bits == 0u && w + 1 < nwords) bits = my_mask[++w * kTilePixels];
+                if (bits == 0u) break;
+                const int j = (w << 5) + __builtin_ctz(bits);
+                bits &= bits - 1u;
+                if constexpr (STATS) {
+                    const unsigned long long m = __ballot(1);
+                    if ((tid & 63) == __builtin_ctzll(m)) {
+                        st[0] += 1;
+                        st[1] += __popcll(m);
+                    }
+                }
+                const float4 w0 = c_w0[j];
+                const float dx = w0.x - pixx, dy = w0.y - pixy;
+                const float4 w1 = c_w1[j];
+                const float alpha = fminf(0.99f, w1.y * __expf(splat_power(w0, w1, dx, dy)));
+                const float4 w2 = c_w2[j];
+                body(alpha, splat_tpeak(w1, w2, dx, dy), w2);
+            }
+        };
+        bool refined = false;   // median depth found by the root refinement
         float t_ref = 0.f;
         float ref_t = 0.f, ref_D = 0.f, ref_E = 0.f;  // the last refinement walk's depth, -H', H''
-        auto pass = [&](auto first_c, auto prune_c) {
+        // one pass of the reference's bisection (render_forward.cu:560-645) over
+        // the lanes still in range and not refined; FIRST evaluates all 9
+        // samples, later passes reuse the bracketing ends
+        auto pass = [&](auto first_c) {
             constexpr bool FIRST = decltype(first_c)::value;
-            constexpr bool prune = decltype(prune_c)::value;
             constexpr int START = FIRST ? 0 : 1;
             constexpr int END = FIRST ? kSplit + 1 : kSplit;
             constexpr int NP = (END - START) / 2;
             constexpr bool HAS1 = ((END - START) & 1) != 0;
-            const float a0 = FIRST || prune ? 1.f : far_A;
             const float interval = (dmax - dmin) * (1.f / (float)kSplit);
             float ts[kSplit + 1];
 #pragma unroll
@@ -421,69 +451,15 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
 #pragma unroll
             for (int k = 0; k < NP; k++) {
                 TS[k] = f32x2{ts[START + 2 * k], ts[START + 2 * k + 1]};
-                A[k] = f32x2{a0, a0};
+                A[k] = f32x2{1.f, 1.f};
                 B[k] = f32x2{1.f, 1.f};
             }
-            float A1 = a0, B1 = 1.f;
+            float A1 = 1.f, B1 = 1.f;
             const float T1 = ts[END - 1];
             if (resident) {
-                // per-lane walk over the blended contributors, increasing index
-                // (same multiplication order as the reference's c = 1..last loop)
-                const int nwords = (in_range && !refined) ? (int)((last + 31) >> 5) : 0;
-                int w = 0;
-                uint32_t bits = nwords ? my_mask[0] : 0u;
-                uint32_t keep = 0u;  // (prune) near contributors of word w
-                while (true) {
-                    while (bits == 0u && w + 1 < nwords) {
-                        if constexpr (prune) {
-                            my_mask[w * kTilePixels] = keep;
-                            keep = 0u;
-                        }
-                        bits = my_mask[++w * kTilePixels];
-                    }
-                    if (bits == 0u) break;
-                    const int j = (w << 5) + __builtin_ctz(bits);
-                    const uint32_t jbit = bits & (0u - bits);
-                    bits &= bits - 1u;
-                    if constexpr (STATS) {
-                        const unsigned long long m = __ballot(1);
-                        if ((tid & 63) == __builtin_ctzll(m)) {
-                            st[0] += 1;
-                            st[1] += __popcll(m);
-                        }
-                    }
-                    const float4 w0 = c_w0[j];
-                    const float dx = w0.x - pixx, dy = w0.y - pixy;
-                    const float4 w1 = c_w1[j];
-                    const float power = splat_power(w0, w1, dx, dy);
-                    const float alpha = fminf(0.99f, w1.y * __expf(power));
-                    const float4 w2 = c_w2[j];
-                    const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                    if constexpr (STATS && !FIRST) {
-                        // lanes whose whole window is > kFarDelta sigma from the peak
-                        const float d_lo = (ts[1] - t_peak) * w2.y, d_hi = (ts[kSplit - 1] - t_peak) * w2.y;
-                        const bool far = w2.y > 0.f && (d_lo > kFarDelta || d_hi < -kFarDelta);
-                        const unsigned long long m = __ballot(1);
-                        const unsigned long long fm = __ballot(far);
-                        if ((tid & 63) == __builtin_ctzll(m)) {
-                            st[2] += __popcll(m);
-                            st[3] += __popcll(fm);
-                        }
-                    }
-                    if constexpr (!FIRST && prune) {
-                        const bool ball = w2.y > 0.f;
-                        const bool behind = ball && (ts[0] - t_peak) * w2.y > kFarDelta;
-                        const bool front = ball && (ts[kSplit] - t_peak) * w2.y < -kFarDelta;
-                        far_A *= behind ? 1.f - alpha : 1.f;
-                        keep |= (behind || front) ? 0u : jbit;
-                        // steepest contributor that can reach the window (a non-ball splat is a step)
-                        if (!(behind || front)) smax = fmaxf(smax, ball ? w2.y : __builtin_inff());
-                    }
+                lane_walk(in_range && !refined, [&](float alpha, float t_peak, float4 w2) {
                     bisect_step<NP, HAS1, SKIP>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
-                }
-                if constexpr (prune) {
-                    if (nwords) my_mask[w * kTilePixels] = keep;
-                }
+                });
             } else {
                 bool bdone = !in_range;
                 uint32_t c = 0;
@@ -514,7 +490,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 Tp[START + 2 * k + 1] = A[k].y * __builtin_amdgcn_rsqf(B[k].y);
             }
             if constexpr (HAS1) Tp[END - 1] = A1 * __builtin_amdgcn_rsqf(B1);
-            if (FIRST) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
+            // (refined lanes did not walk: their in_range stands)
+            if (FIRST && !refined) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
             int start_id = 0;
 #pragma unroll
             for (int p = 1; p < kSplit; p++) start_id = Tp[p] >= 0.5f ? p : start_id;
@@ -530,71 +507,117 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             Tp[0] = lo;
             Tp[kSplit] = hi;
         };
-        if (a.passes > 0) pass(std::true_type{}, std::false_type{});
-        if (a.passes > 1) pass(std::false_type{}, std::integral_constant<bool, kPruneAfterPass2>{});
-        static_assert(kPruneAfterPass2, "the refinement's smoothness test is computed by the pruning pass");
-        if (a.refine && a.passes > 2 && resident) {
-            const bool smooth = !in_range || smax * (dmax - dmin) <= kSmoothCells;
-            if (__all(smooth)) {
-                if constexpr (STATS) {
-                    if ((tid & 63) == 0) st[4] += 1;
-                }
-                // bracket: the pass-2 cell, H(lo) >= 0 >= H(hi); start at the secant root of H
-                float lo = dmin, hi = dmax;
-                const float Hlo = __builtin_amdgcn_logf(Tp[0]) + 1.f;
-                const float Hhi = __builtin_amdgcn_logf(Tp[kSplit]) + 1.f;
-                float wsec = Hlo / (Hlo - Hhi);
-                wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
-                float t = __builtin_fmaf(wsec, hi - lo, lo);
-                const float tol = kRefineTol * fmaxf(t, 1.f);
-                bool live = in_range;
-                for (int k = 0; k < kRefineWalks; k++) {
-                    if (__ballot(live) == 0ull) break;
-                    float A = far_A, B = 1.f, D = 0.f, E = 0.f;
-                    const int nwords = live ? (int)((last + 31) >> 5) : 0;
-                    for (int w = 0; w < nwords; w++) {
-                        uint32_t bits = my_mask[w * kTilePixels];
-                        while (bits) {
-                            const int j = (w << 5) + __builtin_ctz(bits);
-                            bits &= bits - 1u;
-                            const float4 w0 = c_w0[j];
-                            const float dx = w0.x - pixx, dy = w0.y - pixy;
-                            const float4 w1 = c_w1[j];
-                            const float alpha = fminf(0.99f, w1.y * __expf(splat_power(w0, w1, dx, dy)));
-                            const float4 w2 = c_w2[j];
-                            refine_step(A, B, D, E, t, alpha, splat_tpeak(w1, w2, dx, dy), w2.z, w2.w);
-                        }
-                    }
-                    if (live) {
-                        if constexpr (STATS) st[6] += 1;
-                        const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
-                        if (H >= 0.f) lo = t;
-                        else hi = t;
-                        // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
-                        float tn = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
-                        if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
-                        const bool done = (D > 0.f && fabsf(H) <= tol * D) || hi - lo <= tol;
-                        if (done) {
-                            // accepted only where the root is well conditioned: rounding noise of
-                            // ~kHNoise in log2 T moves it by less than tol (T flat near 1/2 — a
-                            // pixel between two splats' peaks — leaves it to the reference's passes)
-                            refined = D * tol >= kHNoise;
-                            t_ref = tn;
-                            live = false;
-                            ref_t = t;
-                            ref_D = D;
-                            ref_E = E;
-                        }
-                        t = tn;
-                    }
-                }
-                if constexpr (STATS) st[7] += live ? 1 : 0;
-            } else if constexpr (STATS) {
-                if ((tid & 63) == 0) st[5] += 1;
+        if (a.refine && resident && a.passes > 0) {
+            // Walk 1: the vacancy transmittance at kProbes depths — the window
+            // ends (the reference's in_range test, same sample arithmetic) and
+            // m0 + kProbeOffsets * SAMPLE_RANGE (clamped into the window), where
+            // the root almost always is.  Samples are in increasing order.
+            const float interval = (win_hi - win_lo) * (1.f / (float)kSplit);
+            const float e0 = win_lo, e8 = __builtin_fmaf(interval, (float)kSplit, win_lo);
+            float tp[kProbes];
+#pragma unroll
+            for (int s = 0; s < kProbes; s++) {
+                const float off = kProbeOffsets[s] * a.sample_range;
+                tp[s] = s == 0 ? e0 : s == kProbes - 1 ? e8 : fminf(fmaxf(m_init + off, e0), e8);
             }
-        }
+            // the m0 probe is the scalar sample, the others go in packed pairs
+            constexpr int NP = (kProbes - 1) / 2, MID = (kProbes - 1) / 2;
+            f32x2 A[NP], B[NP], TS[NP];
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                const int s0 = 2 * k < MID ? 2 * k : 2 * k + 1, s1 = 2 * k + 1 < MID ? 2 * k + 1 : 2 * k + 2;
+                TS[k] = f32x2{tp[s0], tp[s1]};
+                A[k] = f32x2{1.f, 1.f};
+                B[k] = f32x2{1.f, 1.f};
+            }
+            float A1 = 1.f, B1 = 1.f;
+            lane_walk(in_range, [&](float alpha, float t_peak, float4 w2) {
+                bisect_step<NP, true, SKIP>(A, B, TS, A1, B1, tp[MID], alpha, t_peak, w2.y, w2.z, w2.w);
+            });
+            float Tv[kProbes];
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                const int s0 = 2 * k < MID ? 2 * k : 2 * k + 1, s1 = 2 * k + 1 < MID ? 2 * k + 1 : 2 * k + 2;
+                Tv[s0] = A[k].x * __builtin_amdgcn_rsqf(B[k].x);
+                Tv[s1] = A[k].y * __builtin_amdgcn_rsqf(B[k].y);
+            }
+            Tv[MID] = A1 * __builtin_amdgcn_rsqf(B1);
+            in_range = (Tv[0] >= 0.5f) && (Tv[kProbes - 1] <= 0.5f) && in_range;
+            // bracket: the last probe with T >= 1/2 and the next one
+            int k1 = 0;
+#pragma unroll
+            for (int s = 1; s < kProbes - 1; s++) k1 = Tv[s] >= 0.5f ? s : k1;
+            float lo = tp[0], hi = tp[1], Tlo = Tv[0], Thi = Tv[1];
+#pragma unroll
+            for (int s = 1; s < kProbes - 1; s++) {
+                lo = k1 == s ? tp[s] : lo;
+                hi = k1 == s ? tp[s + 1] : hi;
+                Tlo = k1 == s ? Tv[s] : Tlo;
+                Thi = k1 == s ? Tv[s + 1] : Thi;
+            }
+            // bracketed Halley on H(t) = log2 T(t) + 1 from the secant root of H in the bracket
+            const float Hlo = __builtin_amdgcn_logf(Tlo) + 1.f;
+            const float Hhi = __builtin_amdgcn_logf(Thi) + 1.f;
+            float wsec = Hlo / (Hlo - Hhi);
+            wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
+            float t = __builtin_fmaf(wsec, hi - lo, lo);
+            const float scale = fmaxf(t, 1.f);
+            const float tol = kRefineTol * scale, tol_cond = kCondTol * scale;
+            bool live = in_range;
+            if constexpr (STATS) {
+                if ((tid & 63) == 0) st[4] += 1;
+            }
+            for (int k = 0; k < kRefineWalks && a.passes > 1; k++) {
+                if (__ballot(live) == 0ull) break;
+                float A = 1.f, B = 1.f, D = 0.f, E = 0.f;
+                lane_walk(live, [&](float alpha, float t_peak, float4 w2) {
+                    refine_step(A, B, D, E, t, alpha, t_peak, w2.z, w2.w);
+                });
+                if (live) {
+                    if constexpr (STATS) st[6] += 1;
+                    const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
+                    if (H >= 0.f) lo = t;
+                    else hi = t;
+                    // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
+                    float tn = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
+                    if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
+                    const bool done = (D > 0.f && fabsf(H) <= tol * D) || hi - lo <= tol;
+                    if (done) {
+                        // accepted only where the root is well conditioned: rounding noise of
+                        // ~kHNoise in log2 T moves it by less than tol_cond (T flat near 1/2 — a
+                        // pixel between two splats' peaks — leaves it to the reference's passes)
+                        refined = D * tol_cond >= kHNoise;
+                        t_ref = tn;
+                        live = false;
+                        ref_t = t;
+                        ref_D = D;
+                        ref_E = E;
+                    }
+                    t = tn;
+                }
+            }
+            if (a.passes == 1 && in_range) {  // diagnostic timing of walk 1 alone
+                refined = true;
+                t_ref = t;
+            }
+            // lanes left: the reference's passes from its first window
+            const bool left = in_range && !refined;
+            if constexpr (STATS) st[7] += left ? 1 : 0;
+            if (__ballot(left) != 0ull) {
+                if constexpr (STATS) {
+                    if ((tid & 63) == 0) st[5] += 1;
+                }
+                dmin = win_lo;
+                dmax = win_hi;
+                pass(std::true_type{});
 #pragma unroll 1
-        for (int it = 2; it < a.passes; it++) pass(std::false_type{}, std::false_type{});
+                for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{});
+            }
+        } else {
+            if (a.passes > 0) pass(std::true_type{});
+#pragma unroll 1
+            for (int it = 1; it < a.passes; it++) pass(std::false_type{});
+        }
         if constexpr (STATS) {
             for (int q = 0; q < 8; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
@@ -609,9 +632,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         // done here while the blended set is still in LDS: dT/dt_m at the
         // depth the backward will reconstruct from the mdepth output.  The
         // backward uses it when it receives that same mdepth (md_check) and
-        // recomputes it otherwise.  Contributors dropped after pass 2 are
-        // > 6 sigma from every depth of the final window: each of their terms
-        // is below 0.25 e^-18 6 rsigma < 3e-8 rsigma in magnitude.
+        // recomputes it otherwise.
         float mDepth_b;
         if constexpr (SAMPLE) {
             mDepth_b = mDepth;  // the sample backward reads the median depth itself (sample_backward.cu:135)
@@ -628,24 +649,12 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             // Newton step of kRefineTol max(t, 1); the next term is ~(step / sigma)^2 relative)
             if (mDepth_b != 0.f)
                 dT_dtm = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(ref_E, mDepth_b - ref_t, -ref_D);
-        } else if (want_dT && resident && inside && mDepth_b != 0.f && last != 0) {
-            const int nwords = (int)((last + 31) >> 5);
-            for (int w = 0; w < nwords; w++) {
-                uint32_t bits = my_mask[w * kTilePixels];
-                while (bits) {
-                    const int j = (w << 5) + __builtin_ctz(bits);
-                    bits &= bits - 1u;
-                    const float4 w0 = c_w0[j];
-                    const float dx = w0.x - pixx, dy = w0.y - pixy;
-                    const float4 w1 = c_w1[j];
-                    const float alpha = fminf(0.99f, w1.y * __expf(splat_power(w0, w1, dx, dy)));
-                    const float4 w2 = c_w2[j];
-                    const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                    const float t_delta = (mDepth_b - t_peak) * w2.y;
-                    const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
-                    dT_dtm += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
-                }
-            }
+        } else if (resident) {
+            lane_walk(want_dT && inside && mDepth_b != 0.f && last != 0, [&](float alpha, float t_peak, float4 w2) {
+                const float t_delta = (mDepth_b - t_peak) * w2.y;
+                const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
+                dT_dtm += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
+            });
         }
         md_dT = dT_dtm;
         md_ok = resident;

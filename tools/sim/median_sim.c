@@ -323,3 +323,166 @@ void sim_run(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint
     }
     free(buf);
 }
+
+/* near-set sizes: contributors within 6 sigma of the pass-1 window, of the
+ * pass-1 cell (pass-2 window) and of the pass-2 cell, plus those wholly in
+ * front of each (a (1 - a) factor).  out[0] pixels, [1] sum n, [2..4] near
+ * counts, [5..7] in-front counts, [8..10] wave-max near counts. */
+void sim_nearsets(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+                  const uint32_t* point_list, const float* xy, const float* co, const float* rp, double* out) {
+    contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const uint32_t tx = tile % gx, ty = tile / gx;
+        const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
+        for (int wv = 0; wv < 4; wv++) {
+            int wmax[3] = {0, 0, 0};
+            for (int l = 0; l < 64; l++) {
+                const int px = tx * 16 + (l & 15), py = ty * 16 + wv * 4 + (l >> 4);
+                if (px >= W || py >= H) continue;
+                float Tf, m0;
+                const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf, &Tf, &m0);
+                out[0] += 1;
+                out[1] += n;
+                float lo = fmaxf(m0 - RANGE, 0.f), hi = fmaxf(m0 + RANGE, 0.f);
+                float Tp[SPLIT + 1];
+                for (int it = 0; it < 3; it++) {
+                    int near = 0, front = 0;
+                    for (int i = 0; i < n; i++) {
+                        const float rs = buf[i].rs;
+                        const int beh = rs > 0 && (lo - buf[i].tp) * rs > 6.f;
+                        const int fr = rs > 0 && (hi - buf[i].tp) * rs < -6.f;
+                        near += !(beh || fr);
+                        front += beh;
+                    }
+                    out[2 + it] += near;
+                    out[5 + it] += front;
+                    if (near > wmax[it]) wmax[it] = near;
+                    if (it == 2) break;
+                    const float iv = (hi - lo) * (1.f / SPLIT);
+                    for (int s = 0; s <= SPLIT; s++) Tp[s] = vac(buf, n, lo + iv * s);
+                    int sid = 0;
+                    for (int p = 1; p < SPLIT; p++) sid = Tp[p] >= 0.5f ? p : sid;
+                    hi = lo + (sid + 1) * iv;
+                    lo = lo + sid * iv;
+                }
+            }
+            for (int k = 0; k < 3; k++) out[8 + k] += wmax[k];
+            out[11] += 1;
+        }
+    }
+    free(buf);
+}
+
+/* root - m0 per in-range pixel (out_d), the reference's median depth minus m0 */
+void sim_root_offsets(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+                      const uint32_t* point_list, const float* xy, const float* co, const float* rp, float* out_d,
+                      float* out_sig) {
+    contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const uint32_t tx = tile % gx, ty = tile / gx;
+        const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
+        for (int l = 0; l < 256; l++) {
+            const int px = tx * 16 + (l & 15), py = ty * 16 + (l >> 4);
+            out_d[ti * 256 + l] = NAN;
+            if (px >= W || py >= H) continue;
+            float Tf, m0;
+            const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf, &Tf, &m0);
+            int ir;
+            const float md = ref_bisect(buf, n, m0, Tf, &ir);
+            if (!ir) continue;
+            out_d[ti * 256 + l] = md - m0;
+            float sg = 0.f;
+            for (int i = 0; i < n; i++) if (buf[i].tp == m0) sg = buf[i].rs;
+            out_sig[ti * 256 + l] = sg;
+        }
+    }
+    free(buf);
+}
+
+/* Strategy S2: walk 1 evaluates T at the window ends (in_range) and at m0 + off[k] (nk offsets, sorted,
+ * one of them 0 where h, h', h'' are taken too); the bracket is the tightest pair of samples around the
+ * crossing; then bracketed Halley walks (one point each) until |h / h'| <= tol or the bracket is <= tol.
+ * Lanes not converged in maxit walks or ill-conditioned fall back to the reference's 5 passes.
+ * out: [0] in-range lanes, [1] sum walks (after walk 1), [2] fallbacks, [3] max |d|, [4] waves,
+ * [5] sum over waves of the max walks (fallback lanes counted as 100), [6..21] wave-max histogram,
+ * [22..37] lane walk hist, [40] in_range mismatches */
+void sim_s2(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+            const uint32_t* point_list, const float* xy, const float* co, const float* rp, int nk, const float* off,
+            float tol_rel, float tol_abs, int maxit, float hnoise, double* out) {
+    contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const uint32_t tx = tile % gx, ty = tile / gx;
+        const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
+        for (int wv = 0; wv < 4; wv++) {
+            int wmax = 0;
+            for (int l = 0; l < 64; l++) {
+                const int px = tx * 16 + (l & 15), py = ty * 16 + wv * 4 + (l >> 4);
+                if (px >= W || py >= H) continue;
+                float Tf, m0;
+                const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf, &Tf, &m0);
+                int ir;
+                const float mr = ref_bisect(buf, n, m0, Tf, &ir);
+                const float dmin = fmaxf(m0 - RANGE, 0.f), dmax = fmaxf(m0 + RANGE, 0.f);
+                const float T0 = vac(buf, n, dmin), T8 = vac(buf, n, dmax);
+                const int ir2 = T0 >= 0.5f && T8 <= 0.5f && Tf <= 0.45f;
+                out[40] += ir != ir2;
+                if (!ir2) continue;
+                out[0] += 1;
+                float lo = dmin, hi = dmax, hlo = logf(T0) + 0.69314718f, hhi = logf(T8) + 0.69314718f;
+                float h0 = 0, d1 = 0, d2 = 0, tm = fminf(fmaxf(m0, dmin), dmax);
+                for (int k = 0; k < nk; k++) {
+                    const float t = m0 + off[k];
+                    if (!(t > lo && t < hi)) continue;
+                    float h;
+                    if (off[k] == 0.f) { vac_d2(buf, n, t, &h, &d1, &d2); h0 = h; }
+                    else h = logf(vac(buf, n, t)) + 0.69314718f;
+                    if (h >= 0.f) { if (t > lo) { lo = t; hlo = h; } }
+                    else { if (t < hi) { hi = t; hhi = h; } }
+                }
+                /* re-tighten: samples in increasing order, so lo/hi are the last >= 0 / first < 0 only if
+                 * monotone; fine for the sim */
+                float t;
+                {
+                    const float den = 2.f * d1 * d1 - h0 * d2;
+                    t = den != 0.f ? tm - 2.f * h0 * d1 / den : 0.5f * (lo + hi);
+                    if (getenv("SIM_INIT") && atoi(getenv("SIM_INIT")) == 1) t = -1.f;
+                    if (!(t >= lo && t <= hi)) {
+                        float w = hlo / (hlo - hhi);
+                        w = (w != w) ? 0.5f : fminf(fmaxf(w, 0.f), 1.f);
+                        t = lo + w * (hi - lo);
+                    }
+                }
+                const float tol = fmaxf(tol_rel * fmaxf(t, 1.f), tol_abs);
+                int walks = 0, ok = 0;
+                float res = 0.f;
+                for (int k = 0; k < maxit; k++) {
+                    float h, dh, dd;
+                    vac_d2(buf, n, t, &h, &dh, &dd);
+                    walks++;
+                    if (h >= 0.f) lo = t; else hi = t;
+                    const float den = 2.f * dh * dh - h * dd;
+                    float tn = den != 0.f ? t - 2.f * h * dh / den : 0.5f * (lo + hi);
+                    if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
+                    if ((dh < 0.f && fabsf(h) <= tol * -dh) || hi - lo <= tol) {
+                        if (-dh * tol >= hnoise) { ok = 1; res = tn; }
+                        break;
+                    }
+                    t = tn;
+                }
+                if (!ok) { out[2] += 1; walks = 100; res = mr; }
+                else out[1] += walks;
+                out[22 + (walks < 15 ? walks : 15)] += 1;
+                const double d = fabs((double)res - mr);
+                if (d > out[3]) out[3] = d;
+                if (walks > wmax) wmax = walks;
+            }
+            out[4] += 1;
+            out[5] += wmax;
+            out[6 + (wmax < 15 ? wmax : 15)] += 1;
+        }
+    }
+    free(buf);
+}
