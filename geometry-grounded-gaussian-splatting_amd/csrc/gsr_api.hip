@@ -79,7 +79,15 @@ uint32_t higher_msb(uint32_t n) {
 
 using namespace gsr;
 
-size_t carve_geom(void* base, int P, GeomState& g) {
+// Binning path: the tile lists of tilelists.hip where the grid allows, else
+// the instance sort of binning.hip; the per-tile sort of sortbin.hip only on
+// request (GSR_OPT_SORTBIN: measured slower at C3).
+int bin_path(uint32_t gx, uint32_t gy) {
+    if (option(kOptSortbin) && sortbin_fits(gx, gy)) return kBinSortbin;
+    return list_binning(gx, gy) ? kBinLists : kBinInstanceSort;
+}
+
+size_t carve_geom(void* base, int P, uint32_t gx, uint32_t gy, GeomState& g) {
     Carver c(base);
     g.splats = c.take<Splat>(P);
     g.depths = c.take<float>(P);
@@ -97,20 +105,39 @@ size_t carve_geom(void* base, int P, GeomState& g) {
     g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
     g.dsort_tmp_bytes = depth_sort_temp_bytes(P);
     g.dsort_tmp = c.take<char>(g.dsort_tmp_bytes);
+    // (last: the fields above keep their offsets whichever path a call takes)
+    const size_t tiles = (size_t)gx * gy;
+    const bool sb = option(kOptSortbin) && sortbin_fits(gx, gy) && P > 0;
+    g.bin_hist = c.take<uint32_t>(sb ? (size_t)sortbin_blocks(P) * tiles : 0);
+    g.bin_total = c.take<uint32_t>(sb ? tiles : 0);
+    g.bin_start = c.take<uint32_t>(sb ? tiles + 1 : 0);
+    g.bin_info = c.take<uint32_t>(sb ? 4 : 0);
     return c.off + 256;
 }
 
 // Binning buffer.  The point list comes first, so its offset depends only on
 // the base (gsr_debug_binning carves it knowing K alone); the rest depends
 // on the path: tile lists (tilelists.hip) or emit + tile-id sort.
-size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, BinningState& b) {
+size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, int path, BinningState& b) {
     Carver c(base);
     b.point_list = c.take<uint32_t>(K);
     const int tiles = (int)(gx * gy);
     const int tile_bits = (int)higher_msb((uint32_t)tiles);
-    b.use_lists = list_binning(gx, gy);
+    b.path = path;
+    b.use_lists = path == kBinLists;
     b.key_bytes = tile_key_bytes(tile_bits);
-    if (b.use_lists) {
+    b.pairs = nullptr;
+    if (path == kBinSortbin) {
+        b.pairs = c.take<uint2>(K);
+        b.rows = nullptr;
+        b.qrec = nullptr;
+        b.rows_count = b.rows_off = b.segbase = b.tiles_count = b.tiles_off = nullptr;
+        b.list_tmp = nullptr;
+        b.keys_unsorted = b.keys = nullptr;
+        b.values_unsorted = nullptr;
+        b.sort_tmp = nullptr;
+        b.sort_tmp_bytes = 0;
+    } else if (b.use_lists) {
         b.lists = list_layout(P, K, gx, gy);
         b.rows = c.take<uint2>(K);
         b.qrec = c.take<uint4>((size_t)2 * P);
@@ -378,7 +405,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 8; }
+int gsr_abi_version(void) { return 9; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -450,9 +477,9 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     const int tiles = (int)(p.grid_x * p.grid_y);
 
     GeomState gs;
-    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, gs));
+    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, p.grid_x, p.grid_y, gs));
     if (!gbuf) return fail(GSR_ERR_ALLOC, "geometry buffer allocation failed");
-    carve_geom(aligned_base(gbuf), P, gs);
+    carve_geom(aligned_base(gbuf), P, p.grid_x, p.grid_y, gs);
     TileState ts{};
     void* tbuf = tile_alloc(tile_ctx, carve_tiles(nullptr, tiles, ts));
     if (!tbuf) return fail(GSR_ERR_ALLOC, "tile buffer allocation failed");
@@ -469,9 +496,9 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
         if (e == hipSuccess) e = hipMemsetAsync(ts.max_contrib, 0, sizeof(uint32_t) * tiles, stream);
         if (e != hipSuccess) return fail(GSR_ERR_HIP, "memset", e);
         BinningState bs;
-        void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, 0, 0, p.grid_x, p.grid_y, bs));
+        void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, 0, 0, p.grid_x, p.grid_y, kBinLists, bs));
         if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-        carve_binning(aligned_base(bbuf), 0, 0, p.grid_x, p.grid_y, bs);
+        carve_binning(aligned_base(bbuf), 0, 0, p.grid_x, p.grid_y, kBinLists, bs);
         GSR_TRY(launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
         return GSR_OK;
     }
@@ -479,13 +506,13 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, radii, stream), "preprocess");
     if (prefiltered) GSR_TRY(launch_near_violation(P, means3D, viewmatrix, gs.near_flag, stream), "prefiltered check");
     uint32_t near_flag = 0;
-    const bool lists = list_binning(p.grid_x, p.grid_y);
+    const int path = bin_path(p.grid_x, p.grid_y);
     // K = the reference's instance count (rect tiles): returned as
-    // num_rendered and the capacity of the binning buffer.  The sort path
-    // also needs K_live, the instances that survive tile culling.
+    // num_rendered and the capacity of the binning buffer.  The instance-sort
+    // path also needs K_live, the instances that survive tile culling.
     uint2 Ks = make_uint2(0u, 0u);
-    if (lists) {
-        // K depends on preprocess only: read it back while the depth sort runs
+    if (path != kBinInstanceSort) {
+        // K depends on preprocess only: one readback
         HostReadback* rb = nullptr;
         GSR_TRY(readback_slot(rb), "pinned readback buffer");
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
@@ -494,7 +521,10 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
             GSR_TRY(hipMemcpyAsync(rb->pinned + 1, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
                     "memcpy prefiltered flag");
         GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
-        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        // the GPU counts the tile lists (or sorts by depth) while the host waits
+        if (path == kBinSortbin)
+            GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_count(p, gs, radii, ts, stream), "tile counts");
+        if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
         Ks.x = rb->pinned[0];
         if (prefiltered) near_flag = rb->pinned[1];
@@ -512,10 +542,12 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     if (near_flag) return fail(GSR_ERR_ARGS, kPrefilteredMsg);
     const uint32_t K = Ks.x, K_live = Ks.y;
     BinningState bs;
-    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, bs));
+    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, path, bs));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, bs);
-    if (lists) {
+    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, path, bs);
+    if (path == kBinSortbin) {
+        GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_lists(p, gs, radii, bs, ts, stream), "tile lists");
+    } else if (path == kBinLists) {
         GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_list_binning(p, gs, radii, bs, ts, (int)K, stream), "tile lists");
     } else {
         const int tile_bits = (int)higher_msb((uint32_t)tiles);
@@ -587,9 +619,10 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
 
     const int tiles = (int)(b.f.grid_x * b.f.grid_y);
     GeomState gs;
-    carve_geom(aligned_base(const_cast<void*>(geom_buffer)), P, gs);
-    BinningState bs;
-    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, P, b.f.grid_x, b.f.grid_y, bs);
+    carve_geom(aligned_base(const_cast<void*>(geom_buffer)), P, b.f.grid_x, b.f.grid_y, gs);
+    BinningState bs;  // (the backward reads the point list only: first in every layout)
+    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, P, b.f.grid_x, b.f.grid_y,
+                  bin_path(b.f.grid_x, b.f.grid_y), bs);
     ImageState is;
     carve_image(aligned_base(const_cast<void*>(image_buffer)), width * height, is);
     TileState ts{};
@@ -653,9 +686,9 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     const uint32_t tiles = p.grid_x * p.grid_y;
 
     GeomState gs;
-    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, gs));
+    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, p.grid_x, p.grid_y, gs));
     if (!gbuf) return fail(GSR_ERR_ALLOC, "geometry buffer allocation failed");
-    carve_geom(aligned_base(gbuf), P, gs);
+    carve_geom(aligned_base(gbuf), P, p.grid_x, p.grid_y, gs);
     TileState ts{};
     SampleTiles st;
     void* tbuf = tile_alloc(tile_ctx, carve_sample_tiles(nullptr, (int)tiles, ts, st));
@@ -673,12 +706,12 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     GSR_STAGE(GSR_STAGE_PREPROCESS, launch_preprocess_fwd(p, gs, gs.radii, stream), "preprocess");
     if (prefiltered) GSR_TRY(launch_near_violation(P, means3D, viewmatrix, gs.near_flag, stream), "prefiltered check");
     uint32_t near_flag = 0;
-    const bool lists = list_binning(p.grid_x, p.grid_y);
+    const int path = bin_path(p.grid_x, p.grid_y);  // as the render forward
     uint2 Ks = make_uint2(0u, 0u);
     uint32_t totals[4] = {0, 0, 0, 0};
-    if (lists) {
-        // K and the point totals depend on preprocess and the points only:
-        // read them back while the depth sort runs (HostReadback)
+    if (path != kBinInstanceSort) {
+        // K, the tile list sizes and the point totals depend on preprocess and
+        // the points only: one readback (HostReadback)
         HostReadback* rb = nullptr;
         GSR_TRY(readback_slot(rb), "pinned readback buffer");
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
@@ -691,7 +724,10 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
             GSR_TRY(hipMemcpyAsync(rb->pinned + 1, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
                     "memcpy prefiltered flag");
         GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
-        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        // the GPU counts the tile lists (or sorts by depth) while the host waits
+        if (path == kBinSortbin)
+            GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_count(p, gs, gs.radii, ts, stream), "tile counts");
+        if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
         Ks.x = rb->pinned[0];
         if (prefiltered) near_flag = rb->pinned[1];
@@ -713,14 +749,16 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     if (near_flag) return fail(GSR_ERR_ARGS, kPrefilteredMsg);
     const uint32_t K = Ks.x, K_live = Ks.y, n_chunks = totals[2];
     BinningState bs;
-    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, bs));
+    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, path, bs));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, bs);
+    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, path, bs);
     ChunkState cs{};
     void* cbuf = dup_tile_alloc(dup_tile_ctx, carve_chunks(nullptr, n_chunks, cs));
     if (!cbuf) return fail(GSR_ERR_ALLOC, "duplicated-tile buffer allocation failed");
     carve_chunks(aligned_base(cbuf), n_chunks, cs);
-    if (lists) {
+    if (path == kBinSortbin) {
+        GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_lists(p, gs, gs.radii, bs, ts, stream), "tile lists");
+    } else if (path == kBinLists) {
         GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_list_binning(p, gs, gs.radii, bs, ts, (int)K, stream), "tile lists");
     } else {
         const int tile_bits = (int)higher_msb(tiles);
@@ -829,9 +867,10 @@ int gsr_sample_depth_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
     if (cov3D_precomp && !dL_dcov3D) return fail(GSR_ERR_ARGS, "missing cov3D gradient");
     const uint32_t tiles = b.f.grid_x * b.f.grid_y;
     GeomState gs;
-    carve_geom(aligned_base(const_cast<void*>(geom_buffer)), P, gs);
-    BinningState bs;
-    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, P, b.f.grid_x, b.f.grid_y, bs);
+    carve_geom(aligned_base(const_cast<void*>(geom_buffer)), P, b.f.grid_x, b.f.grid_y, gs);
+    BinningState bs;  // (the backward reads the point list only: first in every layout)
+    carve_binning(aligned_base(const_cast<void*>(binning_buffer)), R, P, b.f.grid_x, b.f.grid_y,
+                  bin_path(b.f.grid_x, b.f.grid_y), bs);
     PointState ps;
     carve_points(aligned_base(const_cast<void*>(point_buffer)), PN, ps);
     PointBinState pb;

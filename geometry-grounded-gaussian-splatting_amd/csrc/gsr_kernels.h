@@ -8,7 +8,7 @@ namespace gsr {
 
 // Run-time switches for A/B variants of one kernel in one process
 // (gsr_set_option in include/gsr.h); defaults are the shipped paths.
-enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kNumOptions = 8 };
+enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptSortbin = 7, kNumOptions = 8 };
 int option(int which);
 hipError_t read_render_stats(unsigned long long* out, bool reset);
 
@@ -82,6 +82,14 @@ size_t reduce_temp_bytes(int P);
 hipError_t launch_count_K(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
                                const TileState& ts, int K, hipStream_t stream);
+
+// sortbin.hip
+bool sortbin_fits(uint32_t gx, uint32_t gy);
+int sortbin_blocks(int P);
+hipError_t launch_sortbin_count(const FwdParams& p, const GeomState& gs, const int* radii, const TileState& ts,
+                                hipStream_t stream);
+hipError_t launch_sortbin_lists(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
+                                const TileState& ts, hipStream_t stream);
 
 // render_fwd.hip
 hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const ImageState& is,

@@ -40,6 +40,7 @@ struct RenderBwdArgs {
     float* acc;      // [P][16]
     float* acc_abs;  // [P]
     int skip_prepass;  // diagnostic (GSR_OPT_BWD_NO_PREPASS): time the kernel without the pre-pass
+    int no_cache;      // GSR_OPT_BWD_NO_CACHE: recompute dT/dt_m everywhere
     const uint32_t* tile_order;  // [tiles] launch order (heaviest first) or null: XCD-contiguous
 };
 
@@ -100,7 +101,7 @@ __device__ __forceinline__ PixIn load_pixel(const RenderBwdArgs& a, int px, int 
         const float md = a.mdepth[pix];
         r.mDepth = md * nrm;
         // the forward computed dT/dt_m for exactly this mdepth value
-        r.cached = a.md_check[pix] == __float_as_uint(md);
+        r.cached = !a.no_cache && a.md_check[pix] == __float_as_uint(md);
         r.dT_dtm = a.dT_dtm[pix];
     }
     return r;
@@ -353,6 +354,7 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.acc = ws.acc;
     a.acc_abs = ws.acc_abs;
     a.skip_prepass = option(kOptBwdNoPrepass);
+    a.no_cache = option(kOptBwdNoCache);
     a.tile_order = ws.tile_order;
     if (a.num_tiles == 0) return hipSuccess;
     if (p.require_depth)

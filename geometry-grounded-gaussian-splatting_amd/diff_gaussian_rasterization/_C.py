@@ -43,7 +43,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 def _load():
@@ -114,6 +114,8 @@ OPT_BISECT_PASSES = 2
 OPT_BWD_NO_PREPASS = 3
 OPT_NO_TILE_ORDER = 4
 OPT_NO_REFINE = 5
+OPT_BWD_NO_CACHE = 6
+OPT_SORTBIN = 7
 
 
 def debug_render_stats(reset: bool = True) -> list:

@@ -332,6 +332,12 @@ const char* gsr_stage_name(int stage);
  * XCD-contiguous tile order instead of heaviest-tile-first (backward). */
 /* GSR_OPT_BWD_NO_PREPASS (diagnostic): skip the backward's median-depth pre-pass
  * (its gradient terms are then wrong), to time it. */
+/* GSR_OPT_BWD_NO_CACHE (A/B, default 0): the backward recomputes dT/dt_m at every
+ * pixel in its pre-pass (render_backward.cu:835-880) instead of taking the
+ * forward's cached value. */
+/* GSR_OPT_SORTBIN (A/B, default 0): build the per-tile lists by per-tile LDS
+ * sorts of unordered bins (sortbin.hip) instead of the depth sort + stable
+ * counting passes (tilelists.hip); same lists, slower at 1080p. */
 /* GSR_OPT_NO_REFINE (A/B, default 0): find the median depth with the reference's
  * five bisection passes only, instead of two passes plus the bracketed Halley
  * refinement (render_fwd.hip; results agree to ~1e-7 of the depth, not bitwise). */
@@ -341,7 +347,9 @@ enum gsr_option {
     GSR_OPT_BISECT_PASSES = 2,
     GSR_OPT_BWD_NO_PREPASS = 3,
     GSR_OPT_NO_TILE_ORDER = 4,
-    GSR_OPT_NO_REFINE = 5
+    GSR_OPT_NO_REFINE = 5,
+    GSR_OPT_BWD_NO_CACHE = 6,
+    GSR_OPT_SORTBIN = 7
 };
 int gsr_set_option(int opt, int value);
 /* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (8 values, see render_fwd.hip). */

@@ -158,6 +158,45 @@ def test_parity_small(case):
     _run(Hh.small_case(kernel_size=ks, **case))
 
 
+def _with_depth_ties(c, n_tied):
+    """Gaussians n_tied..2 n_tied-1 get the means of 0..n_tied-1: bit-identical
+    depths, so the per-tile order of each pair is decided by the index alone
+    (the reference's stable sort, rasterizer_impl.cu:403-412)."""
+    m = c["inp"]["means3D"].clone()
+    m[n_tied:2 * n_tied] = m[:n_tied]
+    c["inp"]["means3D"] = m.contiguous()
+    return c
+
+
+@pytest.fixture(params=[0, 1], ids=["lists", "sortbin"])
+def binning(request):
+    """Both binning paths: the depth sort + stable counting passes
+    (tilelists.hip, default) and the per-tile sorts (sortbin.hip)."""
+    from diff_gaussian_rasterization import _C
+
+    _C.set_option(_C.OPT_SORTBIN, request.param)
+    yield request.param
+    _C.set_option(_C.OPT_SORTBIN, 0)
+
+
+def test_parity_depth_ties(binning):
+    _run(_with_depth_ties(Hh.small_case(P=600, W=64, H=48, seed=21), 250))
+
+
+def test_parity_binning_paths(binning):
+    _run(Hh.small_case(P=10000, W=256, H=256, seed=7, log_scale=math.log(0.03)))
+    _run(Hh.small_case(P=500, W=100, H=70, seed=2, kernel_size=0.1))
+
+
+def test_parity_long_tile_lists(binning):
+    """Tiles with ~20k live entries: longer than one workgroup's LDS sort
+    (sortbin.hip: > kSortLarge = 12288 entries, the global-memory per-tile
+    sort); with depth ties among them."""
+    c = _with_depth_ties(Hh.small_case(P=60000, W=32, H=32, seed=22, log_scale=math.log(0.1), z_range=(2.0, 3.0)),
+                         5000)
+    _run(c, check_bwd=False)
+
+
 def test_parity_surfels_forward():
     """1000x-flattened Gaussians (vacancy T(t) made of near-steps): forward
     parity at the 1e-4 bar.  The backward is not compared: there the fp32
@@ -312,8 +351,10 @@ def test_timing_api():
     _C.rasterize_gaussians(*ga)
     _C.timing_enable(False)
     st = _C.timing_collect()
-    for k in ("preprocess", "depth_order", "scan", "tile_lists", "render_fwd"):
-        assert st[k][1] == 1 and st[k][0] > 0, k
+    # (the sort binning of a 1080p-class grid has no separate depth order stage:
+    # tile_lists brackets its pre- and post-synchronisation launches)
+    for k in ("preprocess", "scan", "tile_lists", "render_fwd"):
+        assert st[k][1] >= 1 and st[k][0] > 0, k
     _C.timing_stages(["render_fwd"])
     _C.timing_enable(True)
     _C.rasterize_gaussians(*ga)
@@ -452,6 +493,38 @@ def test_c3_backward_linearity(c3):
             continue
         want = (x + 2 * y).double()
         err = float((z.double() - want).norm() / want.norm().clamp_min(1e-30))
+        assert err <= 1e-4, (name, err)
+
+
+def test_c3_cached_median_gradient(c3):
+    """The backward takes dT/dt_m from the forward (render_fwd.hip: the
+    refinement's last walk continued to the output depth) where the reference
+    recomputes it in a pre-pass (render_backward.cu:835-880).  At full C3 the
+    gradients with the cached value must match those of the recomputing
+    pre-pass (GSR_OPT_BWD_NO_CACHE) within the parity bar."""
+    from diff_gaussian_rasterization import _C
+
+    ga = [_gpu(x) for x in Hh.oracle_args(c3)] + [False]
+    out = _C.rasterize_gaussians(*ga)
+    K, color, alpha, normal, mdepth, radii = out[:6]
+    g = {k: v.to(DEV) for k, v in S.upstream_grads(1080, 1920, seed=3).items()}
+
+    def bwd():
+        return _C.rasterize_gaussians_backward(*ga[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], alpha,
+                                               normal, mdepth, _gpu(c3["cam"].camera_center), radii, out[6], K,
+                                               out[7], out[8], out[9], True, False)
+
+    cached = bwd()
+    try:
+        _C.set_option(_C.OPT_BWD_NO_CACHE, 1)
+        full = bwd()
+    finally:
+        _C.set_option(_C.OPT_BWD_NO_CACHE, 0)
+    for name, x, y in zip(GRAD_NAMES, cached, full):
+        if x.numel() == 0 or not bool(y.any()):
+            continue
+        err = float((x.double() - y.double()).norm() / y.double().norm())
+        print(name, err)
         assert err <= 1e-4, (name, err)
 
 

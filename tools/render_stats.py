@@ -1,0 +1,25 @@
+"""Print the render_fwd diagnostic counters (GSR_OPT_RENDER_STATS) at C3 (development tool)."""
+import math, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd")]
+import torch
+import gsr_scene as S
+from diff_gaussian_rasterization import _C
+
+dev = torch.device("cuda")
+W, H, P = 1920, 1080, 1_000_000
+cam = S.make_camera(W, H).to(dev)
+inp = {k: v.to(dev).contiguous() for k, v in S.activated_inputs(S.make_gaussians(P, aspect=H / W)).items()}
+E = torch.Tensor([])
+args = (torch.zeros(3, device=dev), inp["means3D"], E, inp["opacities"], inp["scales"], inp["rotations"], E,
+        inp["shs"], inp["sg_axis"], inp["sg_sharpness"], inp["sg_color"], 3, 0, 1.0, cam.world_view_transform,
+        cam.full_proj_transform, math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), 0.0, H, W, cam.camera_center,
+        False, True, False)
+_C.set_option(_C.OPT_RENDER_STATS, 1)
+_C.debug_render_stats(reset=True)
+_C.rasterize_gaussians(*args)
+torch.cuda.synchronize()
+st = _C.debug_render_stats(reset=True)
+_C.set_option(_C.OPT_RENDER_STATS, 0)
+print("walk wave-steps", st[0], "active lanes/step", round(st[1] / max(st[0], 1), 2))
+print("refine waves", st[4], "fallback waves", st[5], "refine lane-walks", st[6], "lanes left", st[7])

@@ -486,3 +486,137 @@ void sim_s2(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
     }
     free(buf);
 }
+
+/* |secant estimate - reference depth| and |Halley-from-secant - reference| after the probe walk (S2's walk 1) */
+void sim_secant_err(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+                    const uint32_t* point_list, const float* xy, const float* co, const float* rp, int nk,
+                    const float* off, float* out_sec, float* out_hal, float* out_quad) {
+    contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const uint32_t tx = tile % gx, ty = tile / gx;
+        const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
+        for (int l = 0; l < 256; l++) {
+            const int px = tx * 16 + (l & 15), py = ty * 16 + (l >> 4);
+            const int o = ti * 256 + l;
+            out_sec[o] = out_hal[o] = out_quad[o] = NAN;
+            if (px >= W || py >= H) continue;
+            float Tf, m0;
+            const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf, &Tf, &m0);
+            int ir;
+            const float mr = ref_bisect(buf, n, m0, Tf, &ir);
+            if (!ir) continue;
+            float ts[32], hs[32];
+            const float dmin = fmaxf(m0 - RANGE, 0.f), dmax = fmaxf(m0 + RANGE, 0.f);
+            int m = 0;
+            ts[m++] = dmin;
+            for (int k = 0; k < nk; k++) ts[m++] = fminf(fmaxf(m0 + off[k], dmin), dmax);
+            ts[m++] = dmax;
+            for (int k = 0; k < m; k++) hs[k] = logf(vac(buf, n, ts[k])) + 0.69314718f;
+            int k1 = 0;
+            for (int k = 1; k < m - 1; k++) if (hs[k] >= 0.f) k1 = k;
+            const float lo = ts[k1], hi = ts[k1 + 1];
+            float w = hs[k1] / (hs[k1] - hs[k1 + 1]);
+            w = (w != w) ? 0.5f : fminf(fmaxf(w, 0.f), 1.f);
+            const float t = lo + w * (hi - lo);
+            out_sec[o] = t - mr;
+            float h, d1, d2;
+            vac_d2(buf, n, t, &h, &d1, &d2);
+            const float den = 2.f * d1 * d1 - h * d2;
+            out_hal[o] = (den != 0.f ? t - 2.f * h * d1 / den : t) - mr;
+            /* inverse quadratic through 3 probes around the crossing */
+            int a0 = k1 > 0 ? k1 - 1 : 0;
+            if (a0 + 2 >= m) a0 = m - 3;
+            const float x0 = hs[a0], x1 = hs[a0 + 1], x2 = hs[a0 + 2];
+            const float y0 = ts[a0], y1 = ts[a0 + 1], y2 = ts[a0 + 2];
+            float q = y0 * x1 * x2 / ((x0 - x1) * (x0 - x2)) + y1 * x0 * x2 / ((x1 - x0) * (x1 - x2)) +
+                      y2 * x0 * x1 / ((x2 - x0) * (x2 - x1));
+            if (!(q >= lo && q <= hi)) q = t;
+            out_quad[o] = q - mr;
+        }
+    }
+    free(buf);
+}
+
+/* S3: probe walk, then alternating Halley walks (H, H', H'' at t -> tn) and verification walks (T at
+ * tn -+ eps: the root bracketed within eps of tn -> done, result = log-secant in [tn - eps, tn + eps]);
+ * a failed verification is followed by another Halley walk from tn.  maxit Halley walks.
+ * out: [0] lanes, [1] max |d|, [2] fallbacks, [3] waves, [4] sum wave cost (walk units: halley 1,
+ * verify vcost), [5..20] lane hist of halley walks */
+void sim_s3(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+            const uint32_t* point_list, const float* xy, const float* co, const float* rp, int nk, const float* off,
+            float eps_rel, int maxit, float hnoise, double* out, float* dout) {
+    contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const uint32_t tx = tile % gx, ty = tile / gx;
+        const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
+        for (int wv = 0; wv < 4; wv++) {
+            int seq[64];  /* per lane: number of (halley, verify) rounds used */
+            int nl = 0, wmax = 0;
+            for (int l = 0; l < 64; l++) {
+                const int px = tx * 16 + (l & 15), py = ty * 16 + wv * 4 + (l >> 4);
+                dout[ti * 256 + wv * 64 + l] = 0.f;
+                seq[l] = 0;
+                if (px >= W || py >= H) continue;
+                float Tf, m0;
+                const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf, &Tf, &m0);
+                int ir;
+                const float mr = ref_bisect(buf, n, m0, Tf, &ir);
+                if (!ir) continue;
+                out[0] += 1;
+                float ts[32], hs[32];
+                const float dmin = fmaxf(m0 - RANGE, 0.f), dmax = fmaxf(m0 + RANGE, 0.f);
+                int m = 0;
+                ts[m++] = dmin;
+                for (int k = 0; k < nk; k++) ts[m++] = fminf(fmaxf(m0 + off[k], dmin), dmax);
+                ts[m++] = dmax;
+                for (int k = 0; k < m; k++) hs[k] = logf(vac(buf, n, ts[k])) + 0.69314718f;
+                int k1 = 0;
+                for (int k = 1; k < m - 1; k++) if (hs[k] >= 0.f) k1 = k;
+                float lo = ts[k1], hi = ts[k1 + 1];
+                float w = hs[k1] / (hs[k1] - hs[k1 + 1]);
+                w = (w != w) ? 0.5f : fminf(fmaxf(w, 0.f), 1.f);
+                float t = lo + w * (hi - lo);
+                const float eps = eps_rel * fmaxf(t, 1.f);
+                int rounds = 0, ok = 0;
+                float res = 0.f;
+                for (int k = 0; k < maxit && !ok; k++) {
+                    float h, dh, dd;
+                    vac_d2(buf, n, t, &h, &dh, &dd);
+                    rounds++;
+                    if (h >= 0.f) lo = t; else hi = t;
+                    const float den = 2.f * dh * dh - h * dd;
+                    float tn = den != 0.f ? t - 2.f * h * dh / den : 0.5f * (lo + hi);
+                    if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
+                    /* verification walk */
+                    const float a = tn - eps, b = tn + eps;
+                    const float ha = logf(vac(buf, n, a)) + 0.69314718f, hb = logf(vac(buf, n, b)) + 0.69314718f;
+                    if (ha >= 0.f && hb < 0.f) {
+                        if (-dh * 1e-6f * fmaxf(t, 1.f) >= hnoise) {
+                            float ww = ha / (ha - hb);
+                            ww = (ww != ww) ? 0.5f : fminf(fmaxf(ww, 0.f), 1.f);
+                            res = a + ww * (b - a);
+                            ok = 1;
+                        }
+                        break;
+                    }
+                    if (ha >= 0.f) lo = fmaxf(lo, a); else hi = fminf(hi, a);
+                    if (hb >= 0.f) lo = fmaxf(lo, b); else hi = fminf(hi, b);
+                    t = tn;
+                }
+                if (!ok) { out[2] += 1; rounds = 100; res = mr; }
+                out[5 + (rounds < 15 ? rounds : 15)] += 1;
+                const double d = fabs((double)res - mr);
+                dout[ti * 256 + wv * 64 + l] = (float)d;
+                if (d > out[1]) out[1] = d;
+                seq[l] = rounds;
+                if (rounds > wmax) wmax = rounds;
+                nl++;
+            }
+            out[3] += 1;
+            out[4] += wmax;
+        }
+    }
+    free(buf);
+}
