@@ -37,7 +37,7 @@
 
 namespace gsr {
 
-constexpr int kResident = 384;
+constexpr int kResident = 352;  // (384 measured the same; 352 leaves LDS for the phase exchange)
 constexpr int kMaskWords = kResident / 32;
 constexpr int kRecSlots = 3 * kResident > 4 * kTilePixels ? 3 * kResident : 4 * kTilePixels;
 
@@ -185,6 +185,7 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
 constexpr int kProbes = 11;
 __constant__ constexpr float kProbeOffsets[kProbes] = {0.f,    -0.5f,   -0.25f, -0.125f, -0.0625f, 0.f,
                                                         0.0625f, 0.125f, 0.25f,  0.5f,    0.f};
+constexpr uint32_t kPubRefined = 1u, kPubOut = 2u;  // phase results: root found / not in range
 constexpr int kRefineWalks = 4;
 constexpr float kRefineTol = 3e-5f;
 constexpr float kCondTol = 1e-6f;   // conditioning threshold (as the previous scheme's tolerance)
@@ -209,7 +210,8 @@ __device__ __forceinline__ void refine_step(float& A, float& B, float& D, float&
 }
 
 // Diagnostic counters (STATS builds only, option GSR_OPT_RENDER_STATS):
-// [0] per-lane walk wave-steps and [1] their active lanes; [2], [3] unused;
+// [0] per-lane walk wave-steps and [1] their active lanes; [2] composite
+// wave-steps and [3] their blending lanes;
 // [4] waves running the refinement, [5] waves sending a lane to the
 // reference's passes, [6] refinement lane-walks, [7] lanes left to the passes.
 __device__ unsigned long long g_render_stats[8];
@@ -235,6 +237,12 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     __shared__ uint32_t s_mask[GEOM ? kTilePixels * kMaskWords : 1];
     __shared__ int s_alive[2][4];
     __shared__ uint32_t s_max[4];
+    // (render path, GEOM) the median-depth phases: per pixel the composite's last contributor,
+    // m0 and T, then the worker's result (flags, md_out, dT/dt_m); the grid pixels' roots
+    constexpr int kPub = (GEOM && !SAMPLE) ? kTilePixels : 1;
+    __shared__ uint32_t s_pub_last[kPub];
+    __shared__ float s_pub_m0[kPub], s_pub_T[kPub];
+    __shared__ float s_groot[(GEOM && !SAMPLE) ? 64 : 1];
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -294,6 +302,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     float N0 = 0.f, N1 = 0.f, N2 = 0.f, m_init = 0.f;
     bool done = !inside;
 
+    unsigned long long cst[2] = {0, 0};  // (STATS) composite wave-steps, blending lanes
     int toDo = total;
     for (int i = 0; i < rounds; i++, toDo -= kTilePixels) {
         // block-wide early exit: every wave publishes whether any lane is live
@@ -313,6 +322,10 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         const int n = min(kTilePixels, toDo);
         for (int j = 0; !done && j < n; j++) {
             contributor++;
+            if constexpr (STATS) {
+                const unsigned long long m = __ballot(1);
+                if ((tid & 63) == __builtin_ctzll(m)) cst[0] += 1;
+            }
             const float4 w0 = s_w0[j];
             const float dx = w0.x - pixx, dy = w0.y - pixy;
             const float4 w1 = s_w1[j];
@@ -324,6 +337,10 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             if (test_T < 0.0001f) {
                 done = true;
                 continue;
+            }
+            if constexpr (STATS) {
+                const unsigned long long m = __ballot(1);
+                if ((tid & 63) == __builtin_ctzll(m)) cst[1] += __popcll(m);
             }
             const float aT = alpha * T;
             const float4 w2 = s_w2[j];
@@ -376,7 +393,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     float mDepth = 0.f, md_out = 0.f, md_dT = 0.f;
     bool md_ok = false, md_in_range = false;
     if constexpr (GEOM) {
-        unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long st[8] = {0, 0, cst[0], cst[1], 0, 0, 0, 0};
         float Tp[kSplit + 1];
         // the reference's first window (render_forward.cu:560-562)
         const float win_lo = fmaxf(m_init - a.sample_range, 0.f);
@@ -407,14 +424,22 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         // Per-lane walk over the LDS-resident records of the contributors the
         // lane blended, in increasing index order (the reference's c = 1..last
         // multiplication order); each lane advances through its own mask words.
-        auto lane_walk = [&](bool active, auto&& body) {
-            const int nwords = active ? (int)((last + 31) >> 5) : 0;
+        // Two contributors per iteration (halving the per-step control and
+        // exec-mask work; two independent dependency chains): when a word has
+        // one left, the second is a dummy with alpha = 0, for which every walk
+        // body multiplies by exactly 1 and adds exactly 0.
+        auto walk = [&](const uint32_t* mask, uint32_t plast, float ppx, float ppy, uint32_t filter, bool active,
+                        auto&& body) {
+            const int nwords = active ? (int)((plast + 31) >> 5) : 0;
             int w = 0;
-            uint32_t bits = nwords ? my_mask[0] : 0u;
+            uint32_t bits = nwords ? (mask[0] & filter) : 0u;
             while (true) {
-                while (bits == 0u && w + 1 < nwords) bits = my_mask[++w * kTilePixels];
+                while (bits == 0u && w + 1 < nwords) bits = mask[++w * kTilePixels] & filter;
                 if (bits == 0u) break;
-                const int j = (w << 5) + __builtin_ctz(bits);
+                const int j1 = (w << 5) + __builtin_ctz(bits);
+                bits &= bits - 1u;
+                const bool two = bits != 0u;
+                const int j2 = two ? (w << 5) + __builtin_ctz(bits) : j1;
                 bits &= bits - 1u;
                 if constexpr (STATS) {
                     const unsigned long long m = __ballot(1);
@@ -423,14 +448,18 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                         st[1] += __popcll(m);
                     }
                 }
-                const float4 w0 = c_w0[j];
-                const float dx = w0.x - pixx, dy = w0.y - pixy;
-                const float4 w1 = c_w1[j];
-                const float alpha = fminf(0.99f, w1.y * __expf(splat_power(w0, w1, dx, dy)));
-                const float4 w2 = c_w2[j];
-                body(alpha, splat_tpeak(w1, w2, dx, dy), w2);
+                const float4 a0 = c_w0[j1], b0 = c_w0[j2];
+                const float4 a1 = c_w1[j1], b1 = c_w1[j2];
+                const float adx = a0.x - ppx, ady = a0.y - ppy;
+                const float bdx = b0.x - ppx, bdy = b0.y - ppy;
+                const float alpha_a = fminf(0.99f, a1.y * __expf(splat_power(a0, a1, adx, ady)));
+                const float alpha_b = two ? fminf(0.99f, b1.y * __expf(splat_power(b0, b1, bdx, bdy))) : 0.f;
+                const float4 a2 = c_w2[j1], b2 = c_w2[j2];
+                body(alpha_a, splat_tpeak(a1, a2, adx, ady), a2);
+                body(alpha_b, splat_tpeak(b1, b2, bdx, bdy), b2);
             }
         };
+        auto lane_walk = [&](bool active, auto&& body) { walk(my_mask, last, pixx, pixy, ~0u, active, body); };
         bool refined = false;   // median depth found by the root refinement
         float t_ref = 0.f;
         float ref_t = 0.f, ref_D = 0.f, ref_E = 0.f;  // the last refinement walk's depth, -H', H''
@@ -507,18 +536,105 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             Tp[0] = lo;
             Tp[kSplit] = hi;
         };
-        if (a.refine && resident && a.passes > 0) {
-            // Walk 1: the vacancy transmittance at kProbes depths — the window
-            // ends (the reference's in_range test, same sample arithmetic) and
-            // m0 + kProbeOffsets * SAMPLE_RANGE (clamped into the window), where
-            // the root almost always is.  Samples are in increasing order.
-            const float interval = (win_hi - win_lo) * (1.f / (float)kSplit);
-            const float e0 = win_lo, e8 = __builtin_fmaf(interval, (float)kSplit, win_lo);
+        // Root refinement for one pixel, shared by the phases below: probe
+        // walk + bracketed Halley walks.  A pixel may be worked by a group of
+        // 4 lanes (lane q walks the contributors with index % 4 == q; products
+        // and sums are combined with two xor shuffles, identical in the 4
+        // lanes as float * and + commute) — `grouped` must then be uniform.
+        auto gprod = [&](float v, bool grouped) {
+            if (grouped) {
+                v *= __shfl_xor(v, 1, 64);
+                v *= __shfl_xor(v, 2, 64);
+            }
+            return v;
+        };
+        auto gsum = [&](float v, bool grouped) {
+            if (grouped) {
+                v += __shfl_xor(v, 1, 64);
+                v += __shfl_xor(v, 2, 64);
+            }
+            return v;
+        };
+        // Halley walks from t in the bracket [lo, hi] (H(lo) >= 0 >= H(hi)).  With `ends`,
+        // the first walk also evaluates T at the window ends e0, e8 and sets in_range.
+        struct Refine {
+            bool refined, in_range;
+            float t_ref, ref_t, ref_D, ref_E;
+        };
+        auto halley = [&](const uint32_t* mask, uint32_t plast, float ppx, float ppy, uint32_t filter, bool grouped,
+                          bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0) {
+            Refine r{false, in_range0, 0.f, 0.f, 0.f, 0.f};
+            const float scale = fmaxf(t, 1.f);
+            const float tol = kRefineTol * scale, tol_cond = kCondTol * scale;
+            const f32x2 TSE[1] = {f32x2{e0, e8}};
+            for (int k = 0; k < kRefineWalks && a.passes > 1; k++) {
+                if (__ballot(live) == 0ull) break;
+                float A = 1.f, B = 1.f, D = 0.f, E = 0.f;
+                f32x2 AE[1] = {f32x2{1.f, 1.f}}, BE[1] = {f32x2{1.f, 1.f}};
+                float unusedA = 1.f, unusedB = 1.f;
+                if (ends && k == 0) {
+                    walk(mask, plast, ppx, ppy, filter, live, [&](float alpha, float t_peak, float4 w2) {
+                        refine_step(A, B, D, E, t, alpha, t_peak, w2.z, w2.w);
+                        bisect_step<1, false, SKIP>(AE, BE, TSE, unusedA, unusedB, 0.f, alpha, t_peak, w2.y, w2.z,
+                                                    w2.w);
+                    });
+                } else {
+                    walk(mask, plast, ppx, ppy, filter, live, [&](float alpha, float t_peak, float4 w2) {
+                        refine_step(A, B, D, E, t, alpha, t_peak, w2.z, w2.w);
+                    });
+                }
+                A = gprod(A, grouped);
+                B = gprod(B, grouped);
+                D = gsum(D, grouped);
+                E = gsum(E, grouped);
+                if (ends && k == 0) {
+                    const float T0 = gprod(AE[0].x, grouped) * __builtin_amdgcn_rsqf(gprod(BE[0].x, grouped));
+                    const float T8 = gprod(AE[0].y, grouped) * __builtin_amdgcn_rsqf(gprod(BE[0].y, grouped));
+                    r.in_range = r.in_range && T0 >= 0.5f && T8 <= 0.5f;
+                    live = live && r.in_range;
+                }
+                if (live) {
+                    if constexpr (STATS) st[6] += 1;
+                    const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
+                    if (H >= 0.f) lo = t;
+                    else hi = t;
+                    // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
+                    float tn = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
+                    if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
+                    const bool done = (D > 0.f && fabsf(H) <= tol * D) || hi - lo <= tol;
+                    if (done) {
+                        // accepted only where the root is well conditioned: rounding noise of
+                        // ~kHNoise in log2 T moves it by less than tol_cond (T flat near 1/2 — a
+                        // pixel between two splats' peaks — leaves it to the reference's passes)
+                        r.refined = D * tol_cond >= kHNoise;
+                        r.t_ref = tn;
+                        live = false;
+                        r.ref_t = t;
+                        r.ref_D = D;
+                        r.ref_E = E;
+                    }
+                    t = tn;
+                }
+            }
+            if (a.passes == 1 && r.in_range) {  // diagnostic timing of the probe walk alone
+                r.refined = true;
+                r.t_ref = t;
+            }
+            return r;
+        };
+        // Probe walk (window ends + m0 + kProbeOffsets * SAMPLE_RANGE), then the
+        // Halley walks from the log-secant root of the bracketing probes.
+        auto probe_refine = [&](const uint32_t* mask, uint32_t plast, float ppx, float ppy, float pm0, float pT,
+                                uint32_t filter, bool grouped) {
+            bool pin = pT <= kMinTransmittance;
+            const float lo_w = fmaxf(pm0 - a.sample_range, 0.f), hi_w = fmaxf(pm0 + a.sample_range, 0.f);
+            const float interval = (hi_w - lo_w) * (1.f / (float)kSplit);
+            const float e0 = lo_w, e8 = __builtin_fmaf(interval, (float)kSplit, lo_w);
             float tp[kProbes];
 #pragma unroll
             for (int s = 0; s < kProbes; s++) {
                 const float off = kProbeOffsets[s] * a.sample_range;
-                tp[s] = s == 0 ? e0 : s == kProbes - 1 ? e8 : fminf(fmaxf(m_init + off, e0), e8);
+                tp[s] = s == 0 ? e0 : s == kProbes - 1 ? e8 : fminf(fmaxf(pm0 + off, e0), e8);
             }
             // the m0 probe is the scalar sample, the others go in packed pairs
             constexpr int NP = (kProbes - 1) / 2, MID = (kProbes - 1) / 2;
@@ -531,18 +647,18 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
                 B[k] = f32x2{1.f, 1.f};
             }
             float A1 = 1.f, B1 = 1.f;
-            lane_walk(in_range, [&](float alpha, float t_peak, float4 w2) {
+            walk(mask, plast, ppx, ppy, filter, pin, [&](float alpha, float t_peak, float4 w2) {
                 bisect_step<NP, true, SKIP>(A, B, TS, A1, B1, tp[MID], alpha, t_peak, w2.y, w2.z, w2.w);
             });
             float Tv[kProbes];
 #pragma unroll
             for (int k = 0; k < NP; k++) {
                 const int s0 = 2 * k < MID ? 2 * k : 2 * k + 1, s1 = 2 * k + 1 < MID ? 2 * k + 1 : 2 * k + 2;
-                Tv[s0] = A[k].x * __builtin_amdgcn_rsqf(B[k].x);
-                Tv[s1] = A[k].y * __builtin_amdgcn_rsqf(B[k].y);
+                Tv[s0] = gprod(A[k].x, grouped) * __builtin_amdgcn_rsqf(gprod(B[k].x, grouped));
+                Tv[s1] = gprod(A[k].y, grouped) * __builtin_amdgcn_rsqf(gprod(B[k].y, grouped));
             }
-            Tv[MID] = A1 * __builtin_amdgcn_rsqf(B1);
-            in_range = (Tv[0] >= 0.5f) && (Tv[kProbes - 1] <= 0.5f) && in_range;
+            Tv[MID] = gprod(A1, grouped) * __builtin_amdgcn_rsqf(gprod(B1, grouped));
+            pin = (Tv[0] >= 0.5f) && (Tv[kProbes - 1] <= 0.5f) && pin;
             // bracket: the last probe with T >= 1/2 and the next one
             int k1 = 0;
 #pragma unroll
@@ -560,45 +676,109 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             const float Hhi = __builtin_amdgcn_logf(Thi) + 1.f;
             float wsec = Hlo / (Hlo - Hhi);
             wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
-            float t = __builtin_fmaf(wsec, hi - lo, lo);
-            const float scale = fmaxf(t, 1.f);
-            const float tol = kRefineTol * scale, tol_cond = kCondTol * scale;
-            bool live = in_range;
+            const float t = __builtin_fmaf(wsec, hi - lo, lo);
+            return halley(mask, plast, ppx, ppy, filter, grouped, pin, t, lo, hi, false, 0.f, 0.f, pin);
+        };
+        bool have_out = false;  // (render path) md_out and dT/dt_m published by the pixel's worker
+        if (a.refine && resident && a.passes > 0) {
             if constexpr (STATS) {
                 if ((tid & 63) == 0) st[4] += 1;
             }
-            for (int k = 0; k < kRefineWalks && a.passes > 1; k++) {
-                if (__ballot(live) == 0ull) break;
-                float A = 1.f, B = 1.f, D = 0.f, E = 0.f;
-                lane_walk(live, [&](float alpha, float t_peak, float4 w2) {
-                    refine_step(A, B, D, E, t, alpha, t_peak, w2.z, w2.w);
-                });
-                if (live) {
-                    if constexpr (STATS) st[6] += 1;
-                    const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
-                    if (H >= 0.f) lo = t;
-                    else hi = t;
-                    // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
-                    float tn = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
-                    if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
-                    const bool done = (D > 0.f && fabsf(H) <= tol * D) || hi - lo <= tol;
-                    if (done) {
-                        // accepted only where the root is well conditioned: rounding noise of
-                        // ~kHNoise in log2 T moves it by less than tol_cond (T flat near 1/2 — a
-                        // pixel between two splats' peaks — leaves it to the reference's passes)
-                        refined = D * tol_cond >= kHNoise;
-                        t_ref = tn;
-                        live = false;
-                        ref_t = t;
-                        ref_D = D;
-                        ref_E = E;
+            if constexpr (!SAMPLE) {
+                // Two phases over the tile (render_fwd.hip header, tools/sim/s4_sim.py):
+                //  1. the 64 pixels of the even grid (x, y even), 4 lanes each: probe walk + Halley;
+                //  2. the other 192, one lane each on 3 of the 4 waves: Halley walks from the mean of
+                //     their grid neighbours' roots (the median depth varies slowly: the guess is within
+                //     2e-4 of the root for 90% of pixels at C3, against ~1e-3 for the probe bracket),
+                //     the first walk also sampling the window ends for in_range.
+                // The owner lane then takes the result, or runs the reference's passes where there is
+                // none (not converged, ill-conditioned, no grid neighbour with a root).
+                const int x0 = px - (tid & 15), y0 = py - (tid >> 4);
+                s_pub_last[tid] = last;
+                s_pub_m0[tid] = m_init;
+                s_pub_T[tid] = T;
+                __syncthreads();
+                auto publish = [&](int p, float ppx, float ppy, const Refine& r) {
+                    uint32_t flags = r.in_range ? 0u : kPubOut;
+                    float mo = 0.f, dt = 0.f;
+                    if (r.in_range && r.refined) {
+                        flags = kPubRefined;
+                        const float nrm = pixel_ray_norm(ppx, ppy, a.W, a.H, a.focal_x, a.focal_y);
+                        mo = r.t_ref * (1.0f / nrm);
+                        const float mb = mo * nrm;
+                        if (mb != 0.f) dt = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(r.ref_E, mb - r.ref_t, -r.ref_D);
                     }
-                    t = tn;
+                    s_pub_last[p] = flags;
+                    s_pub_T[p] = mo;
+                    s_pub_m0[p] = dt;
+                };
+                {  // phase 1
+                    const int g = tid >> 2, q = tid & 3;
+                    const int gp = (g >> 3) * 32 + (g & 7) * 2;  // (2 (g / 8), 2 (g % 8)) in the tile
+                    const float gpx = (float)(x0 + (gp & 15)), gpy = (float)(y0 + (gp >> 4));
+                    const uint32_t gl = s_pub_last[gp];
+                    const float gm0 = s_pub_m0[gp], gT = s_pub_T[gp];
+                    const Refine r = probe_refine(s_mask + gp, gl, gpx, gpy, gm0, gT, 0x11111111u << q, true);
+                    if (q == 0) {
+                        s_groot[g] = (r.in_range && r.refined) ? r.t_ref : -1.f;
+                        publish(gp, gpx, gpy, r);
+                    }
                 }
-            }
-            if (a.passes == 1 && in_range) {  // diagnostic timing of walk 1 alone
-                refined = true;
-                t_ref = t;
+                __syncthreads();
+                const int skip = (int)(blockIdx.x & 3u);  // the wave left idle (rotated over the SIMDs)
+                if (wave != skip) {  // phase 2
+                    const int k = (wave < skip ? wave : wave - 1) * 64 + (tid & 63);
+                    const int pair = k / 24, r24 = k - pair * 24;
+                    const int lx = r24 < 8 ? 2 * r24 + 1 : r24 - 8, ly = r24 < 8 ? 2 * pair : 2 * pair + 1;
+                    const int p = ly * 16 + lx;
+                    const float qx = (float)(x0 + lx), qy = (float)(y0 + ly);
+                    const uint32_t ql = s_pub_last[p];
+                    const float qm0 = s_pub_m0[p], qT = s_pub_T[p];
+                    float sum = 0.f;
+                    int cnt = 0;
+#pragma unroll
+                    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; dx++) {
+                            const int nx = lx + dx, ny = ly + dy;
+                            // grid neighbours: the pixel itself on even coordinates, both sides on odd
+                            const bool use = ((lx & 1) ? dx != 0 : dx == 0) && ((ly & 1) ? dy != 0 : dy == 0);
+                            if (use && nx >= 0 && nx < 16 && ny >= 0 && ny < 16) {
+                                const float gr = s_groot[(ny >> 1) * 8 + (nx >> 1)];
+                                if (gr >= 0.f) {
+                                    sum += gr;
+                                    cnt++;
+                                }
+                            }
+                        }
+                    const bool qin = qT <= kMinTransmittance;
+                    const float lo_w = fmaxf(qm0 - a.sample_range, 0.f), hi_w = fmaxf(qm0 + a.sample_range, 0.f);
+                    const float interval = (hi_w - lo_w) * (1.f / (float)kSplit);
+                    const float e0 = lo_w, e8 = __builtin_fmaf(interval, (float)kSplit, lo_w);
+                    const float t0 = cnt ? fminf(fmaxf(sum / (float)cnt, e0), e8) : e0;
+                    const Refine r = halley(s_mask + p, ql, qx, qy, ~0u, false, qin && cnt > 0, t0, e0, e8, true, e0,
+                                            e8, qin);
+                    if (cnt > 0 || !qin) publish(p, qx, qy, r);
+                    else s_pub_last[p] = 0u;  // no guess: the owner runs the passes
+                }
+                __syncthreads();
+                const uint32_t flags = s_pub_last[tid];
+                if (flags & kPubRefined) {
+                    refined = true;
+                    have_out = true;
+                    md_out = s_pub_T[tid];
+                    md_dT = s_pub_m0[tid];
+                } else if (flags & kPubOut) {
+                    in_range = false;
+                }
+            } else {
+                const Refine r = probe_refine(my_mask, last, pixx, pixy, m_init, T, ~0u, false);
+                in_range = r.in_range;
+                refined = r.refined;
+                t_ref = r.t_ref;
+                ref_t = r.ref_t;
+                ref_D = r.ref_D;
+                ref_E = r.ref_E;
             }
             // lanes left: the reference's passes from its first window
             const bool left = in_range && !refined;
@@ -622,41 +802,46 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
             for (int q = 0; q < 8; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
         }
-        float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
-        w_max = fminf(fmaxf(w_max, 0.f), 1.f);  // __saturatef (NaN -> 0)
-        const float w_min = 1.f - w_max;
-        mDepth = in_range ? (refined ? t_ref : __builtin_fmaf(w_max, dmax, w_min * dmin)) : 0.f;
         md_in_range = in_range;
+        if (!have_out) {
+            float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
+            w_max = fminf(fmaxf(w_max, 0.f), 1.f);  // __saturatef (NaN -> 0)
+            const float w_min = 1.f - w_max;
+            mDepth = in_range ? (refined ? t_ref : __builtin_fmaf(w_max, dmax, w_min * dmin)) : 0.f;
 
-        // The backward's median-depth pre-pass (render_backward.cu:835-880),
-        // done here while the blended set is still in LDS: dT/dt_m at the
-        // depth the backward will reconstruct from the mdepth output.  The
-        // backward uses it when it receives that same mdepth (md_check) and
-        // recomputes it otherwise.
-        float mDepth_b;
-        if constexpr (SAMPLE) {
-            mDepth_b = mDepth;  // the sample backward reads the median depth itself (sample_backward.cu:135)
+            // The backward's median-depth pre-pass (render_backward.cu:835-880),
+            // done here while the blended set is still in LDS: dT/dt_m at the
+            // depth the backward will reconstruct from the mdepth output.  The
+            // backward uses it when it receives that same mdepth (md_check) and
+            // recomputes it otherwise.
+            float mDepth_b;
+            if constexpr (SAMPLE) {
+                mDepth_b = mDepth;  // the sample backward reads the median depth itself (sample_backward.cu:135)
+            } else {
+                const float nrm = pixel_ray_norm(pixx, pixy, a.W, a.H, a.focal_x, a.focal_y);
+                md_out = mDepth * (1.0f / nrm);
+                mDepth_b = md_out * nrm;
+            }
+            float dT_dtm = 0.f;
+            const bool want_dT = !SAMPLE || a.query == kQuerySample;
+            if (refined) {
+                // the reference's dT/dt_m (render_backward.cu:876) is T H' ln2 = H' ln2 / 2 at T = 1/2;
+                // continued to mDepth_b from the last walk: H'(t) = -D + E (t - ref_t) (|t - ref_t| <= a
+                // Newton step of kRefineTol max(t, 1); the next term is ~(step / sigma)^2 relative)
+                if (mDepth_b != 0.f)
+                    dT_dtm = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(ref_E, mDepth_b - ref_t, -ref_D);
+            } else if (resident) {
+                lane_walk(want_dT && inside && mDepth_b != 0.f && last != 0, [&](float alpha, float t_peak,
+                                                                                 float4 w2) {
+                    const float t_delta = (mDepth_b - t_peak) * w2.y;
+                    const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
+                    dT_dtm += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
+                });
+            }
+            md_dT = dT_dtm;
         } else {
-            const float nrm = pixel_ray_norm(pixx, pixy, a.W, a.H, a.focal_x, a.focal_y);
-            md_out = mDepth * (1.0f / nrm);
-            mDepth_b = md_out * nrm;
+            mDepth = 1.f;  // (render path: only md_out is used; nonzero = in range)
         }
-        float dT_dtm = 0.f;
-        const bool want_dT = !SAMPLE || a.query == kQuerySample;
-        if (refined) {
-            // the reference's dT/dt_m (render_backward.cu:876) is T H' ln2 = H' ln2 / 2 at T = 1/2;
-            // continued to mDepth_b from the last walk: H'(t) = -D + E (t - ref_t) (|t - ref_t| <= a
-            // Newton step of kRefineTol max(t, 1); the next term is ~(step / sigma)^2 relative)
-            if (mDepth_b != 0.f)
-                dT_dtm = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(ref_E, mDepth_b - ref_t, -ref_D);
-        } else if (resident) {
-            lane_walk(want_dT && inside && mDepth_b != 0.f && last != 0, [&](float alpha, float t_peak, float4 w2) {
-                const float t_delta = (mDepth_b - t_peak) * w2.y;
-                const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
-                dT_dtm += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
-            });
-        }
-        md_dT = dT_dtm;
         md_ok = resident;
     }
 

@@ -22,4 +22,5 @@ torch.cuda.synchronize()
 st = _C.debug_render_stats(reset=True)
 _C.set_option(_C.OPT_RENDER_STATS, 0)
 print("walk wave-steps", st[0], "active lanes/step", round(st[1] / max(st[0], 1), 2))
+print("composite wave-steps", st[2], "blending lanes/step", round(st[3] / max(st[2], 1), 2))
 print("refine waves", st[4], "fallback waves", st[5], "refine lane-walks", st[6], "lanes left", st[7])

@@ -620,3 +620,149 @@ void sim_s3(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
     }
     free(buf);
 }
+
+/* Reference median depth of every pixel of the sampled tiles (0 where not in range): out[ti*256 + l]. */
+void sim_ref_depths(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+                    const uint32_t* point_list, const float* xy, const float* co, const float* rp, float* out,
+                    float* out_m0) {
+    contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const uint32_t tx = tile % gx, ty = tile / gx;
+        const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
+        for (int l = 0; l < 256; l++) {
+            const int px = tx * 16 + (l & 15), py = ty * 16 + (l >> 4);
+            out[ti * 256 + l] = 0.f;
+            out_m0[ti * 256 + l] = 0.f;
+            if (px >= W || py >= H) continue;
+            float Tf, m0;
+            const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf, &Tf, &m0);
+            int ir;
+            out[ti * 256 + l] = ref_bisect(buf, n, m0, Tf, &ir);
+            out_m0[ti * 256 + l] = m0;
+        }
+    }
+    free(buf);
+}
+
+/* S4: grid pixels (even x, even y of a tile: 64) find their root with S2 (probe walk + Halley from the
+ * log-secant); the other 192 start bracketed Halley walks from the average of their tile's grid neighbours'
+ * roots (walk 1 also samples the window ends for in_range).  out: [0] lanes, [1] max|d|, [2] fallbacks,
+ * [3] sum of phase-1 wave max walks, [4] phase-1 waves, [5] sum of phase-2 wave max walks, [6] phase-2 waves,
+ * [8..23] phase-2 lane walk hist, [24] lanes without a grid guess */
+static int halley_from(const contrib_t* c, int n, float t, float lo, float hi, float tol_rel, int maxit,
+                       float hnoise, float* res) {
+    const float tol = tol_rel * fmaxf(t, 1.f);
+    int walks = 0;
+    for (int k = 0; k < maxit; k++) {
+        float h, dh, dd;
+        vac_d2(c, n, t, &h, &dh, &dd);
+        walks++;
+        if (h >= 0.f) lo = t; else hi = t;
+        const float den = 2.f * dh * dh - h * dd;
+        float tn = den != 0.f ? t - 2.f * h * dh / den : 0.5f * (lo + hi);
+        if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
+        if ((dh < 0.f && fabsf(h) <= tol * -dh) || hi - lo <= tol) {
+            if (-dh * 1e-6f * fmaxf(t, 1.f) >= hnoise) { *res = tn; return walks; }
+            return -walks;
+        }
+        t = tn;
+    }
+    return -walks;
+}
+void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+            const uint32_t* point_list, const float* xy, const float* co, const float* rp, int nk, const float* off,
+            float tol_rel, int maxit, float hnoise, double* out) {
+    contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const uint32_t tx = tile % gx, ty = tile / gx;
+        const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
+        float root[256];
+        int have[256], walksv[256];
+        /* phase 1: grid pixels */
+        int wmax1 = 0;
+        for (int l = 0; l < 256; l++) {
+            have[l] = 0;
+            walksv[l] = 0;
+            const int lx = l & 15, ly = l >> 4;
+            if ((lx & 1) || (ly & 1)) continue;
+            const int px = tx * 16 + lx, py = ty * 16 + ly;
+            if (px >= W || py >= H) continue;
+            float Tf, m0;
+            const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf, &Tf, &m0);
+            int ir;
+            const float mr = ref_bisect(buf, n, m0, Tf, &ir);
+            if (!ir) continue;
+            out[0] += 1;
+            float ts[32], hs[32];
+            const float dmin = fmaxf(m0 - RANGE, 0.f), dmax = fmaxf(m0 + RANGE, 0.f);
+            int m = 0;
+            ts[m++] = dmin;
+            for (int k = 0; k < nk; k++) ts[m++] = fminf(fmaxf(m0 + off[k], dmin), dmax);
+            ts[m++] = dmax;
+            for (int k = 0; k < m; k++) hs[k] = logf(vac(buf, n, ts[k])) + 0.69314718f;
+            int k1 = 0;
+            for (int k = 1; k < m - 1; k++) if (hs[k] >= 0.f) k1 = k;
+            float w = hs[k1] / (hs[k1] - hs[k1 + 1]);
+            w = (w != w) ? 0.5f : fminf(fmaxf(w, 0.f), 1.f);
+            const float t0 = ts[k1] + w * (ts[k1 + 1] - ts[k1]);
+            float res = mr;
+            int wk = halley_from(buf, n, t0, ts[k1], ts[k1 + 1], tol_rel, maxit, hnoise, &res);
+            if (wk < 0) { out[2] += 1; res = mr; wk = 100; }
+            root[l] = res;
+            have[l] = 1;
+            const double d = fabs((double)res - mr);
+            if (d > out[1]) out[1] = d;
+            if (wk > wmax1) wmax1 = wk;
+        }
+        out[3] += wmax1;
+        out[4] += 1;
+        /* phase 2: the others, in raster order, 64 per wave */
+        int lane = 0, wmax2 = 0;
+        for (int l = 0; l < 256; l++) {
+            const int lx = l & 15, ly = l >> 4;
+            if (!((lx & 1) || (ly & 1))) continue;
+            const int px = tx * 16 + lx, py = ty * 16 + ly;
+            int wk = 0;
+            if (px < W && py < H) {
+                float Tf, m0;
+                const int n = composite(point_list + r0, (int)(r1 - r0), xy, co, rp, (float)px, (float)py, buf, &Tf, &m0);
+                int ir;
+                const float mr = ref_bisect(buf, n, m0, Tf, &ir);
+                if (ir) {
+                    out[0] += 1;
+                    float sum = 0.f;
+                    int cnt = 0;
+                    for (int yy = ly - (ly & 1); yy <= ly + (ly & 1); yy += 2)
+                        for (int xx = lx - (lx & 1); xx <= lx + (lx & 1); xx += 2)
+                            if (yy >= 0 && yy < 16 && xx >= 0 && xx < 16 && have[yy * 16 + xx]) {
+                                sum += root[yy * 16 + xx];
+                                cnt++;
+                            }
+                    const float dmin = fmaxf(m0 - RANGE, 0.f), dmax = fmaxf(m0 + RANGE, 0.f);
+                    float res = mr;
+                    if (!cnt) {
+                        out[24] += 1;
+                        wk = 100;
+                    } else {
+                        const float t0 = fminf(fmaxf(sum / cnt, dmin), dmax);
+                        wk = halley_from(buf, n, t0, dmin, dmax, tol_rel, maxit, hnoise, &res);
+                        if (wk < 0) { out[2] += 1; res = mr; wk = 100; }
+                    }
+                    const double d = fabs((double)res - mr);
+                    if (d > out[1]) out[1] = d;
+                    out[8 + (wk < 15 ? wk : 15)] += 1;
+                }
+            }
+            if (wk > wmax2) wmax2 = wk;
+            if (++lane == 64) {
+                out[5] += wmax2;
+                out[6] += 1;
+                lane = 0;
+                wmax2 = 0;
+            }
+        }
+    }
+    free(buf);
+}
