@@ -225,8 +225,11 @@ __device__ unsigned long long g_render_stats[8];
 //    keeps only T / last / m0 / blended set, then the bisection runs.
 //  * !GEOM (integrate, evaluateTransmittanceCUDA, :55-169): the composite
 //    also carries the vacancy transmittance at the point's own distance.
+// 5 waves per SIMD: the LDS (31.5 KB per block) allows 5 blocks per CU; the
+// register budget that gives (96) costs a few spilled registers outside the
+// walks.
 template <bool GEOM, bool SKIP, bool STATS = false, bool SAMPLE = false>
-__global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 256 x 16 B = 16 KB) aliased with the
     // bisection cache (3 x 384 x 16 B = 18 KB), plus the 12 KB of masks:
     // 30 KB per block, 5 blocks (20 waves) per CU.  (A 320-record cache
@@ -383,6 +386,25 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
     }
 
     if constexpr (GEOM) my_mask[mask_w * kTilePixels] = mask_cur;
+    if constexpr (!SAMPLE) {
+        // the composite's outputs are final: written before the median depth
+        // (their registers are free for it)
+        if (inside) {
+            const int HW = a.H * a.W;
+            const int pix = a.W * py + px;
+            a.n_contrib[pix] = last;
+            a.out_color[pix] = __builtin_fmaf(T, a.bg[0], C0);
+            a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], C1);
+            a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2);
+            a.out_alpha[pix] = 1.f - T;
+            if constexpr (GEOM) {
+                const float len = 1.f - T;
+                a.out_normal[pix] = last ? N0 / len : 0.f;
+                a.out_normal[HW + pix] = last ? N1 / len : 0.f;
+                a.out_normal[2 * HW + pix] = last ? N2 / len : 0.f;
+            }
+        }
+    }
 
     // block max of last contributor (cub BlockReduce in the reference)
     const uint32_t wmax = wave_max_u(last);
@@ -878,22 +900,13 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a) {
         return;
     }
     if (inside) {
-        const int HW = a.H * a.W;
         const int pix = a.W * py + px;
-        a.n_contrib[pix] = last;
-        a.out_color[pix] = __builtin_fmaf(T, a.bg[0], C0);
-        a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], C1);
-        a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2);
-        a.out_alpha[pix] = 1.f - T;
         if constexpr (GEOM) {
             a.out_mdepth[pix] = md_out;
             a.dT_dtm[pix] = md_dT;
             a.md_check[pix] = md_ok ? __float_as_uint(md_out) : kNoCache;
-            const float len = 1.f - T;
-            a.out_normal[pix] = last ? N0 / len : 0.f;
-            a.out_normal[HW + pix] = last ? N1 / len : 0.f;
-            a.out_normal[2 * HW + pix] = last ? N2 / len : 0.f;
         } else {
+            const int HW = a.H * a.W;
             a.md_check[pix] = kNoCache;
             a.out_mdepth[pix] = 0.f;
             a.out_normal[pix] = 0.f;
