@@ -301,4 +301,20 @@ __device__ __forceinline__ float splat_tpeak(const float4& w1, const float4& w2,
     return __builtin_fmaf(w1.w, dy, w1.z * dx) + w2.x;
 }
 
+// The same for two pixels of one column (shared dx, dy in the halves of a
+// packed register): the packed operations round exactly as the scalar ones.
+typedef float pf32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf32x2 splat_power2(const float4& w0, const float4& w1, float dx, pf32x2 dy) {
+#pragma clang fp contract(off)
+    const float ax = (w0.z * dx) * dx;
+    const pf32x2 q = __builtin_elementwise_fma(pf32x2{w1.x, w1.x} * dy, dy, pf32x2{ax, ax});
+    const float bx = w0.w * dx;
+    return __builtin_elementwise_fma(pf32x2{-0.5f, -0.5f}, q, -(pf32x2{bx, bx} * dy));
+}
+__device__ __forceinline__ pf32x2 splat_tpeak2(const float4& w1, const float4& w2, float dx, pf32x2 dy) {
+#pragma clang fp contract(off)
+    const float cx = w1.z * dx;
+    return __builtin_elementwise_fma(pf32x2{w1.w, w1.w}, dy, pf32x2{cx, cx}) + pf32x2{w2.x, w2.x};
+}
+
 }  // namespace gsr

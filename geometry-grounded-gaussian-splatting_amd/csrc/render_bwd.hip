@@ -52,20 +52,10 @@ __device__ __forceinline__ f2 sel2(bool ca, bool cb, f2 x, f2 y) { return f2{ca 
 __device__ __forceinline__ f2 splat2(float v) { return f2{v, v}; }
 __device__ __forceinline__ float hsum(f2 v) { return v.x + v.y; }
 
-// splat_power / splat_tpeak (gsr_common.h) for the two pixels of a lane,
+// splat_power2 / splat_tpeak2 (gsr_common.h) for the two pixels of a lane,
 // which share the column (dx) and differ in the row (dy.x, dy.y); the
 // packed operations round exactly as the scalar helpers, so alpha and the
 // contribute decision stay bit-identical to the forward.
-__device__ __forceinline__ f2 splat_power2(const float4& w0, const float4& w1, float dx, f2 dy) {
-#pragma clang fp contract(off)
-    const float ax = (w0.z * dx) * dx;
-    const f2 q = __builtin_elementwise_fma(splat2(w1.x) * dy, dy, splat2(ax));
-    return __builtin_elementwise_fma(splat2(-0.5f), q, -(splat2(w0.w * dx) * dy));
-}
-__device__ __forceinline__ f2 splat_tpeak2(const float4& w1, const float4& w2, float dx, f2 dy) {
-#pragma clang fp contract(off)
-    return __builtin_elementwise_fma(splat2(w1.w), dy, splat2(w1.z * dx)) + splat2(w2.x);
-}
 
 // Per-pixel inputs of the backward (render_backward.cu:771-833).
 struct PixIn {

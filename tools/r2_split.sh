@@ -1,4 +1,4 @@
-# render_fwd time split (GSR_OPT_BISECT_PASSES = -1 composite only, 1 = walk 1 only) + refinement stats at C3
+# render_fwd time split (GSR_OPT_BISECT_PASSES = -1 composite only, 1 = probe walk only) + render stats at C3
 set -o pipefail
 mkdir -p gpurun_out
 for v in -1 1; do
