@@ -189,12 +189,15 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
     // ---- main back-to-front pass (render_backward.cu:882-1068)
     // The reference carries (last_alpha, last_colour) one step and folds them
     // into accum_rec at the NEXT valid contributor; here a contributor is
-    // folded in right after its own terms (same values, same operations).  A
-    // pixel for which the splat is not valid runs with alpha = 0, which leaves
-    // T (x rcp(1) = 1), accum_rec (x 1 + 0) and the plane terms unchanged
-    // exactly, so only dL/dopacity and G need a select.
+    // folded in right after its own terms (same values; accum_rec's update is
+    // written as one fma, a few ulp from the reference's rounding).  A pixel
+    // for which the splat is not valid runs with alpha = 0, which leaves
+    // T (x rcp(1) = 1), accum_rec (+ 0 x d) and the plane terms unchanged
+    // exactly, so only G dL/dopacity needs a select.
     uint32_t contributor = (uint32_t)max_contrib;
     f2 T = T_final;
+    const f2 tfd = -T_final * dL_dfinalT;  // dL/dopacity term of the final transmittance, / (1 - alpha)
+    const f2 kappa_q = 0.25f * kappa;
     f2 ar0 = {0.f, 0.f}, ar1 = {0.f, 0.f}, ar2 = {0.f, 0.f};
     f2 an0 = {0.f, 0.f}, an1 = {0.f, 0.f}, an2 = {0.f, 0.f};
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
@@ -236,22 +239,23 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
             const f2 r1a = {fast_rcp(one_m_alpha.x), fast_rcp(one_m_alpha.y)};
             T = T * r1a;
             const f2 bw = alpha * T;
-            const f2 c0 = splat2(w2.z), c1 = splat2(w2.w), c2 = splat2(w3.x);
-            f2 dL_dopa = (c0 - ar0) * dLp0 + (c1 - ar1) * dLp1 + (c2 - ar2) * dLp2;
-            ar0 = alpha * c0 + one_m_alpha * ar0;
-            ar1 = alpha * c1 + one_m_alpha * ar1;
-            ar2 = alpha * c2 + one_m_alpha * ar2;
+            // accum_rec = alpha c + (1 - alpha) accum_rec as accum_rec + alpha (c - accum_rec)
+            const f2 d0 = splat2(w2.z) - ar0, d1 = splat2(w2.w) - ar1, d2 = splat2(w3.x) - ar2;
+            f2 dL_dopa = d0 * dLp0 + d1 * dLp1 + d2 * dLp2;
+            ar0 = __builtin_elementwise_fma(alpha, d0, ar0);
+            ar1 = __builtin_elementwise_fma(alpha, d1, ar1);
+            ar2 = __builtin_elementwise_fma(alpha, d2, ar2);
             float f[16];
             f[kAccColor + 0] = hsum(bw * dLp0);
             f[kAccColor + 1] = hsum(bw * dLp1);
             f[kAccColor + 2] = hsum(bw * dLp2);
             f2 dL_dt = zero;
             if constexpr (GEOM) {
-                const f2 n0 = splat2(w3.y), n1 = splat2(w3.z), n2 = splat2(w3.w);
-                dL_dopa += (n0 - an0) * dLn0 + (n1 - an1) * dLn1 + (n2 - an2) * dLn2;
-                an0 = alpha * n0 + one_m_alpha * an0;
-                an1 = alpha * n1 + one_m_alpha * an1;
-                an2 = alpha * n2 + one_m_alpha * an2;
+                const f2 e0 = splat2(w3.y) - an0, e1 = splat2(w3.z) - an1, e2 = splat2(w3.w) - an2;
+                dL_dopa += e0 * dLn0 + e1 * dLn1 + e2 * dLn2;
+                an0 = __builtin_elementwise_fma(alpha, e0, an0);
+                an1 = __builtin_elementwise_fma(alpha, e1, an1);
+                an2 = __builtin_elementwise_fma(alpha, e2, an2);
                 f[kAccNormal + 0] = hsum(bw * dLn0);
                 f[kAccNormal + 1] = hsum(bw * dLn1);
                 f[kAccNormal + 2] = hsum(bw * dLn2);
@@ -259,45 +263,49 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
                 const float rsig = w2.y;
                 const f2 dmt = mDepth - t_peak;
                 const f2 t_delta = dmt * rsig;
-                const f2 G_exp = {__expf(-0.5f * t_delta.x * t_delta.x), __expf(-0.5f * t_delta.y * t_delta.y)};
+                // exp(-delta^2 / 2) as exp2(delta^2 (-log2 e / 2))
+                const f2 ge = (t_delta * t_delta) * splat2(-0.72134752044448170368f);
+                const f2 G_exp = {__builtin_amdgcn_exp2f(ge.x), __builtin_amdgcn_exp2f(ge.y)};
                 const f2 Gt = alpha * G_exp;  // 0 for a non-valid pixel -> no plane terms
                 const f2 omGt = one - Gt;
-                f2 dL_dGt = kappa * 0.25f * f2{fast_rcp(omGt.x), fast_rcp(omGt.y)};
-                dL_dGt = sel2(mDepth.x > t_peak.x, mDepth.y > t_peak.y, dL_dGt, -dL_dGt);
-                dL_dGt = rsig > 0.f ? dL_dGt : zero;
+                // 0.25 kappa / (1 - Gt), + in front of the peak, - behind; 0 for a non-ball splat
+                f2 dL_dGt = (kappa_q * (rsig > 0.f ? 1.f : 0.f)) * f2{fast_rcp(omGt.x), fast_rcp(omGt.y)};
+                dL_dGt = sel2(dmt.x > 0.f, dmt.y > 0.f, dL_dGt, -dL_dGt);
                 const f2 half_r = sel2(t_delta.x > 0.f, t_delta.y > 0.f, 0.5f * r1a, zero);
                 const f2 dL_dopa_sigma = dL_dGt * G_exp - kappa * half_r;
                 const f2 dL_ddelta = -dL_dGt * Gt * t_delta;
                 dL_dt = -dL_ddelta * rsig;
-                f[kAccPlane + 0] = hsum(dL_dt) * dx;
+                const float hdt = hsum(dL_dt);
+                f[kAccPlane + 0] = hdt * dx;
                 f[kAccPlane + 1] = hsum(dL_dt * dy);
-                f[kAccPlane + 2] = hsum(dL_dt);
+                f[kAccPlane + 2] = hdt;
                 f[kAccPlane + 3] = hsum(dL_ddelta * dmt);
-                dL_dopa = dL_dopa * T + dL_dopa_sigma;
+                dL_dopa = __builtin_elementwise_fma(dL_dopa, T, dL_dopa_sigma);
             } else {
                 dL_dopa = dL_dopa * T;
             }
-            dL_dopa += -T_final * r1a * dL_dfinalT;
-            dL_dopa = sel2(va, vb, dL_dopa, zero);
-            const f2 Gc = sel2(va, vb, G, zero);
-            const f2 dL_dG = w1.y * dL_dopa;
-            const f2 gdx = Gc * dx, gdy = Gc * dy;
-            const f2 dG_ddelx = -gdx * w0.z - gdy * w0.w;
-            const f2 dG_ddely = -gdy * w1.x - gdx * w0.w;
-            f2 dL_ddelx = dL_dG * dG_ddelx;
-            f2 dL_ddely = dL_dG * dG_ddely;
+            dL_dopa = __builtin_elementwise_fma(tfd, r1a, dL_dopa);
+            // p = G dL/dopacity on the valid pixels; every remaining term is a multiple of it:
+            // dL/dG G = op p, dG/ddelx = -G (a dx + b dy), dG/ddely = -G (c dy + b dx),
+            // dG/dconic = -G/2 (dx^2, dx dy, dy^2)
+            const f2 p = sel2(va, vb, G * dL_dopa, zero);
+            const f2 q = w1.y * p;
+            const f2 nq = -q;
+            f2 dL_ddelx = nq * __builtin_elementwise_fma(splat2(w0.w), dy, splat2(w0.z * dx));
+            f2 dL_ddely = nq * __builtin_elementwise_fma(splat2(w1.x), dy, splat2(w0.w * dx));
             if constexpr (GEOM) {
-                dL_ddelx += dL_dt * w1.z;
-                dL_ddely += dL_dt * w1.w;
+                dL_ddelx = __builtin_elementwise_fma(dL_dt, splat2(w1.z), dL_ddelx);
+                dL_ddely = __builtin_elementwise_fma(dL_dt, splat2(w1.w), dL_ddely);
             }
             const f2 mx = dL_ddelx * ddelx_dx, my = dL_ddely * ddely_dy;
             f[kAccMean2D + 0] = hsum(mx);
             f[kAccMean2D + 1] = hsum(my);
             const float fabs_sum = (fabsf(mx.x) + fabsf(my.x)) + (fabsf(mx.y) + fabsf(my.y));
-            f[kAccConic + 0] = hsum(-0.5f * gdx * dx * dL_dG);
-            f[kAccConic + 1] = hsum(-0.5f * gdx * dy * dL_dG);
-            f[kAccConic + 2] = hsum(-0.5f * gdy * dy * dL_dG);
-            f[kAccConic + 3] = hsum(Gc * dL_dopa);
+            const f2 qdy = q * dy;
+            f[kAccConic + 0] = hsum(q) * (-0.5f * dx * dx);
+            f[kAccConic + 1] = hsum(qdy) * (-0.5f * dx);
+            f[kAccConic + 2] = -0.5f * hsum(qdy * dy);
+            f[kAccConic + 3] = hsum(p);
             if constexpr (!GEOM) {
 #pragma unroll
                 for (int q = kAccNormal; q < kAccFields; q++) f[q] = 0.f;
