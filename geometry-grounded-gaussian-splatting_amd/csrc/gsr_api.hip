@@ -349,7 +349,7 @@ struct StageTimer {
 }  // namespace
 
 namespace gsr {
-static int g_options[kNumOptions] = {0, 0, 0, 0, 0, 0, 0, 0};
+static int g_options[kNumOptions] = {};
 int option(int which) { return (which >= 0 && which < kNumOptions) ? g_options[which] : 0; }
 }  // namespace gsr
 

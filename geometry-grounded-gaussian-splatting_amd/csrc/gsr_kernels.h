@@ -8,7 +8,7 @@ namespace gsr {
 
 // Run-time switches for A/B variants of one kernel in one process
 // (gsr_set_option in include/gsr.h); defaults are the shipped paths.
-enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptSortbin = 7, kNumOptions = 8 };
+enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptSortbin = 7, kOptBwdNarrow = 8, kNumOptions = 9 };
 int option(int which);
 hipError_t read_render_stats(unsigned long long* out, bool reset);
 

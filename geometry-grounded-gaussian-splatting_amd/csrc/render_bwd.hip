@@ -3,9 +3,10 @@
 // Replaces renderCUDA<3, GEOMETRY> backward (render_backward.cu:716-1069) and
 // BACKWARD::render (:1164-1209).
 //
-// Same tile/workgroup geometry as render_fwd.hip.  Per (pixel, Gaussian) the
-// kernel recomputes alpha and produces up to 17 gradient terms; they are
-// summed over the 64 pixels of a wave with one transposed butterfly
+// One wave64 per 16x16 tile (four pixels per lane, in two packed pairs;
+// GSR_OPT_BWD_NARROW: two waves, one pair per lane).  Per (pixel, Gaussian)
+// the kernel recomputes alpha and produces up to 17 gradient terms; they are
+// summed over the lane's pixels, then over the wave with one transposed butterfly
 // (wave_transpose_reduce16: v_permlane32_swap / v_permlane16_swap, then DPP
 // mirrors and quad perms, all VALU), after which lanes 0, 4, ..., 60 hold the
 // 16 field totals and issue ONE global_atomic_add_f32 whose 16 field lanes
@@ -45,7 +46,6 @@ struct RenderBwdArgs {
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
-constexpr int kBwdThreads = 128;  // 2 wave64 per tile, two pixels per lane
 constexpr int kBwdBatch = 256;    // splat records staged per LDS batch
 
 __device__ __forceinline__ f2 sel2(bool ca, bool cb, f2 x, f2 y) { return f2{ca ? x.x : y.x, cb ? x.y : y.y}; }
@@ -97,14 +97,52 @@ __device__ __forceinline__ PixIn load_pixel(const RenderBwdArgs& a, int px, int 
     return r;
 }
 
-// One workgroup of 128 lanes (2 wave64) per 16x16 tile; lane l of wave w
-// owns the pixel pair (x, y) and (x, y + 4) with x = l % 16,
-// y = 8 w + l / 16.  The two pixels' state lives in the halves of packed
-// fp32 registers (v_pk_{add,mul,fma}_f32), so one instruction stream serves
-// two pixels, and the per-(wave, Gaussian) reduction and atomic cover 128
-// pixels instead of 64.  Per-pixel validity is a select, not a branch.
+// Per-lane pixel pair: the pixels (x, y) and (x, y + 4) in the halves of
+// packed fp32 registers (v_pk_{add,mul,fma}_f32), one instruction stream for
+// both.  Per-pixel validity is a select, not a branch.
+struct PixPair {
+    f2 pixy, T_final, dLp0, dLp1, dLp2, dL_dfinalT, dLn0, dLn1, dLn2, mDepth, dL_dmt, dT_cached;
+    bool ina, inb, ca, cb;
+    uint32_t last_a, last_b;
+};
+
 template <bool GEOM>
-__global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a) {
+__device__ __forceinline__ PixPair load_pair(const RenderBwdArgs& a, int px, int py) {
+    const PixIn pa = load_pixel<GEOM>(a, px, py), pb = load_pixel<GEOM>(a, px, py + 4);
+    PixPair r;
+    r.pixy = f2{(float)py, (float)(py + 4)};
+    r.T_final = f2{pa.T_final, pb.T_final};
+    r.dLp0 = f2{pa.dLp0, pb.dLp0};
+    r.dLp1 = f2{pa.dLp1, pb.dLp1};
+    r.dLp2 = f2{pa.dLp2, pb.dLp2};
+    r.dL_dfinalT = f2{pa.dL_dfinalT, pb.dL_dfinalT};
+    r.dLn0 = f2{pa.dLn0, pb.dLn0};
+    r.dLn1 = f2{pa.dLn1, pb.dLn1};
+    r.dLn2 = f2{pa.dLn2, pb.dLn2};
+    r.mDepth = f2{pa.mDepth, pb.mDepth};
+    r.dL_dmt = f2{pa.dL_dmt, pb.dL_dmt};
+    r.dT_cached = f2{pa.cached ? pa.dT_dtm : 0.f, pb.cached ? pb.dT_dtm : 0.f};
+    r.ina = pa.inside;
+    r.inb = pb.inside;
+    r.ca = pa.cached;
+    r.cb = pb.cached;
+    r.last_a = pa.last;
+    r.last_b = pb.last;
+    return r;
+}
+
+// One workgroup of 128 / NP lanes per 16x16 tile; lane l of wave w owns NP
+// pixel pairs, pair k at x = l % 16, y = 8 (NP w + k) + l / 16 (and y + 4).
+// The per-(wave, Gaussian) field sums and the one atomic instruction then
+// cover 128 NP pixels: NP = 2 (one wave per tile) halves the reductions and
+// atomics per pixel and amortises the record's shared work over 4 pixels per
+// lane, against a larger register file per wave.  Measured at C3: NP = 2 at
+// 2 waves per SIMD (180 VGPRs) 0.540 ms, at 3 (168 VGPRs) 0.568, with 2
+// spilled registers 0.619; NP = 1 0.569.
+template <bool GEOM, int NP>
+__global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(NP == 1 ? 4 : 2, NP == 1 ? 8 : 2)))
+    render_bwd_kernel(RenderBwdArgs a) {
+    constexpr int kThreads = 128 / NP;
     __shared__ float4 s_w0[kBwdBatch], s_w1[kBwdBatch], s_w2[kBwdBatch], s_w3[kBwdBatch];
     __shared__ uint32_t s_id[kBwdBatch];
 
@@ -118,22 +156,15 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
     if (max_contrib == 0) return;  // uniform over the block
 
     const int px = tx * kTile + (lane & 15);
-    const int pya = ty * kTile + wave * 8 + (lane >> 4), pyb = pya + 4;
-    const PixIn pa = load_pixel<GEOM>(a, px, pya);
-    const PixIn pb = load_pixel<GEOM>(a, px, pyb);
     const float pixx = (float)px;
-    const f2 pixy = {(float)pya, (float)pyb};
-    const bool ina = pa.inside, inb = pb.inside;
-    const uint32_t last_a = pa.last, last_b = pb.last;
-    const f2 T_final = {pa.T_final, pb.T_final};
-    const f2 dLp0 = {pa.dLp0, pb.dLp0}, dLp1 = {pa.dLp1, pb.dLp1}, dLp2 = {pa.dLp2, pb.dLp2};
-    const f2 dL_dfinalT = {pa.dL_dfinalT, pb.dL_dfinalT};
-    const f2 dLn0 = {pa.dLn0, pb.dLn0}, dLn1 = {pa.dLn1, pb.dLn1}, dLn2 = {pa.dLn2, pb.dLn2};
-    const f2 mDepth = {pa.mDepth, pb.mDepth};
+    PixPair pp[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) pp[k] = load_pair<GEOM>(a, px, ty * kTile + 8 * (NP * wave + k) + (lane >> 4));
     const int rounds = (max_contrib + kBwdBatch - 1) / kBwdBatch;
+    const f2 zero = {0.f, 0.f}, one = {1.f, 1.f};
 
     auto stage_fwd = [&](int i) {
-        for (int k = tid; k < kBwdBatch; k += kBwdThreads) {
+        for (int k = tid; k < kBwdBatch; k += kThreads) {
             const int c = i * kBwdBatch + k;
             if (c < max_contrib) {
                 const Splat* sp = a.splats + a.point_list[range.x + c];
@@ -148,13 +179,23 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
     // Pixels whose mdepth is the forward's own output take dT/dt_m from the
     // forward (render_fwd.hip); the others (an mdepth the caller changed, a
     // tile too long for the forward's LDS cache) recompute it here.
-    f2 kappa = {0.f, 0.f};
+    f2 kappa[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) kappa[k] = zero;
     if (GEOM && !a.skip_prepass) {
-        f2 dT_dtm = {pa.cached ? pa.dT_dtm : 0.f, pb.cached ? pb.dT_dtm : 0.f};
-        const bool on_a = ina && pa.mDepth != 0.f && last_a != 0 && !pa.cached;
-        const bool on_b = inb && pb.mDepth != 0.f && last_b != 0 && !pb.cached;
-        const uint32_t wave_last = wave_max_u(max(on_a ? last_a : 0u, on_b ? last_b : 0u));
-        const bool block_needs = __syncthreads_or(wave_last != 0u);
+        f2 dT_dtm[NP];
+        bool on_a[NP], on_b[NP];
+        uint32_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            const PixPair& P = pp[k];
+            dT_dtm[k] = P.dT_cached;
+            on_a[k] = P.ina && P.mDepth.x != 0.f && P.last_a != 0 && !P.ca;
+            on_b[k] = P.inb && P.mDepth.y != 0.f && P.last_b != 0 && !P.cb;
+            mine = max(mine, max(on_a[k] ? P.last_a : 0u, on_b[k] ? P.last_b : 0u));
+        }
+        const uint32_t wave_last = wave_max_u(mine);
+        const bool block_needs = NP == 2 ? wave_last != 0u : __syncthreads_or(wave_last != 0u);
         uint32_t c = 0;
         int toDo = max_contrib;
         for (int i = 0; block_needs && i < rounds; i++, toDo -= kBwdBatch) {
@@ -166,24 +207,30 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
                 c++;
                 const float4 w0 = s_w0[j];
                 const float4 w1 = s_w1[j];
-                const float dx = w0.x - pixx;
-                const f2 dy = splat2(w0.y) - pixy;
-                const f2 power = splat_power2(w0, w1, dx, dy);
-                const f2 alpha = {fminf(0.99f, w1.y * __expf(power.x)), fminf(0.99f, w1.y * __expf(power.y))};
-                const bool va = on_a && c <= last_a && !(power.x > 0.f) && !(alpha.x < 1.0f / 255.0f);
-                const bool vb = on_b && c <= last_b && !(power.y > 0.f) && !(alpha.y < 1.0f / 255.0f);
                 const float4 w2 = s_w2[j];
-                const f2 t_peak = splat_tpeak2(w1, w2, dx, dy);
+                const float dx = w0.x - pixx;
                 const float rsig = w2.y;
-                const f2 t_delta = (mDepth - t_peak) * rsig;
-                const f2 G_exp = {__expf(-0.5f * t_delta.x * t_delta.x), __expf(-0.5f * t_delta.y * t_delta.y)};
-                const f2 Gt = alpha * G_exp;
-                const f2 term = f2{fast_div(-0.25f * Gt.x, 1.f - Gt.x), fast_div(-0.25f * Gt.y, 1.f - Gt.y)} *
-                                f2{fabsf(t_delta.x), fabsf(t_delta.y)} * rsig;
-                dT_dtm += sel2(va, vb, term, splat2(0.f));
+#pragma unroll
+                for (int k = 0; k < NP; k++) {
+                    const PixPair& P = pp[k];
+                    const f2 dy = splat2(w0.y) - P.pixy;
+                    const f2 power = splat_power2(w0, w1, dx, dy);
+                    const f2 alpha = {fminf(0.99f, w1.y * __expf(power.x)), fminf(0.99f, w1.y * __expf(power.y))};
+                    const bool va = on_a[k] && c <= P.last_a && !(power.x > 0.f) && !(alpha.x < 1.0f / 255.0f);
+                    const bool vb = on_b[k] && c <= P.last_b && !(power.y > 0.f) && !(alpha.y < 1.0f / 255.0f);
+                    const f2 t_peak = splat_tpeak2(w1, w2, dx, dy);
+                    const f2 t_delta = (P.mDepth - t_peak) * rsig;
+                    const f2 G_exp = {__expf(-0.5f * t_delta.x * t_delta.x), __expf(-0.5f * t_delta.y * t_delta.y)};
+                    const f2 Gt = alpha * G_exp;
+                    const f2 term = f2{fast_div(-0.25f * Gt.x, 1.f - Gt.x), fast_div(-0.25f * Gt.y, 1.f - Gt.y)} *
+                                    f2{fabsf(t_delta.x), fabsf(t_delta.y)} * rsig;
+                    dT_dtm[k] += sel2(va, vb, term, zero);
+                }
             }
         }
-        kappa = f2{pa.dL_dmt / fmaxf(-dT_dtm.x, 1e-7f), pb.dL_dmt / fmaxf(-dT_dtm.y, 1e-7f)};
+#pragma unroll
+        for (int k = 0; k < NP; k++)
+            kappa[k] = f2{pp[k].dL_dmt.x / fmaxf(-dT_dtm[k].x, 1e-7f), pp[k].dL_dmt.y / fmaxf(-dT_dtm[k].y, 1e-7f)};
     }
 
     // ---- main back-to-front pass (render_backward.cu:882-1068)
@@ -195,17 +242,20 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
     // T (x rcp(1) = 1), accum_rec (+ 0 x d) and the plane terms unchanged
     // exactly, so only G dL/dopacity needs a select.
     uint32_t contributor = (uint32_t)max_contrib;
-    f2 T = T_final;
-    const f2 tfd = -T_final * dL_dfinalT;  // dL/dopacity term of the final transmittance, / (1 - alpha)
-    const f2 kappa_q = 0.25f * kappa;
-    f2 ar0 = {0.f, 0.f}, ar1 = {0.f, 0.f}, ar2 = {0.f, 0.f};
-    f2 an0 = {0.f, 0.f}, an1 = {0.f, 0.f}, an2 = {0.f, 0.f};
+    f2 T[NP], tfd[NP], kh[NP], ar0[NP], ar1[NP], ar2[NP], an0[NP], an1[NP], an2[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        T[k] = pp[k].T_final;
+        tfd[k] = -pp[k].T_final * pp[k].dL_dfinalT;  // dL/dopacity term of the final transmittance, / (1 - alpha)
+        kh[k] = 0.5f * kappa[k];
+        ar0[k] = ar1[k] = ar2[k] = zero;
+        an0[k] = an1[k] = an2[k] = zero;
+    }
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
-    const f2 zero = {0.f, 0.f}, one = {1.f, 1.f};
     int toDo = max_contrib;
     for (int i = 0; i < rounds; i++, toDo -= kBwdBatch) {
         __syncthreads();
-        for (int k = tid; k < kBwdBatch; k += kBwdThreads) {
+        for (int k = tid; k < kBwdBatch; k += kThreads) {
             const int c = i * kBwdBatch + k;
             if (c < max_contrib) {
                 const uint32_t g = a.point_list[range.x + max_contrib - c - 1];
@@ -224,89 +274,125 @@ __global__ void __launch_bounds__(kBwdThreads) render_bwd_kernel(RenderBwdArgs a
             const float4 w0 = s_w0[j];
             const float4 w1 = s_w1[j];
             const float dx = w0.x - pixx;
-            const f2 dy = splat2(w0.y) - pixy;
-            const f2 power = splat_power2(w0, w1, dx, dy);
-            const f2 G = {__expf(power.x), __expf(power.y)};
-            const f2 alpha_raw = {fminf(0.99f, w1.y * G.x), fminf(0.99f, w1.y * G.y)};
-            const bool va = ina && !(contributor >= last_a || power.x > 0.0f || alpha_raw.x < 1.0f / 255.0f);
-            const bool vb = inb && !(contributor >= last_b || power.y > 0.0f || alpha_raw.y < 1.0f / 255.0f);
-            if (__ballot(va || vb) == 0ull) continue;  // wave-uniform skip (warp.any)
+            f2 dy[NP], G[NP], alpha_raw[NP];
+            bool va[NP], vb[NP];
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                dy[k] = splat2(w0.y) - pp[k].pixy;
+                const f2 power = splat_power2(w0, w1, dx, dy[k]);
+                G[k] = f2{__expf(power.x), __expf(power.y)};
+                alpha_raw[k] = f2{fminf(0.99f, w1.y * G[k].x), fminf(0.99f, w1.y * G[k].y)};
+                va[k] = pp[k].ina && !(contributor >= pp[k].last_a || power.x > 0.0f || alpha_raw[k].x < 1.0f / 255.0f);
+                vb[k] = pp[k].inb && !(contributor >= pp[k].last_b || power.y > 0.0f || alpha_raw[k].y < 1.0f / 255.0f);
+                any = any || va[k] || vb[k];
+            }
+            if (__ballot(any) == 0ull) continue;  // wave-uniform skip (warp.any)
 
             const float4 w2 = s_w2[j];
             const float4 w3 = s_w3[j];
-            const f2 alpha = sel2(va, vb, alpha_raw, zero);
-            const f2 one_m_alpha = one - alpha;
-            const f2 r1a = {fast_rcp(one_m_alpha.x), fast_rcp(one_m_alpha.y)};
-            T = T * r1a;
-            const f2 bw = alpha * T;
-            // accum_rec = alpha c + (1 - alpha) accum_rec as accum_rec + alpha (c - accum_rec)
-            const f2 d0 = splat2(w2.z) - ar0, d1 = splat2(w2.w) - ar1, d2 = splat2(w3.x) - ar2;
-            f2 dL_dopa = d0 * dLp0 + d1 * dLp1 + d2 * dLp2;
-            ar0 = __builtin_elementwise_fma(alpha, d0, ar0);
-            ar1 = __builtin_elementwise_fma(alpha, d1, ar1);
-            ar2 = __builtin_elementwise_fma(alpha, d2, ar2);
+            const float rsig = w2.y;
+            const float ks = rsig > 0.f ? 0.5f : 0.f;  // 0.25 kappa = 0.5 kh; non-ball splat: no plane terms
+            // field sums over the lane's pixels (the conic / plane terms keep
+            // their per-lane factors dx out of the sums)
+            f2 Fc0, Fc1, Fc2, Fn0, Fn1, Fn2, Fdt, Fdtdy, Fdd, Fmx, Fmy, Fq, Fqdy, Fqdy2, Fp;
+            float fabs_sum = 0.f;
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                const PixPair& P = pp[k];
+                const f2 alpha = sel2(va[k], vb[k], alpha_raw[k], zero);
+                const f2 one_m_alpha = one - alpha;
+                const f2 r1a = {fast_rcp(one_m_alpha.x), fast_rcp(one_m_alpha.y)};
+                T[k] = T[k] * r1a;
+                const f2 bw = alpha * T[k];
+                // accum_rec = alpha c + (1 - alpha) accum_rec as accum_rec + alpha (c - accum_rec)
+                const f2 d0 = splat2(w2.z) - ar0[k], d1 = splat2(w2.w) - ar1[k], d2 = splat2(w3.x) - ar2[k];
+                f2 dL_dopa = d0 * P.dLp0 + d1 * P.dLp1 + d2 * P.dLp2;
+                ar0[k] = __builtin_elementwise_fma(alpha, d0, ar0[k]);
+                ar1[k] = __builtin_elementwise_fma(alpha, d1, ar1[k]);
+                ar2[k] = __builtin_elementwise_fma(alpha, d2, ar2[k]);
+                const f2 c0 = bw * P.dLp0, c1 = bw * P.dLp1, c2 = bw * P.dLp2;
+                Fc0 = k ? Fc0 + c0 : c0;
+                Fc1 = k ? Fc1 + c1 : c1;
+                Fc2 = k ? Fc2 + c2 : c2;
+                f2 dL_dt = zero;
+                if constexpr (GEOM) {
+                    const f2 e0 = splat2(w3.y) - an0[k], e1 = splat2(w3.z) - an1[k], e2 = splat2(w3.w) - an2[k];
+                    dL_dopa += e0 * P.dLn0 + e1 * P.dLn1 + e2 * P.dLn2;
+                    an0[k] = __builtin_elementwise_fma(alpha, e0, an0[k]);
+                    an1[k] = __builtin_elementwise_fma(alpha, e1, an1[k]);
+                    an2[k] = __builtin_elementwise_fma(alpha, e2, an2[k]);
+                    const f2 n0 = bw * P.dLn0, n1 = bw * P.dLn1, n2 = bw * P.dLn2;
+                    Fn0 = k ? Fn0 + n0 : n0;
+                    Fn1 = k ? Fn1 + n1 : n1;
+                    Fn2 = k ? Fn2 + n2 : n2;
+                    const f2 t_peak = splat_tpeak2(w1, w2, dx, dy[k]);
+                    const f2 dmt = P.mDepth - t_peak;
+                    const f2 t_delta = dmt * rsig;
+                    // exp(-delta^2 / 2) as exp2(delta^2 (-log2 e / 2))
+                    const f2 ge = (t_delta * t_delta) * splat2(-0.72134752044448170368f);
+                    const f2 G_exp = {__builtin_amdgcn_exp2f(ge.x), __builtin_amdgcn_exp2f(ge.y)};
+                    const f2 Gt = alpha * G_exp;  // 0 for a non-valid pixel -> no plane terms
+                    const f2 omGt = one - Gt;
+                    // 0.25 kappa / (1 - Gt), + in front of the peak, - behind
+                    f2 dL_dGt = (kh[k] * ks) * f2{fast_rcp(omGt.x), fast_rcp(omGt.y)};
+                    dL_dGt = sel2(dmt.x > 0.f, dmt.y > 0.f, dL_dGt, -dL_dGt);
+                    // kappa (0.5 / (1 - alpha)) behind the peak (kh = kappa / 2: the same rounding)
+                    const f2 kr = sel2(t_delta.x > 0.f, t_delta.y > 0.f, kh[k] * r1a, zero);
+                    const f2 dL_dopa_sigma = dL_dGt * G_exp - kr;
+                    const f2 dL_ddelta = -dL_dGt * Gt * t_delta;
+                    dL_dt = -dL_ddelta * rsig;
+                    const f2 dtdy = dL_dt * dy[k], dd = dL_ddelta * dmt;
+                    Fdt = k ? Fdt + dL_dt : dL_dt;
+                    Fdtdy = k ? Fdtdy + dtdy : dtdy;
+                    Fdd = k ? Fdd + dd : dd;
+                    dL_dopa = __builtin_elementwise_fma(dL_dopa, T[k], dL_dopa_sigma);
+                } else {
+                    dL_dopa = dL_dopa * T[k];
+                }
+                dL_dopa = __builtin_elementwise_fma(tfd[k], r1a, dL_dopa);
+                // p = G dL/dopacity on the valid pixels; every remaining term is a multiple of it:
+                // dL/dG G = op p, dG/ddelx = -G (a dx + b dy), dG/ddely = -G (c dy + b dx),
+                // dG/dconic = -G/2 (dx^2, dx dy, dy^2)
+                const f2 p = sel2(va[k], vb[k], G[k] * dL_dopa, zero);
+                const f2 q = w1.y * p;
+                const f2 nq = -q;
+                f2 dL_ddelx = nq * __builtin_elementwise_fma(splat2(w0.w), dy[k], splat2(w0.z * dx));
+                f2 dL_ddely = nq * __builtin_elementwise_fma(splat2(w1.x), dy[k], splat2(w0.w * dx));
+                if constexpr (GEOM) {
+                    dL_ddelx = __builtin_elementwise_fma(dL_dt, splat2(w1.z), dL_ddelx);
+                    dL_ddely = __builtin_elementwise_fma(dL_dt, splat2(w1.w), dL_ddely);
+                }
+                const f2 mx = dL_ddelx * ddelx_dx, my = dL_ddely * ddely_dy;
+                fabs_sum += (fabsf(mx.x) + fabsf(my.x)) + (fabsf(mx.y) + fabsf(my.y));
+                const f2 qdy = q * dy[k], qdy2 = qdy * dy[k];
+                Fmx = k ? Fmx + mx : mx;
+                Fmy = k ? Fmy + my : my;
+                Fq = k ? Fq + q : q;
+                Fqdy = k ? Fqdy + qdy : qdy;
+                Fqdy2 = k ? Fqdy2 + qdy2 : qdy2;
+                Fp = k ? Fp + p : p;
+            }
             float f[16];
-            f[kAccColor + 0] = hsum(bw * dLp0);
-            f[kAccColor + 1] = hsum(bw * dLp1);
-            f[kAccColor + 2] = hsum(bw * dLp2);
-            f2 dL_dt = zero;
+            f[kAccColor + 0] = hsum(Fc0);
+            f[kAccColor + 1] = hsum(Fc1);
+            f[kAccColor + 2] = hsum(Fc2);
+            f[kAccMean2D + 0] = hsum(Fmx);
+            f[kAccMean2D + 1] = hsum(Fmy);
+            f[kAccConic + 0] = hsum(Fq) * (-0.5f * dx * dx);
+            f[kAccConic + 1] = hsum(Fqdy) * (-0.5f * dx);
+            f[kAccConic + 2] = -0.5f * hsum(Fqdy2);
+            f[kAccConic + 3] = hsum(Fp);
             if constexpr (GEOM) {
-                const f2 e0 = splat2(w3.y) - an0, e1 = splat2(w3.z) - an1, e2 = splat2(w3.w) - an2;
-                dL_dopa += e0 * dLn0 + e1 * dLn1 + e2 * dLn2;
-                an0 = __builtin_elementwise_fma(alpha, e0, an0);
-                an1 = __builtin_elementwise_fma(alpha, e1, an1);
-                an2 = __builtin_elementwise_fma(alpha, e2, an2);
-                f[kAccNormal + 0] = hsum(bw * dLn0);
-                f[kAccNormal + 1] = hsum(bw * dLn1);
-                f[kAccNormal + 2] = hsum(bw * dLn2);
-                const f2 t_peak = splat_tpeak2(w1, w2, dx, dy);
-                const float rsig = w2.y;
-                const f2 dmt = mDepth - t_peak;
-                const f2 t_delta = dmt * rsig;
-                // exp(-delta^2 / 2) as exp2(delta^2 (-log2 e / 2))
-                const f2 ge = (t_delta * t_delta) * splat2(-0.72134752044448170368f);
-                const f2 G_exp = {__builtin_amdgcn_exp2f(ge.x), __builtin_amdgcn_exp2f(ge.y)};
-                const f2 Gt = alpha * G_exp;  // 0 for a non-valid pixel -> no plane terms
-                const f2 omGt = one - Gt;
-                // 0.25 kappa / (1 - Gt), + in front of the peak, - behind; 0 for a non-ball splat
-                f2 dL_dGt = (kappa_q * (rsig > 0.f ? 1.f : 0.f)) * f2{fast_rcp(omGt.x), fast_rcp(omGt.y)};
-                dL_dGt = sel2(dmt.x > 0.f, dmt.y > 0.f, dL_dGt, -dL_dGt);
-                const f2 half_r = sel2(t_delta.x > 0.f, t_delta.y > 0.f, 0.5f * r1a, zero);
-                const f2 dL_dopa_sigma = dL_dGt * G_exp - kappa * half_r;
-                const f2 dL_ddelta = -dL_dGt * Gt * t_delta;
-                dL_dt = -dL_ddelta * rsig;
-                const float hdt = hsum(dL_dt);
+                f[kAccNormal + 0] = hsum(Fn0);
+                f[kAccNormal + 1] = hsum(Fn1);
+                f[kAccNormal + 2] = hsum(Fn2);
+                const float hdt = hsum(Fdt);
                 f[kAccPlane + 0] = hdt * dx;
-                f[kAccPlane + 1] = hsum(dL_dt * dy);
+                f[kAccPlane + 1] = hsum(Fdtdy);
                 f[kAccPlane + 2] = hdt;
-                f[kAccPlane + 3] = hsum(dL_ddelta * dmt);
-                dL_dopa = __builtin_elementwise_fma(dL_dopa, T, dL_dopa_sigma);
+                f[kAccPlane + 3] = hsum(Fdd);
             } else {
-                dL_dopa = dL_dopa * T;
-            }
-            dL_dopa = __builtin_elementwise_fma(tfd, r1a, dL_dopa);
-            // p = G dL/dopacity on the valid pixels; every remaining term is a multiple of it:
-            // dL/dG G = op p, dG/ddelx = -G (a dx + b dy), dG/ddely = -G (c dy + b dx),
-            // dG/dconic = -G/2 (dx^2, dx dy, dy^2)
-            const f2 p = sel2(va, vb, G * dL_dopa, zero);
-            const f2 q = w1.y * p;
-            const f2 nq = -q;
-            f2 dL_ddelx = nq * __builtin_elementwise_fma(splat2(w0.w), dy, splat2(w0.z * dx));
-            f2 dL_ddely = nq * __builtin_elementwise_fma(splat2(w1.x), dy, splat2(w0.w * dx));
-            if constexpr (GEOM) {
-                dL_ddelx = __builtin_elementwise_fma(dL_dt, splat2(w1.z), dL_ddelx);
-                dL_ddely = __builtin_elementwise_fma(dL_dt, splat2(w1.w), dL_ddely);
-            }
-            const f2 mx = dL_ddelx * ddelx_dx, my = dL_ddely * ddely_dy;
-            f[kAccMean2D + 0] = hsum(mx);
-            f[kAccMean2D + 1] = hsum(my);
-            const float fabs_sum = (fabsf(mx.x) + fabsf(my.x)) + (fabsf(mx.y) + fabsf(my.y));
-            const f2 qdy = q * dy;
-            f[kAccConic + 0] = hsum(q) * (-0.5f * dx * dx);
-            f[kAccConic + 1] = hsum(qdy) * (-0.5f * dx);
-            f[kAccConic + 2] = -0.5f * hsum(qdy * dy);
-            f[kAccConic + 3] = hsum(p);
-            if constexpr (!GEOM) {
 #pragma unroll
                 for (int q = kAccNormal; q < kAccFields; q++) f[q] = 0.f;
             }
@@ -355,10 +441,18 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.no_cache = option(kOptBwdNoCache);
     a.tile_order = ws.tile_order;
     if (a.num_tiles == 0) return hipSuccess;
-    if (p.require_depth)
-        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(a.num_tiles), dim3(kBwdThreads), 0, stream, a);
-    else
-        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(a.num_tiles), dim3(kBwdThreads), 0, stream, a);
+    const bool wide = !option(kOptBwdNarrow);
+    if (p.require_depth) {
+        if (wide)
+            hipLaunchKernelGGL((render_bwd_kernel<true, 2>), dim3(a.num_tiles), dim3(64), 0, stream, a);
+        else
+            hipLaunchKernelGGL((render_bwd_kernel<true, 1>), dim3(a.num_tiles), dim3(128), 0, stream, a);
+    } else {
+        if (wide)
+            hipLaunchKernelGGL((render_bwd_kernel<false, 2>), dim3(a.num_tiles), dim3(64), 0, stream, a);
+        else
+            hipLaunchKernelGGL((render_bwd_kernel<false, 1>), dim3(a.num_tiles), dim3(128), 0, stream, a);
+    }
     return hipGetLastError();
 }
 

@@ -116,6 +116,7 @@ OPT_NO_TILE_ORDER = 4
 OPT_NO_REFINE = 5
 OPT_BWD_NO_CACHE = 6
 OPT_SORTBIN = 7
+OPT_BWD_NARROW = 8
 
 
 def debug_render_stats(reset: bool = True) -> list:

@@ -158,6 +158,21 @@ def test_parity_small(case):
     _run(Hh.small_case(kernel_size=ks, **case))
 
 
+@pytest.mark.parametrize("case", [SMALL[1], SMALL[6], SMALL[8]], ids=["geom", "nogeom", "C1"])
+def test_parity_backward_narrow(case):
+    """The backward's two-waves-per-tile layout (GSR_OPT_BWD_NARROW: 2 pixels
+    per lane) against the oracle, as the default one-wave layout above."""
+    from diff_gaussian_rasterization import _C
+
+    case = dict(case)
+    ks = case.pop("kernel_size", 0.0)
+    _C.set_option(_C.OPT_BWD_NARROW, 1)
+    try:
+        _run(Hh.small_case(kernel_size=ks, **case))
+    finally:
+        _C.set_option(_C.OPT_BWD_NARROW, 0)
+
+
 def _with_depth_ties(c, n_tied):
     """Gaussians n_tied..2 n_tied-1 get the means of 0..n_tied-1: bit-identical
     depths, so the per-tile order of each pair is decided by the index alone
