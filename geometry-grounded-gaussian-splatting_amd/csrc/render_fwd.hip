@@ -245,7 +245,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
     constexpr int kPub = (GEOM && !SAMPLE) ? kTilePixels : 1;
     __shared__ uint32_t s_pub_last[kPub];
     __shared__ float s_pub_m0[kPub], s_pub_T[kPub];
-    __shared__ float s_groot[(GEOM && !SAMPLE) ? 64 : 1];
+    __shared__ float s_groot[(GEOM && !SAMPLE) ? 64 : 1];  // then the compacted phase-2 list (bytes)
+    __shared__ float s_pub_hi[kPub];
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -300,12 +301,73 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
     }
 
     float T = 1.0f, T_pt = 1.0f;
-    uint32_t contributor = 0, last = 0;
+    uint32_t last = 0;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
     float N0 = 0.f, N1 = 0.f, N2 = 0.f, m_init = 0.f;
     bool done = !inside;
 
     unsigned long long cst[2] = {0, 0};  // (STATS) composite wave-steps, blending lanes
+    // One list entry g (0-based) at this lane, the reference's per-pixel loop
+    // body: w0, w1 are the record's footprint words, w2f / w3f fetch the rest
+    // only when the lane blends.
+    auto step = [&](const float4& w0, const float4& w1, auto&& w2f, auto&& w3f, int g) {
+        if constexpr (STATS) {
+            const unsigned long long m = __ballot(1);
+            if ((tid & 63) == __builtin_ctzll(m)) cst[0] += 1;
+        }
+        const float dx = w0.x - pixx, dy = w0.y - pixy;
+        const float power = splat_power(w0, w1, dx, dy);
+        // the reference's three early-outs (power > 0, alpha < 1/255,
+        // saturation) as one branch: every lane evaluates alpha and test_T
+        const float alpha = fminf(0.99f, w1.y * __expf(power));
+        const float test_T = T * (1.f - alpha);
+        const bool pass = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const bool sat = test_T < 0.0001f;
+        if (!pass || sat) {
+            done = done || (pass && sat);
+            return;
+        }
+        if constexpr (STATS) {
+            const unsigned long long m = __ballot(1);
+            if ((tid & 63) == __builtin_ctzll(m)) cst[1] += __popcll(m);
+        }
+        const float aT = alpha * T;
+        const float4 w2 = w2f();
+        if constexpr (SAMPLE && !GEOM) {
+            // vacancy transmittance at the point (sample_forward.cu:152-160)
+            const float t_peak = splat_tpeak(w1, w2, dx, dy);
+            const float rsigma = w2.y;
+            const float delta = (t_peak - pt_t) * rsigma;
+            const float gg = rsigma > 0.f ? __expf(-0.5f * delta * delta) : 0.f;
+            const float omg = 1.f - alpha * gg;
+            T_pt *= (pt_t > t_peak ? 1.f - alpha : omg) * __builtin_amdgcn_rsqf(omg);
+        }
+        if constexpr (!SAMPLE) {
+            const float4 w3 = w3f();
+            C0 = __builtin_fmaf(w2.z, aT, C0);
+            C1 = __builtin_fmaf(w2.w, aT, C1);
+            C2 = __builtin_fmaf(w3.x, aT, C2);
+            if constexpr (GEOM) {
+                N0 = __builtin_fmaf(w3.y, aT, N0);
+                N1 = __builtin_fmaf(w3.z, aT, N1);
+                N2 = __builtin_fmaf(w3.w, aT, N2);
+            }
+        }
+        if constexpr (GEOM) {
+            const float t = splat_tpeak(w1, w2, dx, dy);
+            m_init = T > 0.5f ? t : m_init;
+            if (g < kResident) {
+                if ((g >> 5) != mask_w) {
+                    my_mask[mask_w * kTilePixels] = mask_cur;
+                    mask_cur = 0u;
+                    mask_w = g >> 5;
+                }
+                mask_cur |= 1u << (g & 31);
+            }
+        }
+        T = test_T;
+        last = (uint32_t)g + 1u;  // the reference's 1-based contributor index
+    };
     int toDo = total;
     for (int i = 0; i < rounds; i++, toDo -= kTilePixels) {
         // block-wide early exit: every wave publishes whether any lane is live
@@ -323,66 +385,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
         }
         __syncthreads();
         const int n = min(kTilePixels, toDo);
-        for (int j = 0; !done && j < n; j++) {
-            contributor++;
-            if constexpr (STATS) {
-                const unsigned long long m = __ballot(1);
-                if ((tid & 63) == __builtin_ctzll(m)) cst[0] += 1;
-            }
-            const float4 w0 = s_w0[j];
-            const float dx = w0.x - pixx, dy = w0.y - pixy;
-            const float4 w1 = s_w1[j];
-            const float power = splat_power(w0, w1, dx, dy);
-            if (power > 0.0f) continue;
-            const float alpha = fminf(0.99f, w1.y * __expf(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1.f - alpha);
-            if (test_T < 0.0001f) {
-                done = true;
-                continue;
-            }
-            if constexpr (STATS) {
-                const unsigned long long m = __ballot(1);
-                if ((tid & 63) == __builtin_ctzll(m)) cst[1] += __popcll(m);
-            }
-            const float aT = alpha * T;
-            const float4 w2 = s_w2[j];
-            if constexpr (SAMPLE && !GEOM) {
-                // vacancy transmittance at the point (sample_forward.cu:152-160)
-                const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                const float rsigma = w2.y;
-                const float delta = (t_peak - pt_t) * rsigma;
-                const float g = rsigma > 0.f ? __expf(-0.5f * delta * delta) : 0.f;
-                const float omg = 1.f - alpha * g;
-                T_pt *= (pt_t > t_peak ? 1.f - alpha : omg) * __builtin_amdgcn_rsqf(omg);
-            }
-            if constexpr (!SAMPLE) {
-                const float4 w3 = s_w3[j];
-                C0 = __builtin_fmaf(w2.z, aT, C0);
-                C1 = __builtin_fmaf(w2.w, aT, C1);
-                C2 = __builtin_fmaf(w3.x, aT, C2);
-                if constexpr (GEOM) {
-                    N0 = __builtin_fmaf(w3.y, aT, N0);
-                    N1 = __builtin_fmaf(w3.z, aT, N1);
-                    N2 = __builtin_fmaf(w3.w, aT, N2);
-                }
-            }
-            if constexpr (GEOM) {
-                const float t = splat_tpeak(w1, w2, dx, dy);
-                m_init = T > 0.5f ? t : m_init;
-                const int g = i * kTilePixels + j;
-                if (g < kResident) {
-                    if ((g >> 5) != mask_w) {
-                        my_mask[mask_w * kTilePixels] = mask_cur;
-                        mask_cur = 0u;
-                        mask_w = g >> 5;
-                    }
-                    mask_cur |= 1u << (g & 31);
-                }
-            }
-            T = test_T;
-            last = contributor;
-        }
+        for (int j = 0; !done && j < n; j++)
+            step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kTilePixels + j);
     }
 
     if constexpr (GEOM) my_mask[mask_w * kTilePixels] = mask_cur;
@@ -577,19 +581,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
             }
             return v;
         };
-        // Halley walks from t in the bracket [lo, hi] (H(lo) >= 0 >= H(hi)).  With `ends`,
-        // the first walk also evaluates T at the window ends e0, e8 and sets in_range.
+        // Up to `walks` Halley walks from t in the bracket [lo, hi] (H(lo) >= 0 >= H(hi)),
+        // tolerances relative to `scale`.  With `ends`, the first walk also evaluates T at the
+        // window ends e0, e8 and sets in_range.  A lane still live on return continues from
+        // (t, lo, hi).
         struct Refine {
-            bool refined, in_range;
+            bool refined, in_range, live;
             float t_ref, ref_t, ref_D, ref_E;
+            float t, lo, hi;
         };
         auto halley = [&](const uint32_t* mask, uint32_t plast, float ppx, float ppy, uint32_t filter, bool grouped,
-                          bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0) {
-            Refine r{false, in_range0, 0.f, 0.f, 0.f, 0.f};
-            const float scale = fmaxf(t, 1.f);
+                          bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
+                          int walks, float scale) {
+            Refine r{false, in_range0, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             const float tol = kRefineTol * scale, tol_cond = kCondTol * scale;
             const f32x2 TSE[1] = {f32x2{e0, e8}};
-            for (int k = 0; k < kRefineWalks && a.passes > 1; k++) {
+            for (int k = 0; k < walks && a.passes > 1; k++) {
                 if (__ballot(live) == 0ull) break;
                 float A = 1.f, B = 1.f, D = 0.f, E = 0.f;
                 f32x2 AE[1] = {f32x2{1.f, 1.f}}, BE[1] = {f32x2{1.f, 1.f}};
@@ -641,7 +648,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
             if (a.passes == 1 && r.in_range) {  // diagnostic timing of the probe walk alone
                 r.refined = true;
                 r.t_ref = t;
+                live = false;
             }
+            r.live = live;
+            r.t = t;
+            r.lo = lo;
+            r.hi = hi;
             return r;
         };
         // Probe walk (window ends + m0 + kProbeOffsets * SAMPLE_RANGE), then the
@@ -699,7 +711,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
             float wsec = Hlo / (Hlo - Hhi);
             wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
             const float t = __builtin_fmaf(wsec, hi - lo, lo);
-            return halley(mask, plast, ppx, ppy, filter, grouped, pin, t, lo, hi, false, 0.f, 0.f, pin);
+            return halley(mask, plast, ppx, ppy, filter, grouped, pin, t, lo, hi, false, 0.f, 0.f, pin, kRefineWalks,
+                          fmaxf(t, 1.f));
         };
         bool have_out = false;  // (render path) md_out and dT/dt_m published by the pixel's worker
         if (a.refine && resident && a.passes > 0) {
@@ -709,10 +722,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
             if constexpr (!SAMPLE) {
                 // Two phases over the tile (render_fwd.hip header, tools/sim/s4_sim.py):
                 //  1. the 64 pixels of the even grid (x, y even), 4 lanes each: probe walk + Halley;
-                //  2. the other 192, one lane each on 3 of the 4 waves: Halley walks from the mean of
+                //  2. the other 192, one lane each on 3 of the 4 waves: a Halley walk from the mean of
                 //     their grid neighbours' roots (the median depth varies slowly: the guess is within
                 //     2e-4 of the root for 90% of pixels at C3, against ~1e-3 for the probe bracket),
-                //     the first walk also sampling the window ends for in_range.
+                //     also sampling the window ends for in_range; the ~30% not converged after it are
+                //     compacted and continued by groups of 4 lanes (walk wave-steps at C3 3.08M with
+                //     42 active lanes per step -> 2.53M with 51).
                 // The owner lane then takes the result, or runs the reference's passes where there is
                 // none (not converged, ill-conditioned, no grid neighbour with a root).
                 const int x0 = px - (tid & 15), y0 = py - (tid >> 4);
@@ -748,11 +763,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
                 }
                 __syncthreads();
                 const int skip = (int)(blockIdx.x & 3u);  // the wave left idle (rotated over the SIMDs)
-                if (wave != skip) {  // phase 2
+                bool live2 = false;  // phase-2 pixel not converged after its first walk
+                int p2 = 0;
+                if (wave != skip) {  // phase 2, first walk
                     const int k = (wave < skip ? wave : wave - 1) * 64 + (tid & 63);
                     const int pair = k / 24, r24 = k - pair * 24;
                     const int lx = r24 < 8 ? 2 * r24 + 1 : r24 - 8, ly = r24 < 8 ? 2 * pair : 2 * pair + 1;
                     const int p = ly * 16 + lx;
+                    p2 = p;
                     const float qx = (float)(x0 + lx), qy = (float)(y0 + ly);
                     const uint32_t ql = s_pub_last[p];
                     const float qm0 = s_pub_m0[p], qT = s_pub_T[p];
@@ -779,9 +797,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
                     const float e0 = lo_w, e8 = __builtin_fmaf(interval, (float)kSplit, lo_w);
                     const float t0 = cnt ? fminf(fmaxf(sum / (float)cnt, e0), e8) : e0;
                     const Refine r = halley(s_mask + p, ql, qx, qy, ~0u, false, qin && cnt > 0, t0, e0, e8, true, e0,
-                                            e8, qin);
-                    if (cnt > 0 || !qin) publish(p, qx, qy, r);
-                    else s_pub_last[p] = 0u;  // no guess: the owner runs the passes
+                                            e8, qin, 1, fmaxf(t0, 1.f));
+                    live2 = r.live;
+                    if (live2) {  // continued by a lane group below
+                        s_pub_last[p] = ql;
+                        s_pub_T[p] = r.t;
+                        s_pub_m0[p] = r.lo;
+                        s_pub_hi[p] = r.hi;
+                    } else if (cnt > 0 || !qin) {
+                        publish(p, qx, qy, r);
+                    } else {
+                        s_pub_last[p] = 0u;  // no guess: the owner runs the passes
+                    }
+                }
+                // The pixels not converged after one walk (~30% at C3), compacted and continued by
+                // groups of 4 lanes (as phase 1): their second walk no longer holds every lane of
+                // the three phase-2 waves.
+                const unsigned long long bl = __ballot(live2);
+                if ((tid & 63) == 0) s_max[wave] = (uint32_t)__popcll(bl);
+                __syncthreads();  // also: every phase-2 lane has read s_groot
+                uint32_t before = 0, n_live = 0;
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    before += w < wave ? s_max[w] : 0u;
+                    n_live += s_max[w];
+                }
+                uint8_t* s_list = reinterpret_cast<uint8_t*>(s_groot);
+                if (live2) s_list[before + __popcll(bl & ((1ull << (tid & 63)) - 1ull))] = (uint8_t)p2;
+                __syncthreads();
+                for (uint32_t e = (uint32_t)(tid >> 2); e < n_live; e += kTilePixels / 4) {
+                    const int p = s_list[e], q = tid & 3;
+                    const float qx = (float)(x0 + (p & 15)), qy = (float)(y0 + (p >> 4));
+                    const float t = s_pub_T[p];
+                    const Refine r = halley(s_mask + p, s_pub_last[p], qx, qy, 0x11111111u << q, true, true, t,
+                                            s_pub_m0[p], s_pub_hi[p], false, 0.f, 0.f, true, kRefineWalks - 1,
+                                            fmaxf(t, 1.f));
+                    if (q == 0) publish(p, qx, qy, r);
                 }
                 __syncthreads();
                 const uint32_t flags = s_pub_last[tid];
