@@ -46,7 +46,7 @@ struct RenderBwdArgs {
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
-constexpr int kBwdBatch = 256;    // splat records staged per LDS batch
+constexpr int kBwdBatch = 128;    // splat records staged per LDS batch (8.5 KB: 3 one-wave blocks per SIMD)
 
 __device__ __forceinline__ f2 sel2(bool ca, bool cb, f2 x, f2 y) { return f2{ca ? x.x : y.x, cb ? x.y : y.y}; }
 __device__ __forceinline__ f2 splat2(float v) { return f2{v, v}; }
@@ -136,11 +136,13 @@ __device__ __forceinline__ PixPair load_pair(const RenderBwdArgs& a, int px, int
 // The per-(wave, Gaussian) field sums and the one atomic instruction then
 // cover 128 NP pixels: NP = 2 (one wave per tile) halves the reductions and
 // atomics per pixel and amortises the record's shared work over 4 pixels per
-// lane, against a larger register file per wave.  Measured at C3: NP = 2 at
-// 2 waves per SIMD (180 VGPRs) 0.540 ms, at 3 (168 VGPRs) 0.568, with 2
-// spilled registers 0.619; NP = 1 0.569.
+// lane, against a larger register file per wave.  Measured at C3: NP = 2 with
+// 128-record batches (8.5 KB of LDS) at 3 waves per SIMD (154 VGPRs) 0.516 ms;
+// with 256-record batches (17 KB: at most 9 blocks per CU) 0.540 at 180 VGPRs,
+// 0.568 at 168, 0.619 with 2 spilled registers; 4 waves per SIMD spill 72;
+// NP = 1 0.565.
 template <bool GEOM, int NP>
-__global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(NP == 1 ? 4 : 2, NP == 1 ? 8 : 2)))
+__global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(NP == 1 ? 4 : 3, 8)))
     render_bwd_kernel(RenderBwdArgs a) {
     constexpr int kThreads = 128 / NP;
     __shared__ float4 s_w0[kBwdBatch], s_w1[kBwdBatch], s_w2[kBwdBatch], s_w3[kBwdBatch];

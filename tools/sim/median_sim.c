@@ -697,6 +697,18 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
             out[0] += 1;
             float ts[32], hs[32];
             const float dmin = fmaxf(m0 - RANGE, 0.f), dmax = fmaxf(m0 + RANGE, 0.f);
+            if (getenv("SIM_P1")) {  /* variant: Halley from m0 in the window, no probe walk */
+                float res = mr;
+                int wk = halley_from(buf, n, fminf(fmaxf(m0, dmin), dmax), dmin, dmax, tol_rel, maxit, hnoise, &res);
+                if (wk < 0) { out[2] += 1; res = mr; wk = 100; }
+                out[25 + (wk < 6 ? wk : 6)] += 1;
+                root[l] = res;
+                have[l] = 1;
+                const double d = fabs((double)res - mr);
+                if (d > out[1]) out[1] = d;
+                if (wk > wmax1) wmax1 = wk;
+                continue;
+            }
             int m = 0;
             ts[m++] = dmin;
             for (int k = 0; k < nk; k++) ts[m++] = fminf(fmaxf(m0 + off[k], dmin), dmax);

@@ -6,7 +6,9 @@ maxit = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 sys.argv = ["median_sim.py", "41", "2"]
 g = runpy.run_path(__file__.replace("s4_sim.py", "median_sim.py"))
 sim, tiles, f, u32 = g["sim"], g["tiles"], g["f"], g["u32"]
-o = np.array([-0.2, -0.1, -0.05, -0.025, 0, 0.025, 0.05, 0.1, 0.2], np.float32)
+import os
+o = np.array([float(x) for x in os.environ.get("SIM_OFFS", "-0.2,-0.1,-0.05,-0.025,0,0.025,0.05,0.1,0.2").split(",")],
+             np.float32)
 out = np.zeros(32)
 sim.sim_s4(g["W"], g["H"], g["gx"], len(tiles), u32(tiles), u32(g["rg"]), u32(g["pl"]), f(g["xy"]), f(g["co"]),
            f(g["rp"]), len(o), f(o), ctypes.c_float(tol), maxit, ctypes.c_float(7e-6),
@@ -14,3 +16,4 @@ sim.sim_s4(g["W"], g["H"], g["gx"], len(tiles), u32(tiles), u32(g["rg"]), u32(g[
 print(f"tol {tol}: lanes {out[0]:.0f} max|d| {out[1]:.3e} fallbacks {out[2]:.0f} no-guess {out[24]:.0f}")
 print(f"phase-1 wave max walks {out[3]/out[4]:.2f}  phase-2 wave max walks {out[5]/out[6]:.2f} (fallback=100)")
 print("phase-2 lane walks hist", out[8:24].astype(int).tolist())
+print("phase-1 lane walks hist (SIM_P1)", out[25:32].astype(int).tolist())
