@@ -59,13 +59,16 @@ size_t scan_temp_bytes(int P) {
 // rocPRIM picks a merge sort below 1M items for 32-bit keys (10 merge passes
 // at P = 1M); a merge-sort limit of 0 keeps the 4-pass onesweep radix sort.
 #ifndef GSR_DSORT_BITS
-#define GSR_DSORT_BITS 8  // 0: rocPRIM's tuned onesweep config; measured at C3: 8 / 512 x 16 0.127 ms vs tuned 0.147 (x 12 adopted below) (11 bits: 0.145-0.173, 7: 0.177)
+#define GSR_DSORT_BITS 8  // 0: rocPRIM's tuned onesweep config; measured at C3: 8 / 512 x 16 0.127 ms vs tuned 0.147 (11 bits: 0.145-0.173, 7: 0.177)
 #endif
+// Keys per onesweep block, measured at C3 (depth_order): 1024 x 4 0.104 ms, 512 x 8 0.112, 1024 x 3 0.117,
+// 1024 x 8 0.117, 512 x 12 0.120, 512 x 16 0.126, 1024 x 2 0.129, 256 x 12 0.134, 1024 x 6 0.137, 512 x 20 0.142,
+// 256 x 8 0.145, 256 x 16 0.148, 512 x 6 0.153.
 #ifndef GSR_DSORT_BLOCK
-#define GSR_DSORT_BLOCK 512
+#define GSR_DSORT_BLOCK 1024
 #endif
 #ifndef GSR_DSORT_ITEMS
-#define GSR_DSORT_ITEMS 12  // 512 x 12: 0.122 ms; x 16: 0.126; x 20: 0.142
+#define GSR_DSORT_ITEMS 4
 #endif
 #if GSR_DSORT_BITS
 using DepthOnesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>,
