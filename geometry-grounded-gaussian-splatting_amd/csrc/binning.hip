@@ -33,6 +33,7 @@
 // (count, then emission) and must agree bit for bit.
 #pragma clang fp contract(off)
 
+#include <algorithm>
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -84,7 +85,7 @@ size_t depth_sort_temp_bytes(int P) {
     size_t bytes = 0;
     (void)rocprim::radix_sort_pairs<DepthSortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                     rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)P, 0u, 32u);
-    return bytes;
+    return std::max(bytes, dsort_temp_bytes(P));  // dsort.hip (default) or rocPRIM (GSR_OPT_ROCPRIM_DSORT)
 }
 
 size_t sort_temp_bytes(int K, int tile_bits) {
@@ -133,6 +134,7 @@ __global__ void __launch_bounds__(256)
 
 hipError_t launch_depth_sort(const GeomState& gs, int P, hipStream_t stream) {
     if (P == 0) return hipSuccess;
+    if (!option(kOptRocprimDsort)) return launch_dsort(gs, P, stream);
     size_t bytes = gs.dsort_tmp_bytes;
     return rocprim::radix_sort_pairs<DepthSortConfig>(gs.dsort_tmp, bytes, reinterpret_cast<const uint32_t*>(gs.depths),
                                                       gs.depth_keys_sorted, rocprim::counting_iterator<uint32_t>(0),

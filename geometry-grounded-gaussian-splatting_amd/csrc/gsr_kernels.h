@@ -8,7 +8,7 @@ namespace gsr {
 
 // Run-time switches for A/B variants of one kernel in one process
 // (gsr_set_option in include/gsr.h); defaults are the shipped paths.
-enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptSortbin = 7, kOptBwdNarrow = 8, kNumOptions = 9 };
+enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptSortbin = 7, kOptBwdNarrow = 8, kOptRocprimDsort = 9, kNumOptions = 10 };
 int option(int which);
 hipError_t read_render_stats(unsigned long long* out, bool reset);
 
@@ -68,6 +68,9 @@ size_t scan_temp_bytes(int P);
 size_t depth_sort_temp_bytes(int P);
 size_t sort_temp_bytes(int K, int tile_bits);
 hipError_t launch_depth_sort(const GeomState& gs, int P, hipStream_t stream);
+// dsort.hip
+size_t dsort_temp_bytes(int P);
+hipError_t launch_dsort(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_live_counts(const FwdParams& p, const GeomState& gs, const int* radii, hipStream_t stream);
 hipError_t launch_scan(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_emit_keys(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,

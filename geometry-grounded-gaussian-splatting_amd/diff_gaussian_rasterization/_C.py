@@ -117,6 +117,7 @@ OPT_NO_REFINE = 5
 OPT_BWD_NO_CACHE = 6
 OPT_SORTBIN = 7
 OPT_BWD_NARROW = 8
+OPT_ROCPRIM_DSORT = 9
 
 
 def debug_render_stats(reset: bool = True) -> list:

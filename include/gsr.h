@@ -341,6 +341,8 @@ const char* gsr_stage_name(int stage);
 /* GSR_OPT_BWD_NARROW (A/B, default 0): the backward raster with two wave64 per
  * tile and two pixels per lane instead of one wave64 and four pixels per lane
  * (render_bwd.hip). */
+/* GSR_OPT_ROCPRIM_DSORT (A/B, default 0): the depth order by rocPRIM's onesweep
+ * radix sort instead of dsort.hip's (same order). */
 /* GSR_OPT_NO_REFINE (A/B, default 0): find the median depth with the reference's
  * five bisection passes only, instead of two passes plus the bracketed Halley
  * refinement (render_fwd.hip; results agree to ~1e-7 of the depth, not bitwise). */
@@ -353,7 +355,8 @@ enum gsr_option {
     GSR_OPT_NO_REFINE = 5,
     GSR_OPT_BWD_NO_CACHE = 6,
     GSR_OPT_SORTBIN = 7,
-    GSR_OPT_BWD_NARROW = 8
+    GSR_OPT_BWD_NARROW = 8,
+    GSR_OPT_ROCPRIM_DSORT = 9
 };
 int gsr_set_option(int opt, int value);
 /* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (8 values, see render_fwd.hip). */

@@ -198,6 +198,17 @@ def test_parity_depth_ties(binning):
     _run(_with_depth_ties(Hh.small_case(P=600, W=64, H=48, seed=21), 250))
 
 
+@pytest.mark.parametrize("P", [1, 7, 4095, 4097, 9000])
+def test_parity_depth_sort_tiles(P):
+    """dsort.hip's 4096-key tiles: sizes below, at and across tile
+    boundaries (the last tile's padding keys), with depth ties, against the
+    oracle's stable order."""
+    c = Hh.small_case(P=P, W=64, H=48, seed=30 + P % 7)
+    if P >= 8:
+        c = _with_depth_ties(c, P // 4)
+    _run(c, check_bwd=False)
+
+
 def test_parity_binning_paths(binning):
     _run(Hh.small_case(P=10000, W=256, H=256, seed=7, log_scale=math.log(0.03)))
     _run(Hh.small_case(P=500, W=100, H=70, seed=2, kernel_size=0.1))
@@ -509,6 +520,26 @@ def test_c3_backward_linearity(c3):
         want = (x + 2 * y).double()
         err = float((z.double() - want).norm() / want.norm().clamp_min(1e-30))
         assert err <= 1e-4, (name, err)
+
+
+def test_c3_depth_sort_paths(c3):
+    """At full C3 (1M depth keys, 245 tiles of the onesweep look-back):
+    dsort.hip and rocPRIM's onesweep sort (GSR_OPT_ROCPRIM_DSORT) give the
+    same per-tile lists, entry for entry."""
+    from diff_gaussian_rasterization import _C
+
+    ga = [_gpu(x) for x in Hh.oracle_args(c3)] + [False]
+    lists = []
+    for opt in (0, 1):
+        _C.set_option(_C.OPT_ROCPRIM_DSORT, opt)
+        try:
+            out = _C.rasterize_gaussians(*ga)
+        finally:
+            _C.set_option(_C.OPT_ROCPRIM_DSORT, 0)
+        lists.append(_C.debug_binning(out[7], out[9], out[0], 1080, 1920))
+    assert np.array_equal(lists[0][1], lists[1][1])
+    n = int(lists[0][1][:, 1].max())
+    assert np.array_equal(lists[0][0][:n], lists[1][0][:n])
 
 
 def test_c3_cached_median_gradient(c3):

@@ -1,0 +1,19 @@
+"""Print one step's kernel timeline from a rocprofv3 kernel trace (development tool).
+python tools/ktrace_step.py TRACE_CSV [anchor_kernel_substring]"""
+import csv, re, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+anchor = sys.argv[2] if len(sys.argv) > 2 else "preprocess_fwd"
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
+i0, i1 = idx[-3], idx[-2]
+t0 = int(rows[i0]["Start_Timestamp"])
+prev = t0
+for r in rows[i0:i1]:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    name = r["Kernel_Name"]
+    short = name.split("(")[0][-60:]
+    if "rocprim" in name:
+        m = re.search(r"(onesweep_iteration|histogram|scan|reduce|lookback|init)", name)
+        short = "rocprim " + (m.group(1) if m else "?")
+    print(f"{(s - t0) / 1000:8.1f} us  gap {(s - prev) / 1000:6.1f}  dur {(e - s) / 1000:7.1f}  {short}")
+    prev = e
