@@ -132,9 +132,9 @@ __global__ void __launch_bounds__(256)
     counts[q] = make_uint2(tiles_touched[idx], tiles_live[idx]);
 }
 
-hipError_t launch_depth_sort(const GeomState& gs, int P, hipStream_t stream) {
+hipError_t launch_depth_sort(const GeomState& gs, int P, bool prepared, hipStream_t stream) {
     if (P == 0) return hipSuccess;
-    if (!option(kOptRocprimDsort)) return launch_dsort(gs, P, stream);
+    if (!option(kOptRocprimDsort)) return launch_dsort(gs, P, prepared, stream);
     size_t bytes = gs.dsort_tmp_bytes;
     return rocprim::radix_sort_pairs<DepthSortConfig>(gs.dsort_tmp, bytes, reinterpret_cast<const uint32_t*>(gs.depths),
                                                       gs.depth_keys_sorted, rocprim::counting_iterator<uint32_t>(0),

@@ -20,8 +20,9 @@
 //  2. per digit (lanes 0-255): the wave counts combined into the tile's
 //     digit counts, published at once with flag AGG, and the in-tile prefix;
 //  3. keys and values go to LDS in tile-sorted order;
-//  4. the decoupled look-back over the preceding tiles (32 status words per
-//     round, consumed newest first up to the first INC or not-ready word)
+//  4. the decoupled look-back over the preceding tiles (4 lanes per digit,
+//     32 status words each per round: 128 tiles per round, consumed newest
+//     first up to the first INC or not-ready word)
 //     gives the tile's exclusive prefix, published with flag INC, and the
 //     keys are written out striped: consecutive lanes write consecutive
 //     output positions of a digit run.
@@ -62,6 +63,13 @@ static DsortState carve_dsort(void* base, int P) {
     return s;
 }
 
+// the words the preprocess zeroes before the histogram (hist, counters, status)
+void dsort_zero_region(void* base, int P, uint32_t** first, size_t* words) {
+    DsortState s = carve_dsort(base, P);
+    *first = s.hist;
+    *words = (size_t)(s.status + (size_t)4 * s.tiles * 256 - s.hist);
+}
+
 size_t dsort_temp_bytes(int P) {
     DsortState s = carve_dsort(nullptr, P);
     return reinterpret_cast<size_t>(s.status + (size_t)4 * s.tiles * 256) + 256;
@@ -98,6 +106,51 @@ __global__ void __launch_bounds__(256) dsort_hist_kernel(const uint32_t* __restr
     }
 }
 
+// K (the sum of tiles touched, into a word the preprocess zeroed) and, with
+// `hist`, the four digit histograms of the depth keys: one read of both
+// arrays, replacing a 2-kernel reduce plus this file's zero and histogram
+// kernels on the render path.
+__global__ void __launch_bounds__(256) count_k_hist_kernel(int P, const uint32_t* __restrict__ tiles_touched,
+                                                           const uint32_t* __restrict__ keys, uint32_t* K,
+                                                           int hist, DsortState s) {
+    __shared__ uint32_t h[4][256];
+    __shared__ uint32_t s_sum[4];
+    if (hist)
+        for (int i = threadIdx.x; i < 4 * 256; i += 256) (&h[0][0])[i] = 0u;
+    __syncthreads();
+    const int per = (P + gridDim.x - 1) / gridDim.x;
+    const int i0 = blockIdx.x * per, i1 = min(P, i0 + per);
+    uint32_t sum = 0;
+    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
+        sum += tiles_touched[i];
+        if (hist) {
+            const uint32_t k = keys[i];
+            atomicAdd(&h[0][k & 255u], 1u);
+            atomicAdd(&h[1][(k >> 8) & 255u], 1u);
+            atomicAdd(&h[2][(k >> 16) & 255u], 1u);
+            atomicAdd(&h[3][k >> 24], 1u);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(K, s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3]);
+    if (hist)
+        for (int i = threadIdx.x; i < 4 * 256; i += 256) {
+            const uint32_t v = (&h[0][0])[i];
+            if (v) atomicAdd(&s.hist[i], v);
+        }
+}
+
+hipError_t launch_count_k_hist(const GeomState& gs, int P, bool hist, hipStream_t stream) {
+    if (P == 0) return hipMemsetAsync(gs.offsets_K, 0, sizeof(uint32_t), stream);
+    DsortState s = carve_dsort(gs.dsort_tmp, P);
+    hipLaunchKernelGGL(count_k_hist_kernel, dim3(min(256, (P + 4095) / 4096)), dim3(256), 0, stream, P,
+                       gs.tiles_touched, reinterpret_cast<const uint32_t*>(gs.depths), gs.offsets_K, hist ? 1 : 0, s);
+    return hipGetLastError();
+}
+
 __device__ __forceinline__ uint32_t ds_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -132,6 +185,7 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
     __shared__ uint32_t s_wcnt[kDsWaves][256];  // per-wave digit counters, then the waves' exclusive offsets
     __shared__ uint32_t s_goff[256];     // digit start in the output: global prefix + preceding tiles
     __shared__ uint32_t s_pre[256];      // in-tile exclusive digit prefix
+    __shared__ uint32_t s_cnt[256], s_excl[256];  // the tile's digit counts; the preceding tiles' sums
     __shared__ uint32_t s_keys[kDsTile], s_vals[kDsTile];
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_tile;
@@ -194,32 +248,60 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
         s_keys[rank] = k[i];
         s_vals[rank] = v[i];
     }
-    // 4. look-back over the preceding tiles for the digit's exclusive prefix
-    uint32_t excl = 0;
-    if (dl) {
+    // 4. look-back over the preceding tiles for the digit's exclusive prefix: 4 lanes per digit
+    //    (one quad of a wave), each reading kDsLook status words per round, so a round covers
+    //    4 kDsLook tiles; the quad's parts are consumed newest first up to the first INC or
+    //    not-ready word
+    if (dl) s_cnt[d] = cnt;
+    __syncthreads();
+    {
+        const int dq = tid >> 2, part = tid & 3, quad = lane & ~3;
+        const uint32_t* sq = s.status + ((size_t)PASS * s.tiles) * 256 + dq;
+        uint32_t excl = 0;
         int j = tile - 1;
         while (j >= 0) {
+            const int j0 = j - part * kDsLook;
             uint32_t w[kDsLook];
 #pragma unroll
-            for (int q = 0; q < kDsLook; q++) w[q] = j - q >= 0 ? ds_load(st + (size_t)(j - q) * 256) : kDsInc;
-            int used = 0;
-            bool found = false;
+            for (int q = 0; q < kDsLook; q++) w[q] = j0 - q >= 0 ? ds_load(sq + (size_t)(j0 - q) * 256) : kDsInc;
+            uint32_t sum = 0;
+            int used = 0, kind = 0;  // kind: 0 every word an aggregate, 1 INC reached, 2 a word not ready
 #pragma unroll
             for (int q = 0; q < kDsLook; q++) {
-                if (found || used < q) continue;  // stop at the first INC or not-ready word
-                if ((w[q] & ~kDsVal) == 0u) continue;
-                excl += w[q] & kDsVal;
+                if (kind != 0) continue;
+                if ((w[q] & ~kDsVal) == 0u) {
+                    kind = 2;
+                    continue;
+                }
+                sum += w[q] & kDsVal;
                 used = q + 1;
-                found = (w[q] & ~kDsVal) == kDsInc;
+                if ((w[q] & ~kDsVal) == kDsInc) kind = 1;
             }
-            if (found) break;
-            j -= used;  // (0 when the newest word is not ready yet: read it again)
+            int consumed = 0, fin = 0, stop = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t sp = __shfl(sum, quad + q, 64);
+                const int up = __shfl(used, quad + q, 64), kp = __shfl(kind, quad + q, 64);
+                if (stop) continue;
+                excl += sp;
+                consumed += up;
+                if (kp != 0) {
+                    stop = 1;
+                    fin = kp == 1;
+                }
+            }
+            if (fin) break;
+            j -= consumed;  // (0 when the newest word is not ready yet: read it again)
         }
-        if (tile > 0) ds_store(st + (size_t)tile * 256, kDsInc | (excl + cnt));
+        if (part == 0) {
+            if (tile > 0) ds_store(s.status + ((size_t)PASS * s.tiles + tile) * 256 + dq, kDsInc | (excl + s_cnt[dq]));
+            s_excl[dq] = excl;
+        }
     }
+    __syncthreads();
     // global digit start: exclusive scan of the whole-input histogram, plus the preceding tiles
     const uint32_t gpre = ds_digit_excl(dl ? s.hist[PASS * 256 + d] : 0u, s_w);
-    if (dl) s_goff[d] = gpre + excl;
+    if (dl) s_goff[d] = gpre + s_excl[d];
     __syncthreads();
     const int nvalid = min(kDsTile, P - tile * kDsTile);
 #pragma unroll
@@ -235,13 +317,15 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
     }
 }
 
-hipError_t launch_dsort(const GeomState& gs, int P, hipStream_t stream) {
+hipError_t launch_dsort(const GeomState& gs, int P, bool prepared, hipStream_t stream) {
     if (P == 0) return hipSuccess;
     DsortState s = carve_dsort(gs.dsort_tmp, P);
     const uint32_t* keys = reinterpret_cast<const uint32_t*>(gs.depths);
-    const int zblocks = min(1024, (4 * s.tiles * 256 + 255) / 256);
-    hipLaunchKernelGGL(dsort_zero_kernel, dim3(zblocks), dim3(256), 0, stream, s);
-    hipLaunchKernelGGL(dsort_hist_kernel, dim3(min(256, (P + 4095) / 4096)), dim3(256), 0, stream, keys, P, s);
+    if (!prepared) {  // (render / sample paths: zeroed by the preprocess, histograms by count_k_hist_kernel)
+        const int zblocks = min(1024, (4 * s.tiles * 256 + 255) / 256);
+        hipLaunchKernelGGL(dsort_zero_kernel, dim3(zblocks), dim3(256), 0, stream, s);
+        hipLaunchKernelGGL(dsort_hist_kernel, dim3(min(256, (P + 4095) / 4096)), dim3(256), 0, stream, keys, P, s);
+    }
     const dim3 grid(s.tiles), block(kDsThreads);
     hipLaunchKernelGGL(dsort_pass_kernel<0>, grid, block, 0, stream, keys, nullptr, P, s, s.keys_alt, s.vals_alt);
     hipLaunchKernelGGL(dsort_pass_kernel<1>, grid, block, 0, stream, s.keys_alt, s.vals_alt, P, s,

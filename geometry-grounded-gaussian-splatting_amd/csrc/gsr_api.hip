@@ -515,7 +515,7 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
         // K depends on preprocess only: one readback
         HostReadback* rb = nullptr;
         GSR_TRY(readback_slot(rb), "pinned readback buffer");
-        GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
+        GSR_STAGE(GSR_STAGE_SCAN, launch_count_k_hist(gs, P, path == kBinLists, stream), "count K");
         GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
         if (prefiltered)
             GSR_TRY(hipMemcpyAsync(rb->pinned + 1, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
@@ -524,12 +524,12 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
         // the GPU counts the tile lists (or sorts by depth) while the host waits
         if (path == kBinSortbin)
             GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_count(p, gs, radii, ts, stream), "tile counts");
-        if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, true, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
         Ks.x = rb->pinned[0];
         if (prefiltered) near_flag = rb->pinned[1];
     } else {
-        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, false, stream), "depth order");
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_live_counts(p, gs, radii, stream), "live counts");
         GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
         GSR_TRY(hipMemcpyAsync(&Ks, gs.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, stream), "memcpy K");
@@ -714,7 +714,7 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
         // the points only: one readback (HostReadback)
         HostReadback* rb = nullptr;
         GSR_TRY(readback_slot(rb), "pinned readback buffer");
-        GSR_STAGE(GSR_STAGE_SCAN, launch_count_K(gs, P, stream), "count K");
+        GSR_STAGE(GSR_STAGE_SCAN, launch_count_k_hist(gs, P, path == kBinLists, stream), "count K");
         GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_points(p, PN, points3D, ps, pb, st, stream), "sample points");
         GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_setup(PN, tiles, pb, st, stream), "sample setup");
         GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
@@ -727,13 +727,13 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
         // the GPU counts the tile lists (or sorts by depth) while the host waits
         if (path == kBinSortbin)
             GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_count(p, gs, gs.radii, ts, stream), "tile counts");
-        if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, true, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
         Ks.x = rb->pinned[0];
         if (prefiltered) near_flag = rb->pinned[1];
         for (int k = 0; k < 4; k++) totals[k] = rb->pinned[4 + k];
     } else {
-        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, stream), "depth order");
+        GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, false, stream), "depth order");
         GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_live_counts(p, gs, gs.radii, stream), "live counts");
         GSR_STAGE(GSR_STAGE_SCAN, launch_scan(gs, P, stream), "scan");
         GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_points(p, PN, points3D, ps, pb, st, stream), "sample points");

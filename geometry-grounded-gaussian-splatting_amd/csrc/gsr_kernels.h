@@ -67,10 +67,14 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
 size_t scan_temp_bytes(int P);
 size_t depth_sort_temp_bytes(int P);
 size_t sort_temp_bytes(int K, int tile_bits);
-hipError_t launch_depth_sort(const GeomState& gs, int P, hipStream_t stream);
+hipError_t launch_depth_sort(const GeomState& gs, int P, bool prepared, hipStream_t stream);
 // dsort.hip
 size_t dsort_temp_bytes(int P);
-hipError_t launch_dsort(const GeomState& gs, int P, hipStream_t stream);
+void dsort_zero_region(void* base, int P, uint32_t** first, size_t* words);
+// K into gs.offsets_K and, with `hist`, the depth-key digit histograms (both zeroed by the preprocess)
+hipError_t launch_count_k_hist(const GeomState& gs, int P, bool hist, hipStream_t stream);
+// `prepared`: state zeroed and histograms counted by the two kernels above
+hipError_t launch_dsort(const GeomState& gs, int P, bool prepared, hipStream_t stream);
 hipError_t launch_live_counts(const FwdParams& p, const GeomState& gs, const int* radii, hipStream_t stream);
 hipError_t launch_scan(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_emit_keys(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
@@ -82,7 +86,6 @@ hipError_t launch_tile_ranges(const BinningState& bs, int K, const TileState& ts
 bool list_binning(uint32_t gx, uint32_t gy);
 ListLayout list_layout(int P, int K, uint32_t gx, uint32_t gy);
 size_t reduce_temp_bytes(int P);
-hipError_t launch_count_K(const GeomState& gs, int P, hipStream_t stream);
 hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
                                const TileState& ts, int K, hipStream_t stream);
 

@@ -45,6 +45,9 @@ struct PreprocessArgs {
     Splat* splats;
     uint32_t* tiles_touched;
     bool no_color;
+    uint32_t* zero_first;  // words zeroed for the next kernels (dsort state; dsort_zero_region)
+    size_t zero_words;
+    uint32_t* zero_K;      // K accumulator of count_k_hist_kernel
 };
 
 // ndc2Pix in double, as the reference (auxiliary.h:38-40)
@@ -52,6 +55,8 @@ __device__ inline float ndc2pix(float v, int S) { return (float)((((double)v + 1
 
 __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    for (size_t i = (size_t)idx; i < a.zero_words; i += (size_t)gridDim.x * blockDim.x) a.zero_first[i] = 0u;
+    if (idx == 0) *a.zero_K = 0u;
     if (idx >= a.P) return;
     a.radii[idx] = 0;
     a.tiles_touched[idx] = 0;
@@ -313,6 +318,8 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
     a.depths = gs.depths;
     a.splats = gs.splats;
     a.tiles_touched = gs.tiles_touched;
+    dsort_zero_region(gs.dsort_tmp, p.P, &a.zero_first, &a.zero_words);
+    a.zero_K = gs.offsets_K;
     hipLaunchKernelGGL(preprocess_fwd_kernel, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }

@@ -213,11 +213,6 @@ size_t reduce_temp_bytes(int P) {
     return c;
 }
 
-hipError_t launch_count_K(const GeomState& gs, int P, hipStream_t stream) {
-    size_t bytes = gs.scan_tmp_bytes;
-    return rocprim::reduce(gs.scan_tmp, bytes, gs.tiles_touched, gs.offsets_K, 0u, (size_t)P,
-                           rocprim::plus<uint32_t>(), stream);
-}
 
 // --------------------------------------------------------------- rows pass
 struct QGauss {  // one Gaussian in q order, as the row kernels need it
