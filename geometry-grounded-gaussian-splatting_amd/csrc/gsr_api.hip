@@ -586,10 +586,11 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
                       scale_modifier, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, kernel_size, require_depth);
     if (P == 0) return GSR_OK;
     if (const char* msg = check_params(b.f)) return fail(GSR_ERR_ARGS, msg);
-    if (!geom_buffer || !binning_buffer || !image_buffer || !tile_buffer || !radii || !alphas || !dL_dpix ||
-        !dL_dalphas || !dL_dmean3D || !dL_dmean2D || !dL_dcolor || !dL_dopacity)
+    // (a NULL upstream image gradient is zero: gsr.h)
+    if (!geom_buffer || !binning_buffer || !image_buffer || !tile_buffer || !radii || !alphas || !dL_dmean3D ||
+        !dL_dmean2D || !dL_dcolor || !dL_dopacity)
         return fail(GSR_ERR_ARGS, "missing backward buffer");
-    if (b.f.require_depth && (!normalmap || !mdepth || !dL_dpix_mdepth || !dL_dpixel_normals))
+    if (b.f.require_depth && (!normalmap || !mdepth))
         return fail(GSR_ERR_ARGS, "missing geometry buffers for require_depth");
     if (scales && (!dL_dscale || !dL_drot)) return fail(GSR_ERR_ARGS, "missing scale/rotation gradients");
     if (cov3D_precomp && !dL_dcov3D) return fail(GSR_ERR_ARGS, "missing cov3D gradient");

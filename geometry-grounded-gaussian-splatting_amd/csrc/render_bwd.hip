@@ -76,17 +76,18 @@ __device__ __forceinline__ PixIn load_pixel(const RenderBwdArgs& a, int px, int 
     r.T_final = 1.f - w_final;
     r.last = a.n_contrib[pix];
     if (r.last == 0) return r;  // blended nothing: no gradient terms (and 1/alpha would be inf)
-    r.dLp0 = a.dL_dpix[pix];
-    r.dLp1 = a.dL_dpix[HW + pix];
-    r.dLp2 = a.dL_dpix[2 * HW + pix];
-    r.dL_dfinalT = -a.dL_dalpha[pix] + a.bg[0] * r.dLp0 + a.bg[1] * r.dLp1 + a.bg[2] * r.dLp2;
+    // (a NULL upstream gradient is zero)
+    r.dLp0 = a.dL_dpix ? a.dL_dpix[pix] : 0.f;
+    r.dLp1 = a.dL_dpix ? a.dL_dpix[HW + pix] : 0.f;
+    r.dLp2 = a.dL_dpix ? a.dL_dpix[2 * HW + pix] : 0.f;
+    r.dL_dfinalT = -(a.dL_dalpha ? a.dL_dalpha[pix] : 0.f) + a.bg[0] * r.dLp0 + a.bg[1] * r.dLp1 + a.bg[2] * r.dLp2;
     if constexpr (GEOM) {
         const float inv_w = 1.f / w_final;
         const float nrm = pixel_ray_norm((float)px, (float)py, a.W, a.H, a.focal_x, a.focal_y);
-        r.dL_dmt = a.dL_dmdepth[pix] * (1.0f / nrm);
-        r.dLn0 = a.dL_dnormal[pix] * inv_w;
-        r.dLn1 = a.dL_dnormal[HW + pix] * inv_w;
-        r.dLn2 = a.dL_dnormal[2 * HW + pix] * inv_w;
+        r.dL_dmt = (a.dL_dmdepth ? a.dL_dmdepth[pix] : 0.f) * (1.0f / nrm);
+        r.dLn0 = (a.dL_dnormal ? a.dL_dnormal[pix] : 0.f) * inv_w;
+        r.dLn1 = (a.dL_dnormal ? a.dL_dnormal[HW + pix] : 0.f) * inv_w;
+        r.dLn2 = (a.dL_dnormal ? a.dL_dnormal[2 * HW + pix] : 0.f) * inv_w;
         r.dL_dfinalT += r.dLn0 * a.normalmap[pix] + r.dLn1 * a.normalmap[HW + pix] + r.dLn2 * a.normalmap[2 * HW + pix];
         const float md = a.mdepth[pix];
         r.mDepth = md * nrm;

@@ -286,7 +286,8 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
                                  geomBuffer, R, binningBuffer, imageBuffer, tileBuffer, require_depth, debug):
     L = _load()
     P = means3D.size(0)
-    H, W = dL_dout_color.size(1), dL_dout_color.size(2)
+    img = dL_dout_color if dL_dout_color is not None else alphas  # (a None upstream gradient is zero)
+    H, W = img.size(1), img.size(2)
     SHM = sh.size(1) if sh is not None and sh.size(0) != 0 else 0
     SGM = sg_color.size(1) if sg_color is not None and sg_color.size(0) != 0 else 0
     dev = means3D.device

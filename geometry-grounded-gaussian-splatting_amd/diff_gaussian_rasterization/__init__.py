@@ -56,6 +56,10 @@ class _RasterizeGaussians(torch.autograd.Function):
         num_rendered, color, alpha, normal, mdepth, radii, geomBuffer, binningBuffer, imgBuffer, tileBuffer = out
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
+        # unused outputs reach the backward as None (zero upstream gradient: the kernels skip them)
+        # instead of as materialised zero images; radii has no gradient
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis,
                               sg_sharpness, sg_color, alpha, normal, mdepth, radii, geomBuffer, binningBuffer,
                               imgBuffer, tileBuffer)

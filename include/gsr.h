@@ -77,6 +77,10 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
  * dL_dcolor [P,3], dL_dopacity [P,1], dL_dscale [P,3], dL_drot [P,4],
  * dL_dcov3D [P,6], dL_dsh [P,SHM,3], dL_dsg_axis [P,SGM,3],
  * dL_dsg_sharpness [P,SGM], dL_dsg_color [P,SGM,3].
+ * An upstream image gradient (dL_dpix, dL_dpix_mdepth, dL_dalphas,
+ * dL_dpixel_normals) may be NULL for an output the loss does not use: it is
+ * then zero (no reference equivalent; the autograd wrapper passes None
+ * instead of materialising zero images).
  */
 int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
                            int sg_degree, int SGM, int R, const float* background, int width, int height,

@@ -332,6 +332,34 @@ def test_mark_visible_matches_oracle():
     assert np.array_equal(got.cpu().numpy(), O.mark_visible(m, c["cam"].world_view_transform))
 
 
+def test_backward_none_upstream():
+    """A None upstream image gradient (the autograd wrapper's unused outputs,
+    no materialised zero images) gives the gradients of a zero one."""
+    from diff_gaussian_rasterization import _C
+
+    c = Hh.small_case(P=500, W=100, H=70, seed=2)
+    ga = [_gpu(x) for x in _fwd_args(c)] + [False]
+    out = _C.rasterize_gaussians(*ga)
+    K, color, alpha, normal, mdepth, radii = out[:6]
+    g = {k: _gpu(v) for k, v in S.upstream_grads(70, 100).items()}
+    g["alpha"] = torch.zeros_like(alpha)
+
+    def bwd(gc, gm, ga_, gn):
+        return _C.rasterize_gaussians_backward(*ga[:19], gc, gm, ga_, gn, alpha, normal, mdepth,
+                                               _gpu(c["cam"].camera_center), radii, out[6], K, out[7], out[8],
+                                               out[9], True, False)
+
+    z = {k: torch.zeros_like(v) for k, v in g.items()}
+    for none in ("alpha", "mdepth", "normal", "color"):
+        args = [None if none == k else (z[k] if k == "alpha" else g[k]) for k in ("color", "mdepth", "alpha", "normal")]
+        ref = [z[k] if none == k else (z[k] if k == "alpha" else g[k]) for k in ("color", "mdepth", "alpha", "normal")]
+        for name, x, y in zip(GRAD_NAMES, bwd(*args), bwd(*ref)):
+            if x.numel() == 0:
+                continue
+            err = float((x - y).abs().max()) / max(float(y.abs().max()), 1e-30)
+            assert err <= 1e-5, (none, name, err)
+
+
 def test_autograd_render_end_to_end():
     """gaussian_renderer.render() -> GaussianRasterizer -> autograd, with the
     GaussianModel getters in front: gradients reach the raw parameters and the
