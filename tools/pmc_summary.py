@@ -42,8 +42,10 @@ def stage_of(name: str) -> str | None:
         return "render_bwd"
     if "tile_order_kernel" in n or "bwd_prepare_kernel" in n:
         return "bwd_clear"
-    if "gather_counts_kernel" in n or "live_tiles_kernel" in n:
+    if "gather_counts_kernel" in n or "live_tiles_kernel" in n or "dsort_" in n:
         return "depth_order"
+    if "count_k_hist_kernel" in n:
+        return "scan"
     if "radix_sort" in n or "onesweep" in n or "merge_sort" in n:
         # rocPRIM kernels are named by key/value types: the tile sort has
         # 16-bit keys (grids <= 65536 tiles), the depth sort 32-bit keys
