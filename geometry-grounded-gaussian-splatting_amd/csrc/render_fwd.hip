@@ -37,9 +37,16 @@
 
 namespace gsr {
 
-constexpr int kResident = 352;  // (384 measured the same; 352 leaves LDS for the phase exchange)
+#ifndef GSR_RESIDENT
+#define GSR_RESIDENT 256
+#endif
+#ifndef GSR_BATCH
+#define GSR_BATCH 128
+#endif
+constexpr int kResident = GSR_RESIDENT;  // LDS-resident contributing prefix (C3: every tile's max contributor <= 184)
 constexpr int kMaskWords = kResident / 32;
-constexpr int kRecSlots = 3 * kResident > 4 * kTilePixels ? 3 * kResident : 4 * kTilePixels;
+constexpr int kBatch = GSR_BATCH;        // records per composite staging batch
+constexpr int kRecSlots = 3 * kResident > 4 * kBatch ? 3 * kResident : 4 * kBatch;
 
 struct RenderFwdArgs {
     const uint2* ranges;
@@ -225,16 +232,22 @@ __device__ unsigned long long g_render_stats[8];
 //    keeps only T / last / m0 / blended set, then the bisection runs.
 //  * !GEOM (integrate, evaluateTransmittanceCUDA, :55-169): the composite
 //    also carries the vacancy transmittance at the point's own distance.
-// 5 waves per SIMD: the LDS (31.5 KB per block) allows 5 blocks per CU; the
-// register budget that gives (96) costs a few spilled registers outside the
-// walks.
+// Occupancy (C3, GSR_* build variants through tools/ab_libs.sh): 24.3 KB of
+// LDS per block (a 256-record resident cache, 128-record composite batches)
+// fits 6 blocks per CU, and 6 waves per SIMD (80 VGPRs, spills outside the
+// walks): 0.812 ms; the same at 5 waves per SIMD (96 VGPRs) 0.823; a
+// 352-record cache with 256-record batches (31.8 KB: the LDS granule left 4
+// blocks per CU) 0.893; a 192-record cache 0.820; 64-record batches 0.825.
+// Tiles whose contributing prefix exceeds the cache take the wave-uniform
+// walk (C3's largest per-tile max contributor is 184).
+#ifndef GSR_FWD_WAVES
+#define GSR_FWD_WAVES 6
+#endif
 template <bool GEOM, bool SKIP, bool STATS = false, bool SAMPLE = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) render_fwd_kernel(RenderFwdArgs a) {
-    // LDS: composite staging (4 x 256 x 16 B = 16 KB) aliased with the
-    // bisection cache (3 x 384 x 16 B = 18 KB), plus the 12 KB of masks:
-    // 30 KB per block, 5 blocks (20 waves) per CU.  (A 320-record cache
-    // reaches 6 blocks per CU but sends C3's longest tiles to the
-    // wave-uniform walk: measured slower.)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, 8))) render_fwd_kernel(RenderFwdArgs a) {
+    // LDS: composite staging (4 x 128 x 16 B = 8 KB) aliased with the
+    // resident cache (3 x 256 x 16 B = 12 KB), the 8 KB of masks and the
+    // phase exchange: 24.3 KB per block, 6 blocks (24 waves) per CU.
     __shared__ float4 s_rec[kRecSlots];
     // blended contributors per pixel, word-major (word w of lane t at w * 256 + t: conflict-free)
     __shared__ uint32_t s_mask[GEOM ? kTilePixels * kMaskWords : 1];
@@ -284,12 +297,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
 
     const uint2 range = a.ranges[tile];
     const int total = (int)(range.y - range.x);
-    const int rounds = (total + kTilePixels - 1) / kTilePixels;
+    const int rounds = (total + kBatch - 1) / kBatch;
 
     float4* s_w0 = s_rec;
-    float4* s_w1 = s_rec + kTilePixels;
-    float4* s_w2 = s_rec + 2 * kTilePixels;
-    float4* s_w3 = s_rec + 3 * kTilePixels;
+    float4* s_w1 = s_rec + kBatch;
+    float4* s_w2 = s_rec + 2 * kBatch;
+    float4* s_w3 = s_rec + 3 * kBatch;
 
     // each lane owns one mask column: no barrier needed between init, writes and reads
     uint32_t* my_mask = s_mask + (GEOM ? tid : 0);
@@ -369,14 +382,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
         last = (uint32_t)g + 1u;  // the reference's 1-based contributor index
     };
     int toDo = total;
-    for (int i = 0; i < rounds; i++, toDo -= kTilePixels) {
+    for (int i = 0; i < rounds; i++, toDo -= kBatch) {
         // block-wide early exit: every wave publishes whether any lane is live
         const bool wave_alive = __ballot(!done) != 0ull;
         if ((tid & 63) == 0) s_alive[i & 1][wave] = wave_alive;
         __syncthreads();  // also: everyone finished reading the previous batch
         if (!(s_alive[i & 1][0] | s_alive[i & 1][1] | s_alive[i & 1][2] | s_alive[i & 1][3])) break;
-        const int k = i * kTilePixels + tid;
-        if (k < total) {
+        const int k = i * kBatch + tid;
+        if (tid < kBatch && k < total) {
             const Splat* sp = a.splats + a.point_list[range.x + k];
             s_w0[tid] = sp->w0;
             s_w1[tid] = sp->w1;
@@ -384,9 +397,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
             if constexpr (!SAMPLE) s_w3[tid] = sp->w3;
         }
         __syncthreads();
-        const int n = min(kTilePixels, toDo);
+        const int n = min(kBatch, toDo);
         for (int j = 0; !done && j < n; j++)
-            step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kTilePixels + j);
+            step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
     }
 
     if constexpr (GEOM) my_mask[mask_w * kTilePixels] = mask_cur;
