@@ -718,7 +718,15 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
             for (int k = 1; k < m - 1; k++) if (hs[k] >= 0.f) k1 = k;
             float w = hs[k1] / (hs[k1] - hs[k1 + 1]);
             w = (w != w) ? 0.5f : fminf(fmaxf(w, 0.f), 1.f);
-            const float t0 = ts[k1] + w * (ts[k1 + 1] - ts[k1]);
+            float t0 = ts[k1] + w * (ts[k1 + 1] - ts[k1]);
+            if (getenv("SIM_P1H")) {  /* variant: a Halley step from m0 (h, h', h'' taken in the probe walk) */
+                float h0, d1, d2;
+                const float tm = fminf(fmaxf(m0, dmin), dmax);
+                vac_d2(buf, n, tm, &h0, &d1, &d2);
+                const float den = 2.f * d1 * d1 - h0 * d2;
+                const float th = den != 0.f ? tm - 2.f * h0 * d1 / den : -1.f;
+                if (th >= ts[k1] && th <= ts[k1 + 1]) t0 = th;
+            }
             float res = mr;
             int wk = halley_from(buf, n, t0, ts[k1], ts[k1 + 1], tol_rel, maxit, hnoise, &res);
             if (wk < 0) { out[2] += 1; res = mr; wk = 100; }
