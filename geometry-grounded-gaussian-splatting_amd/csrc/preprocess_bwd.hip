@@ -131,7 +131,35 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
 #endif
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
-    const float* acc = a.acc + (size_t)idx * kAccFields;
+    // every per-Gaussian input row is requested up front, before the culled
+    // test and the dependent chains (one memory round trip instead of one per
+    // phase; the kernel is latency-bound)
+    float acc[kAccFields];
+    {
+        const float4* a4 = reinterpret_cast<const float4*>(a.acc + (size_t)idx * kAccFields);  // 64-B records
+#pragma unroll
+        for (int k = 0; k < kAccFields / 4; k++) {
+            const float4 v = a4[k];
+            acc[4 * k] = v.x;
+            acc[4 * k + 1] = v.y;
+            acc[4 * k + 2] = v.z;
+            acc[4 * k + 3] = v.w;
+        }
+    }
+    const int radius = a.radii[idx];
+    const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
+    const float opacity = a.opacities[idx];
+    float sc_in[3] = {0.f, 0.f, 0.f}, q_in[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.scales) {
+        sc_in[0] = a.scales[3 * idx];
+        sc_in[1] = a.scales[3 * idx + 1];
+        sc_in[2] = a.scales[3 * idx + 2];
+        const float4 q4 = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
+        q_in[0] = q4.x;
+        q_in[1] = q4.y;
+        q_in[2] = q4.z;
+        q_in[3] = q4.w;
+    }
     // extension outputs straight from the accumulator (zero for culled
     // Gaussians); sample_depth returns neither (rasterize_points.cu:633)
     if (a.dL_dmean2D) {
@@ -144,13 +172,12 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         a.dL_dcolor[3 * idx + 1] = acc[kAccColor + 1];
         a.dL_dcolor[3 * idx + 2] = acc[kAccColor + 2];
     }
-    if (!(a.radii[idx] > 0)) {
+    if (!(radius > 0)) {
         zero_outputs(a, idx);
         return;
     }
     const float fx = a.focal_x, fy = a.focal_y;
     const float* V = a.view;
-    const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
     const float dconx = acc[kAccConic + 0], dcony = acc[kAccConic + 1], dconz = acc[kAccConic + 2],
                 dconw = acc[kAccConic + 3];
     const float dnx = acc[kAccNormal + 0], dny = acc[kAccNormal + 1], dnz = acc[kAccNormal + 2];
@@ -181,10 +208,10 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     float evl[3] = {0.f, 0.f, 0.f}, EV[9];
     bool well_conditioned = true;
     if (a.scales) {
-        s[0] = a.scale_modifier * a.scales[3 * idx];
-        s[1] = a.scale_modifier * a.scales[3 * idx + 1];
-        s[2] = a.scale_modifier * a.scales[3 * idx + 2];
-        const float* q = a.rotations + 4 * idx;
+        s[0] = a.scale_modifier * sc_in[0];
+        s[1] = a.scale_modifier * sc_in[1];
+        s[2] = a.scale_modifier * sc_in[2];
+        const float* q = q_in;
         float A_unused[9];
         rot_view(V, q[0], q[1], q[2], q[3], A_unused, Rq);
         const float s2[3] = {s[0] * s[0], s[1] * s[1], s[2] * s[2]};
@@ -352,7 +379,6 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         }
     }
     // conic / coefficient backward (render_backward.cu:547-579)
-    const float opacity = a.opacities[idx];
     const float dL_dcoef = dconw * opacity;
     const float dL_dsqrtcoef = dL_dcoef * 0.5f / (coef + 1e-6f);
     const float dL_ddet0 = dL_dsqrtcoef / det_1;
@@ -414,7 +440,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         a.dL_dscale[3 * idx] = dsc[0];
         a.dL_dscale[3 * idx + 1] = dsc[1];
         a.dL_dscale[3 * idx + 2] = dsc[2];
-        const float* q = a.rotations + 4 * idx;
+        const float* q = q_in;
         const float r = q[0], x = q[1], y = q[2], z = q[3];
 #define D_(i, j) d[3 * (i) + (j)]
         a.dL_drot[4 * idx + 0] = 2 * z * (D_(0, 1) - D_(1, 0)) + 2 * y * (D_(2, 0) - D_(0, 2)) + 2 * x * (D_(1, 2) - D_(2, 1));
