@@ -81,16 +81,24 @@ __device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
 // contiguous accesses issued together, instead of 7 dependent iterations of
 // 3-float pieces.  Same arithmetic in the same order as the generic loop.
 constexpr int kSG7 = 7;
-__device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, float x, float y, float z, float dR0,
-                                        float dR1, float dR2, float& ddx, float& ddy, float& ddz) {
-    const size_t o0 = (size_t)idx * kSG7;
+struct SG7Rows {
     float ax[3 * kSG7], gc[3 * kSG7], sharp[kSG7];
+};
+__device__ __forceinline__ void sg7_load(const PreprocessBwdArgs& a, int idx, SG7Rows& r) {
+    const size_t o0 = (size_t)idx * kSG7;
 #pragma unroll
-    for (int k = 0; k < 3 * kSG7; k++) ax[k] = a.sg_axis[3 * o0 + k];
+    for (int k = 0; k < 3 * kSG7; k++) r.ax[k] = a.sg_axis[3 * o0 + k];
 #pragma unroll
-    for (int k = 0; k < 3 * kSG7; k++) gc[k] = a.sg_color[3 * o0 + k];
+    for (int k = 0; k < 3 * kSG7; k++) r.gc[k] = a.sg_color[3 * o0 + k];
 #pragma unroll
-    for (int k = 0; k < kSG7; k++) sharp[k] = a.sg_sharpness[o0 + k];
+    for (int k = 0; k < kSG7; k++) r.sharp[k] = a.sg_sharpness[o0 + k];
+}
+__device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, const SG7Rows& rows, float x, float y,
+                                        float z, float dR0, float dR1, float dR2, float& ddx, float& ddy, float& ddz) {
+    const size_t o0 = (size_t)idx * kSG7;
+    const float* ax = rows.ax;
+    const float* gc = rows.gc;
+    const float* sharp = rows.sharp;
     float dcol[3 * kSG7], dax[3 * kSG7], dsh[kSG7];
 #pragma unroll
     for (int sg = 0; sg < kSG7; sg++) {
@@ -160,6 +168,12 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         q_in[2] = q4.z;
         q_in[3] = q4.w;
     }
+#if GSR_SG_UNROLL
+    // (SG degree 7: the 196-B lobe rows as well; 2 waves per SIMD fit them)
+    const bool sg7 = a.shs && a.SGM == kSG7 && a.SGD == kSG7;
+    SG7Rows sgr;
+    if (sg7) sg7_load(a, idx, sgr);
+#endif
     // extension outputs straight from the accumulator (zero for culled
     // Gaussians); sample_depth returns neither (rasterize_points.cu:633)
     if (a.dL_dmean2D) {
@@ -549,8 +563,8 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         float ddy = gdy[0] * dR0 + gdy[1] * dR1 + gdy[2] * dR2;
         float ddz = gdz[0] * dR0 + gdz[1] * dR1 + gdz[2] * dR2;
 #if GSR_SG_UNROLL
-        if (a.SGM == kSG7 && a.SGD == kSG7) {
-            sg7_bwd(a, idx, x, y, z, dR0, dR1, dR2, ddx, ddy, ddz);
+        if (sg7) {
+            sg7_bwd(a, idx, sgr, x, y, z, dR0, dR1, dR2, ddx, ddy, ddz);
         } else
 #endif
         for (int sg = 0; sg < a.SGM; sg++) {
