@@ -53,6 +53,11 @@ struct PreprocessArgs {
 // ndc2Pix in double, as the reference (auxiliary.h:38-40)
 __device__ inline float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
 
+// HOIST (the SH 3 + SG 7 colour model, BASELINE C5): the colour rows (192-B
+// SH row, 196-B SG lobe rows) are requested at the top with the geometry
+// inputs, before the culling branches (one memory round trip instead of
+// three); the plain instance loads them where they are used.
+template <bool HOIST>
 __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     for (size_t i = (size_t)idx; i < a.zero_words; i += (size_t)gridDim.x * blockDim.x) a.zero_first[i] = 0u;
@@ -62,6 +67,27 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
     a.tiles_touched[idx] = 0;
 
     const float px = a.means3D[3 * idx], py = a.means3D[3 * idx + 1], pz = a.means3D[3 * idx + 2];
+    float sh[48], ax[21], sc[21], sh7[7];
+    float opacity = 0.f, sc_in[3] = {0.f, 0.f, 0.f}, q_in[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (HOIST) {
+        opacity = a.opacities[idx];
+        sc_in[0] = a.scales[3 * idx];
+        sc_in[1] = a.scales[3 * idx + 1];
+        sc_in[2] = a.scales[3 * idx + 2];
+        const float4 q4 = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
+        q_in[0] = q4.x;
+        q_in[1] = q4.y;
+        q_in[2] = q4.z;
+        q_in[3] = q4.w;
+        load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, sh_count(a.D), sh);
+        const size_t o0 = (size_t)idx * 7;
+#pragma unroll
+        for (int k = 0; k < 21; k++) ax[k] = a.sg_axis[3 * o0 + k];
+#pragma unroll
+        for (int k = 0; k < 21; k++) sc[k] = a.sg_color[3 * o0 + k];
+#pragma unroll
+        for (int k = 0; k < 7; k++) sh7[k] = a.sg_sharpness[o0 + k];
+    }
     const float* V = a.view;
     const ViewGeom g = view_geom(V, px, py, pz, a.tan_fovx, a.tan_fovy);
     if (g.t[2] <= kNearPlane) return;  // in_frustum (auxiliary.h:133-153)
@@ -94,11 +120,20 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
         Tc1[i] = V[4 * i + 1] * j11 + V[4 * i + 2] * j12;
     }
     if (a.scales) {
-        const float* q = a.rotations + 4 * idx;
-        rot_view(V, q[0], q[1], q[2], q[3], A, Rq);
-        s[0] = a.scale_modifier * a.scales[3 * idx];
-        s[1] = a.scale_modifier * a.scales[3 * idx + 1];
-        s[2] = a.scale_modifier * a.scales[3 * idx + 2];
+        if constexpr (!HOIST) {
+            const float* q = a.rotations + 4 * idx;
+            q_in[0] = q[0];
+            q_in[1] = q[1];
+            q_in[2] = q[2];
+            q_in[3] = q[3];
+            sc_in[0] = a.scales[3 * idx];
+            sc_in[1] = a.scales[3 * idx + 1];
+            sc_in[2] = a.scales[3 * idx + 2];
+        }
+        rot_view(V, q_in[0], q_in[1], q_in[2], q_in[3], A, Rq);
+        s[0] = a.scale_modifier * sc_in[0];
+        s[1] = a.scale_modifier * sc_in[1];
+        s[2] = a.scale_modifier * sc_in[2];
         // glm R column j = row j of R_q: R.c[j][i] = Rq[3*j + i]; (S R).c[j][i] = s_i * R.c[j][i]
         // M = (S R) T: M.c[j][i] = SR.c[0][i] T.c[j][0] + SR.c[1][i] T.c[j][1] + SR.c[2][i] T.c[j][2]
         float M0[3], M1[3];
@@ -213,8 +248,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
         float Y[16];
         sh_basis(a.D, dx, dy, dz, Y);
         const int n = sh_count(a.D);
-        float sh[48];
-        load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
+        if constexpr (!HOIST) load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
         col[0] = Y[0] * sh[0];
         col[1] = Y[0] * sh[1];
         col[2] = Y[0] * sh[2];
@@ -230,14 +264,15 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
             // SG degree 7 (C5): every lobe's axis / colour / sharpness rows
             // loaded at once as wide contiguous accesses (preprocess_bwd.hip
             // sg7_bwd); same arithmetic and order as the loop below
-            const size_t o0 = (size_t)idx * 7;
-            float ax[21], sc[21], sh7[7];
+            if constexpr (!HOIST) {
+                const size_t o0 = (size_t)idx * 7;
 #pragma unroll
-            for (int k = 0; k < 21; k++) ax[k] = a.sg_axis[3 * o0 + k];
+                for (int k = 0; k < 21; k++) ax[k] = a.sg_axis[3 * o0 + k];
 #pragma unroll
-            for (int k = 0; k < 21; k++) sc[k] = a.sg_color[3 * o0 + k];
+                for (int k = 0; k < 21; k++) sc[k] = a.sg_color[3 * o0 + k];
 #pragma unroll
-            for (int k = 0; k < 7; k++) sh7[k] = a.sg_sharpness[o0 + k];
+                for (int k = 0; k < 7; k++) sh7[k] = a.sg_sharpness[o0 + k];
+            }
 #pragma unroll
             for (int sg = 0; sg < 7; sg++) {
                 const float gs =
@@ -272,7 +307,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
 
     Splat sp;
     sp.w0 = make_float4(xpix, ypix, cc * det_inv, -cb * det_inv);
-    sp.w1 = make_float4(ca * det_inv, a.opacities[idx] * coef, plx * fnorm / fx, ply * fnorm / fy);
+    sp.w1 = make_float4(ca * det_inv, (HOIST ? opacity : a.opacities[idx]) * coef, plx * fnorm / fx, ply * fnorm / fy);
     sp.w2 = make_float4(g.tc, rsig, col[0], col[1]);
     sp.w3 = make_float4(col[2], cnx * inn, cny * inn, cnz * inn);
     a.splats[idx] = sp;
@@ -320,7 +355,12 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
     a.tiles_touched = gs.tiles_touched;
     dsort_zero_region(gs.dsort_tmp, p.P, &a.zero_first, &a.zero_words);
     a.zero_K = gs.offsets_K;
-    hipLaunchKernelGGL(preprocess_fwd_kernel, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
+    // (the hoisted instance needs every colour row: SH + 7 SG lobes, scales / rotations, no precomputed colours)
+    const bool hoist = p.SGM == 7 && p.SGD == 7 && p.shs && p.scales && !p.colors_precomp && !p.no_color;
+    if (hoist)
+        hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(preprocess_fwd_kernel<false>, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
