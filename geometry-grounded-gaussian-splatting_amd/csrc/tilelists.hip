@@ -491,6 +491,96 @@ __global__ void __launch_bounds__(64)
     });
 }
 
+// tiles_emit with the writes coalesced: the direct emission above writes one
+// 4-B id per lane to ~64 different tiles per store instruction (one L2
+// request per lane).  Here a chunk's instances are first placed in LDS
+// ordered by (tile, rank) — a tile's base in the chunk is the exclusive
+// scan of the tiles' counts, popcount(cov[x]) — and then written out by
+// consecutive lanes to consecutive slots of the same tile's run.  Same
+// slots, same values; chunks with more than kEmitCap instances write
+// directly.
+#ifndef GSR_TILES_EMIT_SORTED
+#define GSR_TILES_EMIT_SORTED 1
+#endif
+constexpr int kEmitCap = 512;  // instances staged per 64-entry chunk (C3 averages ~3 tiles per row entry)
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+__global__ void __launch_bounds__(64)
+    tiles_emit_sorted_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
+                             const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
+                             const uint2* __restrict__ rows, const uint32_t* __restrict__ O,
+                             uint32_t* __restrict__ point_list) {
+    // LDS: [gx] masks, [gx] running slots, [gx] chunk offsets, [gx] write bases, kEmitCap ids and tiles
+    extern __shared__ unsigned long long s_dyn[];
+    unsigned long long* s_cov = s_dyn;
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + gx);
+    uint32_t* s_off = s_run + gx;
+    uint32_t* s_base = s_off + gx;
+    uint32_t* s_id = s_base + gx;
+    uint16_t* s_x = reinterpret_cast<uint16_t*>(s_id + kEmitCap);
+    const int lane = threadIdx.x;
+    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
+    const unsigned long long bit = 1ull << lane, below = bit - 1ull;
+    for_xcd_segments(segbase[gy], [&](uint32_t l) {
+        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
+        const size_t base = (size_t)gx * segbase[S.y];
+        __syncthreads();  // previous segment done with the LDS
+        for (uint32_t x = lane; x < gx; x += 64) {
+            s_run[x] = O[base + (size_t)x * S.nk + S.k];
+            s_cov[x] = 0ull;
+        }
+        __syncthreads();
+        for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64) {
+            const uint32_t e = c0 + lane;
+            const bool on = e < S.e1;
+            const uint2 ent = on ? rows[e] : make_uint2(0u, 1u);  // empty span when off
+            const uint32_t lo = ent.y & 0xffffu, hi = on ? (ent.y >> 16) : 0u;
+            for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&s_cov[x], bit);
+            __syncthreads();
+            // per tile: its count in the chunk, its base among the chunk's instances, its write base
+            uint32_t carry = 0;
+            for (uint32_t xb = 0; xb < gx; xb += 64) {
+                const uint32_t x = xb + lane;
+                const uint32_t cnt = x < gx ? (uint32_t)__popcll(s_cov[x]) : 0u;
+                const uint32_t incl = wave_incl_scan(cnt);
+                if (x < gx) {
+                    const uint32_t off = carry + incl - cnt;
+                    const uint32_t r = s_run[x];
+                    s_off[x] = off;
+                    s_base[x] = r - off;
+                    s_run[x] = r + cnt;
+                }
+                carry += __shfl(incl, 63, 64);
+            }
+            __syncthreads();
+            if (carry <= (uint32_t)kEmitCap) {
+                for (uint32_t x = lo; on && x <= hi; x++) {
+                    const uint32_t p = s_off[x] + (uint32_t)__popcll(s_cov[x] & below);
+                    s_id[p] = ent.x;
+                    s_x[p] = (uint16_t)x;
+                }
+                __syncthreads();
+                for (uint32_t p = lane; p < carry; p += 64) point_list[s_base[s_x[p]] + p] = s_id[p];
+            } else {
+                for (uint32_t x = lo; on && x <= hi; x++)
+                    point_list[s_base[x] + s_off[x] + (uint32_t)__popcll(s_cov[x] & below)] = ent.x;
+            }
+            __syncthreads();
+            for (uint32_t x = lane; x < gx; x += 64) s_cov[x] = 0ull;
+            __syncthreads();
+        }
+    });
+}
+
 __global__ void __launch_bounds__(256)
     list_ranges_kernel(uint32_t gx, uint32_t gy, const uint32_t* __restrict__ segbase, const uint32_t* __restrict__ O,
                        uint2* __restrict__ ranges) {
@@ -539,8 +629,12 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     if ((e = launch_scan_excl(bs.tiles_count, bs.tiles_off, (size_t)gx * L.nseg_tiles_max, 0u, bs.segbase + gy, gx,
                               sums, stream)) != hipSuccess)
         return e;
-    hipLaunchKernelGGL(tiles_emit_kernel, dim3(kTileBlocks), dim3(64), 24 * gx, stream, gx, gy, L.nseg_rows,
-                       bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
+    if (GSR_TILES_EMIT_SORTED)
+        hipLaunchKernelGGL(tiles_emit_sorted_kernel, dim3(kTileBlocks), dim3(64), 20 * gx + 6 * kEmitCap, stream, gx,
+                           gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
+    else
+        hipLaunchKernelGGL(tiles_emit_kernel, dim3(kTileBlocks), dim3(64), 24 * gx, stream, gx, gy, L.nseg_rows,
+                           bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(list_ranges_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, stream, gx, gy, bs.segbase,
                        bs.tiles_off, ts.ranges);
