@@ -346,6 +346,42 @@ __global__ void __launch_bounds__(64)
     }
 }
 
+// Coalesced emission helpers (tiles_emit_sorted_kernel below).  (The rows
+// pass with the same staging measured 0.234 -> 0.239 ms at C3, 1.018 -> 1.008
+// at C5: not adopted; its 8-B entries land in only ~5 rows per Gaussian.)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// per bucket b < n: its count in the chunk (popcount of its mask), its base
+// among the chunk's entries, its write base; advances the running slots.
+// Returns the chunk's entry total (wave-uniform).
+__device__ __forceinline__ uint32_t chunk_bases(uint32_t n, const unsigned long long* cov, uint32_t* run,
+                                                uint32_t* off, uint32_t* wbase) {
+    const int lane = threadIdx.x & 63;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+        const uint32_t b = b0 + lane;
+        const uint32_t cnt = b < n ? (uint32_t)__popcll(cov[b]) : 0u;
+        const uint32_t incl = wave_incl_scan(cnt);
+        if (b < n) {
+            const uint32_t o = carry + incl - cnt;
+            const uint32_t r = run[b];
+            off[b] = o;
+            wbase[b] = r - o;
+            run[b] = r + cnt;
+        }
+        carry += __shfl(incl, 63, 64);
+    }
+    return carry;
+}
+
 // --------------------------------------------------------------- tiles pass
 // Row y's entries are [O_rows[y * nseg_rows], O_rows[(y + 1) * nseg_rows]);
 // it is cut into ceil(len / kTileSeg) segments; segbase[y] is the exclusive
@@ -504,16 +540,6 @@ __global__ void __launch_bounds__(64)
 #endif
 constexpr int kEmitCap = 512;  // instances staged per 64-entry chunk (C3 averages ~3 tiles per row entry)
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    return x;
-}
-
 __global__ void __launch_bounds__(64)
     tiles_emit_sorted_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
                              const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
@@ -547,20 +573,7 @@ __global__ void __launch_bounds__(64)
             for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&s_cov[x], bit);
             __syncthreads();
             // per tile: its count in the chunk, its base among the chunk's instances, its write base
-            uint32_t carry = 0;
-            for (uint32_t xb = 0; xb < gx; xb += 64) {
-                const uint32_t x = xb + lane;
-                const uint32_t cnt = x < gx ? (uint32_t)__popcll(s_cov[x]) : 0u;
-                const uint32_t incl = wave_incl_scan(cnt);
-                if (x < gx) {
-                    const uint32_t off = carry + incl - cnt;
-                    const uint32_t r = s_run[x];
-                    s_off[x] = off;
-                    s_base[x] = r - off;
-                    s_run[x] = r + cnt;
-                }
-                carry += __shfl(incl, 63, 64);
-            }
+            const uint32_t carry = chunk_bases(gx, s_cov, s_run, s_off, s_base);
             __syncthreads();
             if (carry <= (uint32_t)kEmitCap) {
                 for (uint32_t x = lo; on && x <= hi; x++) {
@@ -614,8 +627,7 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
                               stream)) != hipSuccess)
         return e;
     hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, gx, gy,
-                       p.cull_pad, gs.order,
-                       gs.splats, radii, bs.rows_off, bs.qrec, bs.rows);
+                       p.cull_pad, gs.order, gs.splats, radii, bs.rows_off, bs.qrec, bs.rows);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // tiles pass
     const uint32_t* last = bs.rows_count + (size_t)gy * L.nseg_rows - 1;
