@@ -12,9 +12,12 @@ losses, optimiser and the Python getters are outside the step.
 
 With N > 1 (launched by torch.distributed.run, one rank per GPU) every rank
 renders its own view (C4: cameras orbiting the scene) of the same Gaussians
-and the per-Gaussian gradients are summed with one RCCL all_reduce per step
-(the only exchange of view-parallel training).  `value` = views/s over all
-ranks, time = max over ranks.
+and the per-Gaussian gradients are summed over the ranks every step (the only
+exchange of view-parallel training): by default gsr_dist.FactoredViewGrads —
+the geometry rows all-reduced over RCCL, the SH / SG rows rebuilt on every
+rank from the all-gathered per-view DC rows and camera centres (2.6x fewer
+xGMI bytes at SH 3); `--exchange allreduce` all-reduces every row.  `value` =
+views/s over all ranks, time = max over ranks.
 
 Rank 0 prints one JSON line: the contract fields, a `roofline` object for the
 dominant kernel (algorithmic bytes per launch / its HIP-event-timed average
@@ -62,6 +65,8 @@ def parse():
     ap.add_argument("--sg-degree", type=int, default=None)
     ap.add_argument("--no-depth", action="store_true", help="require_depth=False (iterations < 7000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", choices=["factored", "allreduce"], default="factored",
+                    help="N > 1: gradient exchange (gsr_dist.FactoredViewGrads, or an all-reduce of every row)")
     ap.add_argument("--cpu-tile-stride", type=int, default=0, help="0 = auto")
     ap.add_argument("--stage-steps", type=int, default=5,
                     help="untimed steps with every stage bracketed by hipEvents (the per-stage table)")
@@ -170,7 +175,7 @@ def main():
     if world > 1:
         cam_cpu = S.orbit_cameras(8, W, H)[rank % 8]
         tag = "C4" if args.config == "C3" else "C5"
-        workload = f"{tag}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), one {W}x{H} view per GPU (orbit), fwd+bwd + RCCL grad all_reduce"
+        workload = f"{tag}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), one {W}x{H} view per GPU (orbit), fwd+bwd + RCCL gradient exchange ({args.exchange})"
     else:
         cam_cpu = S.make_camera(W, H)
         workload = f"{args.config}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), {W}x{H}, fwd+bwd"
@@ -191,10 +196,14 @@ def main():
         require_depth=geom, debug=False)
     rasterizer = GaussianRasterizer(settings)
     grad_keys = ["means3D", "shs", "sg_axis", "sg_sharpness", "sg_color", "opacities", "scales", "rotations"]
-    reducer = None
-    if world > 1:
+    reducer = exchanger = None
+    if world > 1 and args.exchange == "allreduce":
         from gsr_dist import ViewParallelGrads
         reducer = ViewParallelGrads([params[k] for k in grad_keys])
+    elif world > 1:  # colour rows rebuilt from the all-gathered DC rows (gsr_dist.FactoredViewGrads)
+        from gsr_dist import FactoredViewGrads
+        exchanger = FactoredViewGrads(params["means3D"], params["opacities"], params["scales"], params["rotations"],
+                                      params["shs"], params["sg_axis"], params["sg_sharpness"], params["sg_color"])
     state = {}
 
     def step():
@@ -211,6 +220,8 @@ def main():
         torch.autograd.backward(outs, gs)
         if reducer is not None:  # view-parallel gradient exchange
             reducer.all_reduce()
+        if exchanger is not None:
+            exchanger.exchange(cam.camera_center, args.sh_degree, args.sg_degree)
         state["radii"] = radii
 
     log(f"[bench] rank {rank}/{world} device {torch.cuda.get_device_name(dev)} P={P} {W}x{H} geom={geom}")

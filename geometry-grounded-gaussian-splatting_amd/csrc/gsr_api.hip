@@ -405,7 +405,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 9; }
+int gsr_abi_version(void) { return 10; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -940,6 +940,23 @@ int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_ra
         return fail(GSR_ERR_ARGS, "densify stats: invalid arguments");
     hipError_t e = launch_densify_stats(P, vgrad, radii, max_radii2D, accum, accum_abs, denom, (hipStream_t)stream_ptr);
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "densify stats", e);
+}
+
+int gsr_view_color_grads(int P, int sh_degree, int SHM, int sg_degree, int SGM, int n_views, const float* gathered,
+                         const float* means3D, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                         float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness, float* dL_dsg_color,
+                         void* stream_ptr) {
+    if (P < 0 || n_views < 1 || sh_degree < 0 || sh_degree > 3 || SHM < (sh_degree + 1) * (sh_degree + 1) ||
+        SGM < 0 || sg_degree < 0 || sg_degree > 7 || sg_degree > SGM)
+        return fail(GSR_ERR_ARGS, "view colour grads: invalid arguments");
+    if (P > 0 && (!gathered || !means3D || !dL_dsh ||
+                  (SGM > 0 && (!dL_dsg_axis || !dL_dsg_sharpness || !dL_dsg_color)) ||
+                  (sg_degree > 0 && (!sg_axis || !sg_sharpness || !sg_color))))
+        return fail(GSR_ERR_ARGS, "view colour grads: missing buffer");
+    hipError_t e = launch_view_color_grads(P, sh_degree, SHM, sg_degree, SGM, n_views, gathered, means3D, sg_axis,
+                                           sg_sharpness, sg_color, dL_dsh, dL_dsg_axis, dL_dsg_sharpness,
+                                           dL_dsg_color, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "view colour grads", e);
 }
 
 int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const int* uvs, const float* R,

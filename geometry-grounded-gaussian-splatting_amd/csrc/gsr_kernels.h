@@ -149,6 +149,11 @@ struct AdamGroup {
 };
 hipError_t launch_adam(int n_groups, const AdamGroup* groups, const double* lr, double step, double beta1,
                        double beta2, double eps, hipStream_t stream);
+// view_grads.hip: a view-parallel step's SH / SG gradients from the gathered DC rows
+hipError_t launch_view_color_grads(int P, int D, int SHM, int SGD, int SGM, int n_views, const float* gathered,
+                                   const float* means3D, const float* sg_axis, const float* sg_sharpness,
+                                   const float* sg_color, float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness,
+                                   float* dL_dsg_color, hipStream_t stream);
 hipError_t launch_densify_stats(int P, const float* vgrad, const int* radii, float* max_radii2D, float* accum,
                                 float* accum_abs, float* denom, hipStream_t stream);
 

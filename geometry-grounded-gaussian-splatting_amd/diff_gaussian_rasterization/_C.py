@@ -43,7 +43,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 def _load():
@@ -82,6 +82,8 @@ def _load():
                                 ctypes.c_double, vp]
     L.gsr_densify_stats.restype = i
     L.gsr_densify_stats.argtypes = [i] + [vp] * 7
+    L.gsr_view_color_grads.restype = i
+    L.gsr_view_color_grads.argtypes = [i] * 6 + [vp] * 10
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     L.gsr_set_option.argtypes = [i, i]
@@ -506,3 +508,31 @@ def densify_stats(viewspace_grad, radii, max_radii2D, accum, accum_abs, denom) -
     with torch.cuda.device(dev):
         _check(L.gsr_densify_stats(P, _ptr(viewspace_grad), _ptr(r), _ptr(max_radii2D), _ptr(accum), _ptr(accum_abs),
                                    _ptr(denom), _stream(dev)))
+
+
+def view_color_grads(gathered, n_views: int, means3D, sh_degree: int, dL_dsh, sg_degree: int = 0, sg_axis=None,
+                     sg_sharpness=None, sg_color=None, dL_dsg_axis=None, dL_dsg_sharpness=None,
+                     dL_dsg_color=None) -> None:
+    """gsr_view_color_grads (view_grads.hip): the SH / SG gradient rows of a
+    view-parallel step summed over `n_views` views, from the gathered
+    [n_views, P * 3 + 4] DC rows + camera centres; outputs written in place."""
+    L = _load()
+    P = means3D.shape[0]
+    SHM = dL_dsh.shape[1]
+    SGM = dL_dsg_color.shape[1] if dL_dsg_color is not None and dL_dsg_color.numel() else 0
+    need = [(gathered, "gathered"), (means3D, "means3D"), (dL_dsh, "dL_dsh")]
+    if SGM:
+        need += [(dL_dsg_axis, "dL_dsg_axis"), (dL_dsg_sharpness, "dL_dsg_sharpness"), (dL_dsg_color, "dL_dsg_color")]
+    if sg_degree:
+        need += [(sg_axis, "sg_axis"), (sg_sharpness, "sg_sharpness"), (sg_color, "sg_color")]
+    for t, name in need:
+        if t is None or not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError(f"gsr view_color_grads: `{name}` must be a contiguous fp32 HIP tensor")
+    if gathered.numel() != n_views * (3 * P + 4) or dL_dsh.shape[0] != P:
+        raise RuntimeError("gsr view_color_grads: shape mismatch")
+    dev = means3D.device
+    p = lambda t: _ptr(t) if t is not None and t.numel() else None  # noqa: E731
+    with torch.cuda.device(dev):
+        _check(L.gsr_view_color_grads(P, int(sh_degree), SHM, int(sg_degree), SGM, int(n_views), _ptr(gathered),
+                                      _ptr(means3D), p(sg_axis), p(sg_sharpness), p(sg_color), _ptr(dL_dsh),
+                                      p(dL_dsg_axis), p(dL_dsg_sharpness), p(dL_dsg_color), _stream(dev)))

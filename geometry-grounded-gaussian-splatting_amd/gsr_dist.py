@@ -131,6 +131,87 @@ class ViewParallelGrads:
         return [4 * sum(p.numel() for p in b) for b in self.buckets]
 
 
+class FactoredViewGrads:
+    """The view-parallel gradient exchange with the colour rows factored.
+
+    Per view, every SH / SG gradient row of a Gaussian is a function of three
+    numbers — the clamp-masked dL/dRGB, which is dL/dsh[:, 0, :] / SH_C0 — and
+    of the view direction (CR/render_backward.cu:56-191; view_grads.hip).  So
+    instead of all-reducing those rows (192 B per Gaussian at SH 3, 388 B with
+    SG 7), the ranks all-gather each view's DC row and camera centre (12 B per
+    Gaussian per view, one collective) and every rank rebuilds the summed rows
+    with one HIP kernel (gsr_view_color_grads, views summed in rank order, so
+    the replicas stay bit-identical).  Only the geometry gradients (means3D,
+    opacity, scales, rotations: 44 B per Gaussian) are all-reduced.  At 8
+    ranks and SH 3 the xGMI bytes per rank drop from 2 * 7/8 * 236 MB = 413 MB
+    (ring all-reduce of every row) to 2 * 7/8 * 44 + 7 * 12 = 161 MB per 1M
+    Gaussians.
+
+    `exchange(campos, sh_degree, sg_degree)` after the backward: `campos` is
+    this rank's camera centre (the rasterizer settings' `campos`), the degrees
+    are the active ones of that backward.  `expand` replaces the HIP kernel
+    (same signature as `_C.view_color_grads`; CPU tests only).
+
+    The SH rows may be the rasterizer's `shs` input or the reference's two
+    parameters `(features_dc, features_rest)` (gaussian_model.py:165-169: the
+    activation is a concatenation, so their .grad are the two slices of
+    dL/dshs).  SG tensors must be the rasterizer inputs (the SG activations
+    are not linear in the rows, so raw SG parameters go in `extra`, which is
+    all-reduced with the geometry rows).
+    """
+
+    def __init__(self, means3D: torch.Tensor, opacities: torch.Tensor, scales: torch.Tensor,
+                 rotations: torch.Tensor, shs, sg_axis: Optional[torch.Tensor] = None,
+                 sg_sharpness: Optional[torch.Tensor] = None, sg_color: Optional[torch.Tensor] = None,
+                 group: Optional[dist.ProcessGroup] = None, expand=None, extra: Iterable[torch.Tensor] = ()):
+        self.means3D = means3D
+        self.split = isinstance(shs, (tuple, list))
+        self.shs = tuple(shs) if self.split else shs
+        self.sg = [t if t is not None and t.numel() else None for t in (sg_axis, sg_sharpness, sg_color)]
+        self.group = group
+        self.geometry = ViewParallelGrads([means3D, opacities, scales, rotations, *extra], group=group)
+        if expand is None:
+            from diff_gaussian_rasterization import _C
+            expand = _C.view_color_grads
+        self.expand = expand
+        self._buf = None
+        self._gathered = None
+
+    def exchange(self, campos: torch.Tensor, sh_degree: int, sg_degree: int = 0) -> None:
+        world = dist.get_world_size(self.group)
+        P = self.means3D.shape[0]
+        for t in (self.shs if self.split else (self.shs,)):
+            if t.grad is None:
+                t.grad = torch.zeros_like(t)
+        dev = self.means3D.device
+        n = 3 * P + 4
+        if self._buf is None or self._buf.numel() != n or self._buf.device != dev:
+            self._buf = torch.zeros(n, dtype=torch.float32, device=dev)
+            self._gathered = torch.empty(world * n, dtype=torch.float32, device=dev)
+        dc = self.shs[0].grad if self.split else self.shs.grad
+        self._buf[:3 * P].view(P, 3).copy_(dc[:, 0, :])
+        self._buf[3 * P:3 * P + 3].copy_(campos.reshape(3))
+        work = dist.all_gather_into_tensor(self._gathered, self._buf, group=self.group, async_op=True)
+        self.geometry.all_reduce()
+        work.wait()
+        sgo = []
+        for t in self.sg:
+            if t is not None and t.grad is None:
+                t.grad = torch.zeros_like(t)
+            sgo.append(None if t is None else t.grad)
+        if self.split:
+            dc_t, rest_t = self.shs
+            rows = torch.empty(P, dc_t.shape[1] + rest_t.shape[1], 3, dtype=torch.float32, device=dev)
+        else:
+            rows = self.shs.grad
+        self.expand(self._gathered, world, self.means3D.detach(), sh_degree, rows, sg_degree,
+                    *[None if t is None else t.detach() for t in self.sg], *sgo)
+        if self.split:
+            k = dc_t.shape[1]
+            dc_t.grad.copy_(rows[:, :k])
+            rest_t.grad.copy_(rows[:, k:])
+
+
 def reduce_densification_stats(grad_norm_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
                                group: Optional[dist.ProcessGroup] = None) -> None:
     """Densification statistics of the views seen since the last densify step

@@ -233,6 +233,24 @@ int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_ra
                       float* accum_abs, float* denom, void* stream);
 
 /*
+ * View-parallel training (no reference equivalent: the
+ * reference trains one view per step on one GPU).  The SH / SG gradient rows
+ * of a step summed over n_views views, rebuilt from each view's DC gradient
+ * row and camera centre (view_grads.hip): per view the colour backward
+ * (CR/render_backward.cu:56-191) makes every row a function of the
+ * clamp-masked dL/dRGB = dL/dsh[:, 0, :] / SH_C0 and the view direction.
+ * gathered: [n_views][P * 3 + 4] fp32, view v's dL/dsh[:, 0, :] (P x 3)
+ * followed by its camera centre (3) and one pad float.  Outputs are
+ * overwritten: dL_dsh [P, SHM, 3] (rows past (sh_degree + 1)^2 zero), and
+ * when SGM > 0 dL_dsg_axis [P, SGM, 3], dL_dsg_sharpness [P, SGM],
+ * dL_dsg_color [P, SGM, 3] (lobes past sg_degree zero); sg_degree <= 7.
+ */
+int gsr_view_color_grads(int P, int sh_degree, int SHM, int sg_degree, int SGM, int n_views, const float* gathered,
+                         const float* means3D, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                         float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness, float* dL_dsg_color,
+                         void* stream);
+
+/*
  * Multi-view photometric term: replaces WarpPatchNCC /
  * forward_mode_differentiation (submodules/warp-patch-ncc/warp_patch_ncc.cu:5-52,
  * cuda_warp_patch_ncc/warp_patch_ncc_impl.cu:18-302), bound as

@@ -96,3 +96,85 @@ def test_view_parallel_allreduce_sums_views(tmp_path):
     assert torch.equal(r0["den"], torch.full((30,), 3.0))
     assert torch.equal(r0["mr"], torch.maximum(torch.arange(30, dtype=torch.int32),
                                                100 - torch.arange(30, dtype=torch.int32)))
+
+
+# ---- factored colour exchange (gsr_dist.FactoredViewGrads) ----------------
+_C0, _C1 = 0.28209479177387814, 0.4886025119029199
+_C2 = (1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396)
+_C3 = (-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+       1.445305721320277, -0.5900435899266435)
+
+
+def _sh_basis(d):
+    """SH basis [P, 16] of unit directions [P, 3] (CR/auxiliary.h:21-36, render_forward.cu:22-78)."""
+    x, y, z = d[:, 0], d[:, 1], d[:, 2]
+    xx, yy, zz, xy, yz, xz = x * x, y * y, z * z, x * y, y * z, x * z
+    return torch.stack([torch.full_like(x, _C0), -_C1 * y, _C1 * z, -_C1 * x,
+                        _C2[0] * xy, _C2[1] * yz, _C2[2] * (2 * zz - xx - yy), _C2[3] * xz, _C2[4] * (xx - yy),
+                        _C3[0] * y * (3 * xx - yy), _C3[1] * xy * z, _C3[2] * y * (4 * zz - xx - yy),
+                        _C3[3] * z * (2 * zz - 3 * xx - 3 * yy), _C3[4] * x * (4 * zz - xx - yy),
+                        _C3[5] * z * (xx - yy), _C3[6] * x * (xx - 3 * yy)], dim=1)
+
+
+def _expand_ref(gathered, n_views, means3D, sh_degree, dL_dsh, sg_degree=0, *_sg):
+    """float64 torch restatement of gsr_view_color_grads (view_grads.hip) for
+    SH only: dL/dsh[k] = sum_v Y_k(d_v) dsh0_v / SH_C0, the DC row summed as is."""
+    P = means3D.shape[0]
+    g = gathered.double().view(n_views, 3 * P + 4)
+    n = (sh_degree + 1) ** 2
+    out = torch.zeros(P, dL_dsh.shape[1], 3, dtype=torch.float64)
+    for v in range(n_views):
+        dsh0 = g[v, :3 * P].view(P, 3)
+        d = means3D.double() - g[v, 3 * P:3 * P + 3]
+        Y = _sh_basis(d / d.norm(dim=1, keepdim=True))
+        out[:, 0] += dsh0
+        out[:, 1:n] += Y[:, 1:n, None] * (dsh0 / _C0)[:, None, :]
+    dL_dsh.copy_(out.to(dL_dsh.dtype))
+
+
+def _factored_worker(rank, world, port, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd"), HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gsr_scene as S
+    from gsr_dist import FactoredViewGrads
+
+    inp = _view_grads(rank)
+    names = ("means3D", "opacities", "scales", "rotations", "shs")
+    ps = {k: inp[k].float().detach().requires_grad_(True) for k in names}
+    for k in names:
+        ps[k].grad = inp[k].grad.float().clone()
+    campos = S.orbit_cameras(2, 32, 24, center_z=3.0, max_deg=10.0)[rank].camera_center.float()
+    ex = FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"],
+                           expand=_expand_ref)
+    # the reference's split SH parameters (features_dc, features_rest) before the exchange above overwrites shs.grad
+    dc = ps["shs"][:, :1].detach().clone().requires_grad_(True)
+    rest = ps["shs"][:, 1:].detach().clone().requires_grad_(True)
+    dc.grad = ps["shs"].grad[:, :1].clone()
+    rest.grad = ps["shs"].grad[:, 1:].clone()
+    ex.exchange(campos, sh_degree=3)
+    geo = [t.detach().clone().requires_grad_(True) for t in (ps["means3D"], ps["opacities"], ps["scales"],
+                                                           ps["rotations"])]
+    for t, k in zip(geo, ("means3D", "opacities", "scales", "rotations")):
+        t.grad = inp[k].grad.float().clone()
+    FactoredViewGrads(*geo, (dc, rest), expand=_expand_ref).exchange(campos, sh_degree=3)
+    assert torch.equal(torch.cat([dc.grad, rest.grad], dim=1), ps["shs"].grad)
+    torch.save({k: ps[k].grad for k in names}, os.path.join(outdir, f"f{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_factored_exchange_sums_views(tmp_path):
+    """The factored exchange (geometry rows all-reduced, colour rows rebuilt
+    from the all-gathered DC rows + camera centres) gives every rank the sum
+    over views of the per-view gradients — the SH rows included — identically
+    on both ranks."""
+    port = _free_port()
+    mp.start_processes(_factored_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    f0 = torch.load(tmp_path / "f0.pt", weights_only=True)
+    f1 = torch.load(tmp_path / "f1.pt", weights_only=True)
+    g0, g1 = _view_grads(0), _view_grads(1)
+    for name in ("means3D", "opacities", "scales", "rotations", "shs"):
+        want = (g0[name].grad + g1[name].grad).float()
+        assert torch.equal(f0[name], f1[name]), name
+        torch.testing.assert_close(f0[name], want, rtol=1e-5, atol=1e-7)

@@ -44,3 +44,98 @@ def test_rccl_inplace_and_bucketed_allreduce(tmp_path):
                 assert [p.grad.data_ptr() for p in params] == ptrs
     finally:
         dist.destroy_process_group()
+
+
+def _views_backward(P, W, H, sh_degree, sg_degree, n_views, seed):
+    """Per-view gradients of one shared scene seen by n orbit views (the
+    C4 / C5 view-parallel setting), through the product autograd path."""
+    import math
+
+    import gsr_scene as S
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+
+    dev = torch.device("cuda", 0)
+    raw = S.make_gaussians(P, sh_degree=3, sg_degree=sg_degree, seed=seed, aspect=H / W, z_range=(4.0, 8.0))
+    inp = {k: v.detach().contiguous().to(dev) for k, v in S.activated_inputs(raw).items()}
+    cams = S.orbit_cameras(n_views, W, H)
+    per_view, campos = [], []
+    for v, cam_cpu in enumerate(cams):
+        cam = cam_cpu.to(dev)
+        ps = {k: t.clone().requires_grad_(True) for k, t in inp.items()}
+        settings = GaussianRasterizationSettings(
+            image_height=H, image_width=W, tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2),
+            kernel_size=0.0, bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam.world_view_transform,
+            projmatrix=cam.full_proj_transform, sh_degree=sh_degree, sg_degree=sg_degree, campos=cam.camera_center,
+            prefiltered=False, require_depth=True, debug=False)
+        color, radii, mdepth, alpha, normal = GaussianRasterizer(settings)(
+            means3D=ps["means3D"], means2D=torch.zeros(P, 3, device=dev, requires_grad=True),
+            opacities=ps["opacities"], shs=ps["shs"], sg_axis=ps["sg_axis"], sg_sharpness=ps["sg_sharpness"],
+            sg_color=ps["sg_color"], scales=ps["scales"], rotations=ps["rotations"])
+        g = S.upstream_grads(H, W, seed=20 + v)
+        torch.autograd.backward([color, mdepth, normal], [g["color"].to(dev), g["mdepth"].to(dev),
+                                                          g["normal"].to(dev)])
+        per_view.append({k: t.grad for k, t in ps.items()})
+        campos.append(cam.camera_center.float())
+    torch.cuda.synchronize()
+    return inp, per_view, campos
+
+
+@pytest.mark.parametrize("sh_degree,sg_degree", [(3, 0), (3, 7), (1, 0), (2, 3)])
+def test_view_color_grads_match_summed_views(sh_degree, sg_degree):
+    """gsr_view_color_grads (view_grads.hip) rebuilds the SH / SG gradient
+    rows of a view-parallel step from each view's DC row and camera centre:
+    against the sum over 3 views of the rows the backward itself produced
+    (clamped colour channels included), within fp32 rounding."""
+    from diff_gaussian_rasterization import _C
+
+    P, W, H, n = 20000, 320, 240, 3
+    inp, per_view, campos = _views_backward(P, W, H, sh_degree, sg_degree, n, seed=sh_degree + sg_degree)
+    dev = inp["means3D"].device
+    gathered = torch.cat([torch.cat([pv["shs"][:, 0, :].reshape(-1), c.reshape(3), torch.zeros(1, device=dev)])
+                          for pv, c in zip(per_view, campos)])
+    out = {k: torch.full_like(inp[k], float("nan")) for k in ("shs", "sg_axis", "sg_sharpness", "sg_color")}
+    _C.view_color_grads(gathered, n, inp["means3D"], sh_degree, out["shs"], sg_degree, inp["sg_axis"],
+                        inp["sg_sharpness"], inp["sg_color"], out["sg_axis"], out["sg_sharpness"], out["sg_color"])
+    torch.cuda.synchronize()
+    for k in ("shs", "sg_axis", "sg_sharpness", "sg_color"):
+        want = sum(pv[k].double() for pv in per_view)
+        got = out[k].double()
+        if want.numel() == 0:
+            continue
+        assert bool(torch.isfinite(got).all()), k
+        if not bool(want.any()):
+            assert not bool(got.any()), k
+            continue
+        err = float((got - want).norm() / want.norm())
+        assert err <= 1e-5, (k, err)
+        assert float((got - want).abs().max() / want.abs().max()) <= 1e-4, k
+    # the DC row is summed as gathered
+    assert torch.equal(out["shs"][:, 0, :], per_view[0]["shs"][:, 0, :] + per_view[1]["shs"][:, 0, :]
+                       + per_view[2]["shs"][:, 0, :])
+
+
+def test_rccl_factored_exchange_one_rank(tmp_path):
+    """FactoredViewGrads through RCCL on a one-rank group: the all-gather,
+    the geometry all-reduce and the kernel rebuild this view's own SH / SG
+    rows from its DC row (the two-rank sums: test_dist.py on gloo, and the
+    kernel against summed views above)."""
+    from gsr_dist import FactoredViewGrads
+
+    dev = torch.device("cuda", 0)
+    inp, per_view, campos = _views_backward(8000, 256, 192, 3, 7, 1, seed=5)
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        ps = {k: t.clone().requires_grad_(True) for k, t in inp.items()}
+        for k in ps:
+            ps[k].grad = per_view[0][k].clone()
+        ex = FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"],
+                               ps["sg_axis"], ps["sg_sharpness"], ps["sg_color"])
+        ex.exchange(campos[0], 3, 7)
+        torch.cuda.synchronize()
+        for k in ps:
+            want, got = per_view[0][k].double(), ps[k].grad.double()
+            err = float((got - want).norm() / want.norm().clamp_min(1e-30))
+            assert err <= 1e-5, (k, err)
+    finally:
+        dist.destroy_process_group()
