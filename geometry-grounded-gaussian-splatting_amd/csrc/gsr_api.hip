@@ -87,8 +87,13 @@ int bin_path(uint32_t gx, uint32_t gy) {
     return list_binning(gx, gy) ? kBinLists : kBinInstanceSort;
 }
 
-size_t carve_geom(void* base, int P, uint32_t gx, uint32_t gy, GeomState& g) {
+// `tmp`: where the forward-only scratch (scan / depth-sort temporaries, the
+// sortbin counts) goes; NULL keeps it at the end of the buffer itself.  The
+// fields the backward reads come first either way, so it re-carves without
+// knowing which layout the forward used.
+size_t carve_geom(void* base, int P, uint32_t gx, uint32_t gy, GeomState& g, Carver* tmp = nullptr) {
     Carver c(base);
+    Carver& t = tmp ? *tmp : c;
     g.splats = c.take<Splat>(P);
     g.depths = c.take<float>(P);
     g.tiles_touched = c.take<uint32_t>(P);
@@ -102,24 +107,28 @@ size_t carve_geom(void* base, int P, uint32_t gx, uint32_t gy, GeomState& g) {
     g.offsets_K = c.take<uint32_t>(1);
     g.near_flag = c.take<uint32_t>(1);
     g.scan_tmp_bytes = scan_temp_bytes(P) > reduce_temp_bytes(P) ? scan_temp_bytes(P) : reduce_temp_bytes(P);
-    g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
+    g.scan_tmp = t.take<char>(g.scan_tmp_bytes);
     g.dsort_tmp_bytes = depth_sort_temp_bytes(P);
-    g.dsort_tmp = c.take<char>(g.dsort_tmp_bytes);
+    g.dsort_tmp = t.take<char>(g.dsort_tmp_bytes);
     // (last: the fields above keep their offsets whichever path a call takes)
     const size_t tiles = (size_t)gx * gy;
     const bool sb = option(kOptSortbin) && sortbin_fits(gx, gy) && P > 0;
-    g.bin_hist = c.take<uint32_t>(sb ? (size_t)sortbin_blocks(P) * tiles : 0);
-    g.bin_total = c.take<uint32_t>(sb ? tiles : 0);
-    g.bin_start = c.take<uint32_t>(sb ? tiles + 1 : 0);
-    g.bin_info = c.take<uint32_t>(sb ? 4 : 0);
+    g.bin_hist = t.take<uint32_t>(sb ? (size_t)sortbin_blocks(P) * tiles : 0);
+    g.bin_total = t.take<uint32_t>(sb ? tiles : 0);
+    g.bin_start = t.take<uint32_t>(sb ? tiles + 1 : 0);
+    g.bin_info = t.take<uint32_t>(sb ? 4 : 0);
     return c.off + 256;
 }
 
 // Binning buffer.  The point list comes first, so its offset depends only on
 // the base (gsr_debug_binning carves it knowing K alone); the rest depends
 // on the path: tile lists (tilelists.hip) or emit + tile-id sort.
-size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, int path, BinningState& b) {
+// `tmp` as in carve_geom: the list-building (or key-sort) scratch, dead once
+// the point list is written, goes there instead of into the saved buffer.
+size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, int path, BinningState& b,
+                     Carver* tmp = nullptr) {
     Carver c(base);
+    Carver& t = tmp ? *tmp : c;
     b.point_list = c.take<uint32_t>(K);
     const int tiles = (int)(gx * gy);
     const int tile_bits = (int)higher_msb((uint32_t)tiles);
@@ -128,7 +137,7 @@ size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, int pat
     b.key_bytes = tile_key_bytes(tile_bits);
     b.pairs = nullptr;
     if (path == kBinSortbin) {
-        b.pairs = c.take<uint2>(K);
+        b.pairs = t.take<uint2>(K);
         b.rows = nullptr;
         b.qrec = nullptr;
         b.rows_count = b.rows_off = b.segbase = b.tiles_count = b.tiles_off = nullptr;
@@ -139,24 +148,24 @@ size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, int pat
         b.sort_tmp_bytes = 0;
     } else if (b.use_lists) {
         b.lists = list_layout(P, K, gx, gy);
-        b.rows = c.take<uint2>(K);
-        b.qrec = c.take<uint4>((size_t)2 * P);
-        b.rows_count = c.take<uint32_t>((size_t)gy * b.lists.nseg_rows);
-        b.rows_off = c.take<uint32_t>((size_t)gy * b.lists.nseg_rows);
-        b.segbase = c.take<uint32_t>(gy + 1);
-        b.tiles_count = c.take<uint32_t>((size_t)gx * b.lists.nseg_tiles_max + 1);
-        b.tiles_off = c.take<uint32_t>((size_t)gx * b.lists.nseg_tiles_max + 1);
-        b.list_tmp = c.take<char>(b.lists.tmp_bytes);
+        b.rows = t.take<uint2>(K);
+        b.qrec = t.take<uint4>((size_t)2 * P);
+        b.rows_count = t.take<uint32_t>((size_t)gy * b.lists.nseg_rows);
+        b.rows_off = t.take<uint32_t>((size_t)gy * b.lists.nseg_rows);
+        b.segbase = t.take<uint32_t>(gy + 1);
+        b.tiles_count = t.take<uint32_t>((size_t)gx * b.lists.nseg_tiles_max + 1);
+        b.tiles_off = t.take<uint32_t>((size_t)gx * b.lists.nseg_tiles_max + 1);
+        b.list_tmp = t.take<char>(b.lists.tmp_bytes);
         b.keys_unsorted = b.keys = nullptr;
         b.values_unsorted = nullptr;
         b.sort_tmp = nullptr;
         b.sort_tmp_bytes = 0;
     } else {
-        b.keys_unsorted = c.take<char>((size_t)K * b.key_bytes);
-        b.keys = c.take<char>((size_t)K * b.key_bytes);
-        b.values_unsorted = c.take<uint32_t>(K);
+        b.keys_unsorted = t.take<char>((size_t)K * b.key_bytes);
+        b.keys = t.take<char>((size_t)K * b.key_bytes);
+        b.values_unsorted = t.take<uint32_t>(K);
         b.sort_tmp_bytes = sort_temp_bytes(K, tile_bits);
-        b.sort_tmp = c.take<char>(b.sort_tmp_bytes);
+        b.sort_tmp = t.take<char>(b.sort_tmp_bytes);
     }
     return c.off + 256;
 }
@@ -405,7 +414,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 10; }
+int gsr_abi_version(void) { return 11; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -455,16 +464,17 @@ const char* gsr_last_error(void) { return g_last_error.c_str(); }
 // CR/auxiliary.h:146-148 (the reference traps the kernel)
 static const char* kPrefilteredMsg = "Point is filtered although prefiltered is set. This shouldn't happen!";
 
-int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
-                          gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
-                          int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
-                          int height, const float* means3D, const float* colors_precomp, const float* opacities,
-                          const float* scales, const float* rotations, const float* cov3D_precomp,
-                          const float* shs, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
-                          float scale_modifier, const float* viewmatrix, const float* projmatrix,
-                          const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
-                          float* out_color, float* out_mdepth, float* out_alpha, float* out_normal, int* radii,
-                          int require_depth, int debug, void* stream_ptr, int* num_rendered) {
+int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                             int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
+                             int height, const float* means3D, const float* colors_precomp, const float* opacities,
+                             const float* scales, const float* rotations, const float* cov3D_precomp,
+                             const float* shs, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                             float scale_modifier, const float* viewmatrix, const float* projmatrix,
+                             const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
+                             float* out_color, float* out_mdepth, float* out_alpha, float* out_normal, int* radii,
+                             int require_depth, int debug, void* stream_ptr, int* num_rendered,
+                             gsr_alloc_fn scratch_alloc, void* scratch_ctx) {
     hipStream_t stream = (hipStream_t)stream_ptr;
     if (num_rendered) *num_rendered = 0;
     FwdParams p = make_params(P, sh_degree, SHM, sg_degree, SGM, background, width, height, means3D, colors_precomp,
@@ -476,10 +486,19 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     if (!geom_alloc || !binning_alloc || !image_alloc || !tile_alloc) return fail(GSR_ERR_ARGS, "missing allocator");
     const int tiles = (int)(p.grid_x * p.grid_y);
 
+    // forward-only scratch from scratch_alloc when given (two blocks: the
+    // per-Gaussian sort/scan temporaries now, the list-building scratch once
+    // K is known), else inside the geometry / binning buffers
     GeomState gs;
-    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, p.grid_x, p.grid_y, gs));
+    Carver gtmp(nullptr);
+    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, p.grid_x, p.grid_y, gs, scratch_alloc ? &gtmp : nullptr));
     if (!gbuf) return fail(GSR_ERR_ALLOC, "geometry buffer allocation failed");
-    carve_geom(aligned_base(gbuf), P, p.grid_x, p.grid_y, gs);
+    if (scratch_alloc) {
+        void* sbuf = scratch_alloc(scratch_ctx, gtmp.off + 256);
+        if (!sbuf) return fail(GSR_ERR_ALLOC, "scratch allocation failed");
+        gtmp = Carver(aligned_base(sbuf));
+    }
+    carve_geom(aligned_base(gbuf), P, p.grid_x, p.grid_y, gs, scratch_alloc ? &gtmp : nullptr);
     TileState ts{};
     void* tbuf = tile_alloc(tile_ctx, carve_tiles(nullptr, tiles, ts));
     if (!tbuf) return fail(GSR_ERR_ALLOC, "tile buffer allocation failed");
@@ -542,9 +561,16 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     if (near_flag) return fail(GSR_ERR_ARGS, kPrefilteredMsg);
     const uint32_t K = Ks.x, K_live = Ks.y;
     BinningState bs;
-    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, path, bs));
+    Carver btmp(nullptr);
+    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, path, bs,
+                                                          scratch_alloc ? &btmp : nullptr));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, path, bs);
+    if (scratch_alloc) {
+        void* sbuf = scratch_alloc(scratch_ctx, btmp.off + 256);
+        if (!sbuf) return fail(GSR_ERR_ALLOC, "scratch allocation failed");
+        btmp = Carver(aligned_base(sbuf));
+    }
+    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, path, bs, scratch_alloc ? &btmp : nullptr);
     if (path == kBinSortbin) {
         GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_lists(p, gs, radii, bs, ts, stream), "tile lists");
     } else if (path == kBinLists) {
@@ -562,6 +588,25 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
               launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
     if (num_rendered) *num_rendered = (int)K;
     return GSR_OK;
+}
+
+int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                          gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                          int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
+                          int height, const float* means3D, const float* colors_precomp, const float* opacities,
+                          const float* scales, const float* rotations, const float* cov3D_precomp,
+                          const float* shs, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                          float scale_modifier, const float* viewmatrix, const float* projmatrix,
+                          const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
+                          float* out_color, float* out_mdepth, float* out_alpha, float* out_normal, int* radii,
+                          int require_depth, int debug, void* stream_ptr, int* num_rendered) {
+    return gsr_rasterize_forward_ex(geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx,
+                                    tile_alloc, tile_ctx, P, sh_degree, SHM, sg_degree, SGM, background, width,
+                                    height, means3D, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                                    shs, sg_axis, sg_sharpness, sg_color, scale_modifier, viewmatrix, projmatrix,
+                                    cam_pos, tan_fovx, tan_fovy, kernel_size, prefiltered, out_color, out_mdepth,
+                                    out_alpha, out_normal, radii, require_depth, debug, stream_ptr, num_rendered,
+                                    nullptr, nullptr);
 }
 
 int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
@@ -665,7 +710,8 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
                                const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
                                float kernel_size, int prefiltered, float* output, float* output2, uint8_t* inside,
                                int debug, void* stream_ptr, int* num_rendered, int* num_points,
-                               int* num_duplicated_tiles) {
+                               int* num_duplicated_tiles, gsr_alloc_fn scratch_alloc = nullptr,
+                               void* scratch_ctx = nullptr) {
     hipStream_t stream = (hipStream_t)stream_ptr;
     if (num_rendered) *num_rendered = 0;
     if (num_points) *num_points = 0;
@@ -686,10 +732,17 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
         return fail(GSR_ERR_ARGS, "missing allocator");
     const uint32_t tiles = p.grid_x * p.grid_y;
 
+    // forward-only scratch as in gsr_rasterize_forward_ex
     GeomState gs;
-    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, p.grid_x, p.grid_y, gs));
+    Carver gtmp(nullptr);
+    void* gbuf = geom_alloc(geom_ctx, carve_geom(nullptr, P, p.grid_x, p.grid_y, gs, scratch_alloc ? &gtmp : nullptr));
     if (!gbuf) return fail(GSR_ERR_ALLOC, "geometry buffer allocation failed");
-    carve_geom(aligned_base(gbuf), P, p.grid_x, p.grid_y, gs);
+    if (scratch_alloc) {
+        void* sbuf = scratch_alloc(scratch_ctx, gtmp.off + 256);
+        if (!sbuf) return fail(GSR_ERR_ALLOC, "scratch allocation failed");
+        gtmp = Carver(aligned_base(sbuf));
+    }
+    carve_geom(aligned_base(gbuf), P, p.grid_x, p.grid_y, gs, scratch_alloc ? &gtmp : nullptr);
     TileState ts{};
     SampleTiles st;
     void* tbuf = tile_alloc(tile_ctx, carve_sample_tiles(nullptr, (int)tiles, ts, st));
@@ -750,9 +803,16 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     if (near_flag) return fail(GSR_ERR_ARGS, kPrefilteredMsg);
     const uint32_t K = Ks.x, K_live = Ks.y, n_chunks = totals[2];
     BinningState bs;
-    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, path, bs));
+    Carver btmp(nullptr);
+    void* bbuf = binning_alloc(binning_ctx, carve_binning(nullptr, (int)K, P, p.grid_x, p.grid_y, path, bs,
+                                                          scratch_alloc ? &btmp : nullptr));
     if (!bbuf) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, path, bs);
+    if (scratch_alloc) {
+        void* sbuf = scratch_alloc(scratch_ctx, btmp.off + 256);
+        if (!sbuf) return fail(GSR_ERR_ALLOC, "scratch allocation failed");
+        btmp = Carver(aligned_base(sbuf));
+    }
+    carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, path, bs, scratch_alloc ? &btmp : nullptr);
     ChunkState cs{};
     void* cbuf = dup_tile_alloc(dup_tile_ctx, carve_chunks(nullptr, n_chunks, cs));
     if (!cbuf) return fail(GSR_ERR_ALLOC, "duplicated-tile buffer allocation failed");
@@ -794,6 +854,26 @@ int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
                                scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos,
                                tan_fovx, tan_fovy, kernel_size, prefiltered, output, nullptr, inside, debug,
                                stream_ptr, num_rendered, num_points, num_duplicated_tiles);
+}
+
+int gsr_sample_depth_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc,
+                                void* binning_ctx, gsr_alloc_fn point_alloc, void* point_ctx,
+                                gsr_alloc_fn point_binning_alloc, void* point_binning_ctx, gsr_alloc_fn tile_alloc,
+                                void* tile_ctx, gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P,
+                                int width, int height, const float* points3D, const float* means3D,
+                                const float* opacities, const float* scales, float scale_modifier,
+                                const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                                const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                                float kernel_size, int prefiltered, float* output, uint8_t* inside, int debug,
+                                void* stream_ptr, int* num_rendered, int* num_points, int* num_duplicated_tiles,
+                                gsr_alloc_fn scratch_alloc, void* scratch_ctx) {
+    return point_query_forward(kQuerySample, geom_alloc, geom_ctx, binning_alloc, binning_ctx, point_alloc,
+                               point_ctx, point_binning_alloc, point_binning_ctx, tile_alloc, tile_ctx,
+                               dup_tile_alloc, dup_tile_ctx, PN, P, width, height, points3D, means3D, opacities,
+                               scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos,
+                               tan_fovx, tan_fovy, kernel_size, prefiltered, output, nullptr, inside, debug,
+                               stream_ptr, num_rendered, num_points, num_duplicated_tiles, scratch_alloc,
+                               scratch_ctx);
 }
 
 int gsr_integrate_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,

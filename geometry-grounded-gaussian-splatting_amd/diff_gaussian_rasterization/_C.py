@@ -43,7 +43,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 def _load():
@@ -62,12 +62,16 @@ def _load():
     L.gsr_rasterize_forward.restype = i
     L.gsr_rasterize_forward.argtypes = ([_ALLOC, vp] * 4 + [i] * 5 + [vp, i, i] + [vp] * 10 + [f] + [vp] * 3
                                         + [f] * 3 + [i] + [vp] * 5 + [i, i, vp, ctypes.POINTER(i)])
+    L.gsr_rasterize_forward_ex.restype = i
+    L.gsr_rasterize_forward_ex.argtypes = L.gsr_rasterize_forward.argtypes + [_ALLOC, vp]
     L.gsr_rasterize_backward.restype = i
     L.gsr_rasterize_backward.argtypes = ([_ALLOC, vp] + [i] * 6 + [vp, i, i] + [vp] * 10 + [f] + [vp] * 3
                                          + [f] * 3 + [vp] * 4 + [vp] * 4 + [vp] * 4 + [vp] * 11 + [i, i, vp])
     L.gsr_sample_depth_forward.restype = i
     L.gsr_sample_depth_forward.argtypes = ([_ALLOC, vp] * 6 + [i] * 4 + [vp] * 4 + [f] + [vp] * 5 + [f] * 3 + [i]
                                            + [vp, vp, i, vp] + [ctypes.POINTER(i)] * 3)
+    L.gsr_sample_depth_forward_ex.restype = i
+    L.gsr_sample_depth_forward_ex.argtypes = L.gsr_sample_depth_forward.argtypes + [_ALLOC, vp]
     L.gsr_integrate_forward.restype = i
     L.gsr_integrate_forward.argtypes = ([_ALLOC, vp] * 6 + [i] * 4 + [vp] * 4 + [f] + [vp] * 6 + [f] * 3 + [i]
                                         + [vp, vp, i, vp, ctypes.POINTER(i)])
@@ -211,6 +215,27 @@ class _ByteBuffer:
         self.cb = _ALLOC(_cb)
 
 
+class _ScratchBlocks:
+    """Forward-only scratch for gsr_rasterize_forward_ex: every block the
+    callback hands out is kept until the forward returns, then dropped (the
+    caching allocator reuses it in stream order), so it is not saved for the
+    backward as the binning buffer is."""
+
+    def __init__(self, device):
+        self.device = device
+        self.blocks = []
+
+        def _cb(_ctx, n):
+            try:
+                t = torch.empty(max(int(n), 1), dtype=torch.uint8, device=self.device)
+                self.blocks.append(t)
+                return t.data_ptr()
+            except Exception:  # noqa: BLE001 - allocation failure is reported as NULL
+                return None
+
+        self.cb = _ALLOC(_cb)
+
+
 def _ptr(t):
     if t is None or t.numel() == 0:
         return None
@@ -265,9 +290,10 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     normal = torch.empty(3, H, W, **fopt)
     radii = torch.empty(P, dtype=torch.int32, device=dev)
     bufs = [_ByteBuffer(dev) for _ in range(4)]
+    scratch = _ScratchBlocks(dev)
     K = ctypes.c_int(0)
     with torch.cuda.device(dev):
-        rc = L.gsr_rasterize_forward(
+        rc = L.gsr_rasterize_forward_ex(
             bufs[0].cb, None, bufs[1].cb, None, bufs[2].cb, None, bufs[3].cb, None,
             P, int(sh_degree), SHM, int(sg_degree), SGM, _ptr(args["background"]), W, H, _ptr(args["means3D"]),
             _ptr(args["colors"]), _ptr(args["opacity"]), _ptr(args["scales"]), _ptr(args["rotations"]),
@@ -275,7 +301,8 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
             _ptr(args["sg_color"]), float(scale_modifier), _ptr(args["viewmatrix"]), _ptr(args["projmatrix"]),
             _ptr(args["campos"]), float(tan_fovx), float(tan_fovy), float(kernel_size), int(bool(prefiltered)),
             _ptr(color), _ptr(mdepth), _ptr(alpha), _ptr(normal), _ptr(radii), int(bool(require_depth)),
-            int(bool(debug)), _stream(dev), ctypes.byref(K))
+            int(bool(debug)), _stream(dev), ctypes.byref(K), scratch.cb, None)
+    del scratch
     _check(rc)
     return (K.value, color, alpha, normal, mdepth, radii, bufs[0].tensor, bufs[1].tensor, bufs[2].tensor,
             bufs[3].tensor)
@@ -414,19 +441,21 @@ def sample_rasterized_depth(points3D, means3D, opacity, scales, rotations, scale
     output = torch.zeros_like(points3D)
     inside = torch.zeros(points3D.shape[:-1], dtype=torch.bool, device=points3D.device)
     bufs = [_ByteBuffer(dev) for _ in range(6)]
+    scratch = _ScratchBlocks(dev)
     K, RN, TN = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
     if P != 0 and PN != 0:
         a = {k: _dev_contig(v, k) for k, v in dict(
             points3D=points3D, means3D=means3D, opacity=opacity, scales=scales, rotations=rotations,
             cov3D_precomp=cov3D_precomp, viewmatrix=viewmatrix, projmatrix=projmatrix, campos=campos).items()}
         with torch.cuda.device(dev):
-            rc = L.gsr_sample_depth_forward(
+            rc = L.gsr_sample_depth_forward_ex(
                 bufs[0].cb, None, bufs[1].cb, None, bufs[2].cb, None, bufs[3].cb, None, bufs[4].cb, None,
                 bufs[5].cb, None, PN, P, W, H, _ptr(a["points3D"]), _ptr(a["means3D"]), _ptr(a["opacity"]),
                 _ptr(a["scales"]), float(scale_modifier), _ptr(a["rotations"]), _ptr(a["cov3D_precomp"]),
                 _ptr(a["viewmatrix"]), _ptr(a["projmatrix"]), _ptr(a["campos"]), float(tan_fovx), float(tan_fovy),
                 float(kernel_size), int(bool(prefiltered)), _ptr(output), _ptr(inside), int(bool(debug)),
-                _stream(dev), ctypes.byref(K), ctypes.byref(RN), ctypes.byref(TN))
+                _stream(dev), ctypes.byref(K), ctypes.byref(RN), ctypes.byref(TN), scratch.cb, None)
+        del scratch
         _check(rc)
     return (K.value, RN.value, TN.value, output, inside, *[b.tensor for b in bufs])
 

@@ -69,6 +69,28 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
                           int require_depth, int debug, void* stream, int* num_rendered);
 
 /*
+ * gsr_rasterize_forward with a fifth allocator for the forward-only scratch
+ * (the depth-sort / scan temporaries and the tile-list building state: at 1M
+ * Gaussians and 1080p about 0.25 GB that the reference keeps inside the saved
+ * geometry / binning buffers until the backward).  scratch_alloc may be called
+ * more than once per call; every block it returns must stay valid until the
+ * call returns, and may be released then (stream-ordered: the kernels that use
+ * it are queued on `stream`).  scratch_alloc == NULL is gsr_rasterize_forward.
+ * The buffers the backward reads have the same layout either way.
+ */
+int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                             int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
+                             int height, const float* means3D, const float* colors_precomp, const float* opacities,
+                             const float* scales, const float* rotations, const float* cov3D_precomp,
+                             const float* shs, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                             float scale_modifier, const float* viewmatrix, const float* projmatrix,
+                             const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
+                             float* out_color, float* out_mdepth, float* out_alpha, float* out_normal, int* radii,
+                             int require_depth, int debug, void* stream, int* num_rendered,
+                             gsr_alloc_fn scratch_alloc, void* scratch_ctx);
+
+/*
  * Replaces CudaRasterizer::Rasterizer::backward (rasterizer.h:63-109,
  * rasterizer_impl.cu:452-592).  geom/binning/image/tile buffers are the ones
  * the forward obtained from its callbacks; R is the forward's num_rendered.
@@ -135,6 +157,20 @@ int gsr_sample_depth_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
                              const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size,
                              int prefiltered, float* output, uint8_t* inside, int debug, void* stream,
                              int* num_rendered, int* num_points, int* num_duplicated_tiles);
+
+/* gsr_sample_depth_forward with the forward-only scratch allocator of
+ * gsr_rasterize_forward_ex (same contract; the saved buffers keep their layout). */
+int gsr_sample_depth_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc,
+                                void* binning_ctx, gsr_alloc_fn point_alloc, void* point_ctx,
+                                gsr_alloc_fn point_binning_alloc, void* point_binning_ctx, gsr_alloc_fn tile_alloc,
+                                void* tile_ctx, gsr_alloc_fn dup_tile_alloc, void* dup_tile_ctx, int PN, int P,
+                                int width, int height, const float* points3D, const float* means3D,
+                                const float* opacities, const float* scales, float scale_modifier,
+                                const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                                const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                                float kernel_size, int prefiltered, float* output, uint8_t* inside, int debug,
+                                void* stream, int* num_rendered, int* num_points, int* num_duplicated_tiles,
+                                gsr_alloc_fn scratch_alloc, void* scratch_ctx);
 
 /*
  * integrate / evaluate_sdf: forward-only queries of the

@@ -360,6 +360,47 @@ def test_backward_none_upstream():
             assert err <= 1e-5, (none, name, err)
 
 
+def test_forward_scratch_split_is_exact(binning, monkeypatch):
+    """gsr_rasterize_forward_ex (the Python binding's forward) keeps the
+    forward-only scratch out of the saved buffers: same images, point list and
+    gradients as gsr_rasterize_forward (scratch in the buffers, the reference's
+    layout), bit for bit (gradients: to the atomics' summation order), with
+    smaller geometry and binning buffers."""
+    from diff_gaussian_rasterization import _C
+
+    c = Hh.small_case(P=4000, W=200, H=120, seed=5, log_scale=math.log(0.03))
+    ga = [_gpu(x) for x in _fwd_args(c)] + [False]
+    g = {k: _gpu(v) for k, v in S.upstream_grads(120, 200).items()}
+
+    def run():
+        out = _C.rasterize_gaussians(*ga)
+        K, color, alpha, normal, mdepth, radii = out[:6]
+        grads = _C.rasterize_gaussians_backward(*ga[:19], g["color"], g["mdepth"], None, g["normal"], alpha, normal,
+                                                mdepth, _gpu(c["cam"].camera_center), radii, out[6], K, out[7],
+                                                out[8], out[9], True, False)
+        plist, ranges = _C.debug_binning(out[7], out[9], K, 120, 200)
+        live = int(ranges[:, 1].max())  # (past the live entries the capacity is unwritten)
+        return out, grads, torch.from_numpy(plist[:live].astype(np.int64)), torch.from_numpy(ranges.astype(np.int64))
+
+    split = run()
+
+    class _NoScratch:  # a NULL scratch allocator: gsr_rasterize_forward's layout
+        def __init__(self, _dev):
+            self.cb = _C._ALLOC()
+
+    monkeypatch.setattr(_C, "_ScratchBlocks", _NoScratch)
+    whole = run()
+    assert split[0][0] == whole[0][0]
+    for a, b in zip(split[0][1:6], whole[0][1:6]):
+        assert torch.equal(a, b)
+    assert torch.equal(split[2], whole[2]) and torch.equal(split[3], whole[3])
+    for name, a, b in zip(GRAD_NAMES, split[1], whole[1]):  # (float atomics: order-dependent at ~1 ulp)
+        if b.numel():
+            assert float((a - b).abs().max()) <= 1e-5 * max(float(b.abs().max()), 1e-30), name
+    assert split[0][6].numel() < whole[0][6].numel()  # geometry buffer
+    assert split[0][7].numel() < whole[0][7].numel()  # binning buffer
+
+
 def test_autograd_render_end_to_end():
     """gaussian_renderer.render() -> GaussianRasterizer -> autograd, with the
     GaussianModel getters in front: gradients reach the raw parameters and the
