@@ -85,8 +85,11 @@ void sim_set_hnoise(float v) { g_hnoise = v; }
 void sim_set_pred(int sel, float smax) { g_sel = sel; g_smax = smax; }
 void sim_set_halley(int v) { g_halley = v; }
 /* h, h', h'' of h = log T + ln 2 */
+static float g_lastF = 0.f;  /* sum |e| of the last vac_d2 (a bound on |H''| either side of a splat peak) */
+static float g_loose = 0.f, g_tolF = 0.f;
+void sim_set_loose(float loose_rel, float tolF) { g_loose = loose_rel; g_tolF = tolF; }
 static void vac_d2(const contrib_t* c, int n, float t, float* hv, float* d1, float* d2) {
-    float A = 1.f, B = 1.f, D = 0.f, E = 0.f;
+    float A = 1.f, B = 1.f, D = 0.f, E = 0.f, F = 0.f;
     for (int i = 0; i < n; i++) {
         const int ball = c[i].rs > 0;
         const float d = (t - c[i].tp) * c[i].rs;
@@ -101,8 +104,10 @@ static void vac_d2(const contrib_t* c, int n, float t, float* hv, float* d1, flo
             D += -0.5f * x * fabsf(d) * c[i].rs;
             const float e = 0.5f * c[i].rs * c[i].rs * x * (1.f - d * d * (1.f + x));
             E += before ? e : -e;
+            F += fabsf(e);
         }
     }
+    g_lastF = F;
     *hv = logf(A) - 0.5f * logf(B) + 0.69314718f;
     *d1 = D;
     *d2 = E;
@@ -662,7 +667,10 @@ static int halley_from(const contrib_t* c, int n, float t, float lo, float hi, f
         const float den = 2.f * dh * dh - h * dd;
         float tn = den != 0.f ? t - 2.f * h * dh / den : 0.5f * (lo + hi);
         if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
-        if ((dh < 0.f && fabsf(h) <= tol * -dh) || hi - lo <= tol) {
+        const float sc = fmaxf(t, 1.f), D = -dh;
+        const int loose = g_loose > 0.f && D > 0.f && fabsf(h) <= g_loose * sc * D &&
+                          fabsf(h) * g_lastF <= g_tolF * D * D;  /* step x curvature (F / D) <= tolF */
+        if ((dh < 0.f && fabsf(h) <= tol * -dh) || hi - lo <= tol || loose) {
             if (-dh * 1e-6f * fmaxf(t, 1.f) >= hnoise) { *res = tn; return walks; }
             return -walks;
         }

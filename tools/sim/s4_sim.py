@@ -7,6 +7,8 @@ sys.argv = ["median_sim.py", "41", "2"]
 g = runpy.run_path(__file__.replace("s4_sim.py", "median_sim.py"))
 sim, tiles, f, u32 = g["sim"], g["tiles"], g["f"], g["u32"]
 import os
+sim.sim_set_loose(ctypes.c_float(float(os.environ.get("SIM_LOOSE", "0"))),
+                  ctypes.c_float(float(os.environ.get("SIM_TOLF", "1e-6"))))
 o = np.array([float(x) for x in os.environ.get("SIM_OFFS", "-0.2,-0.1,-0.05,-0.025,0,0.025,0.05,0.1,0.2").split(",")],
              np.float32)
 out = np.zeros(32)
