@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(64)
 // slots, same values; chunks with more than kEmitCap instances write
 // directly.
 #ifndef GSR_TILES_EMIT_SORTED
-#define GSR_TILES_EMIT_SORTED 1
+#define GSR_TILES_EMIT_SORTED 2  // 2: tiles_emit_wide_kernel (default), 1: 64-entry chunks, 0: direct
 #endif
 constexpr int kEmitCap = 512;  // instances staged per 64-entry chunk (C3 averages ~3 tiles per row entry)
 
@@ -594,6 +594,108 @@ __global__ void __launch_bounds__(64)
     });
 }
 
+// tiles_emit_sorted with chunks of 64 NPL entries (NPL per lane: entries
+// c0 + 64 h + lane, h < NPL, with a mask plane each), so the per-chunk work —
+// the bucket scan of chunk_bases, the mask clearing and the barriers — is
+// shared by NPL times the instances.  A bucket's plane-h entries rank after
+// all of its entries in planes < h (they precede them in the row), so the
+// slots and values are those of the 64-entry kernel.
+#ifndef GSR_EMIT_PLANES
+#define GSR_EMIT_PLANES 2
+#endif
+constexpr int kEmitPlanes = GSR_EMIT_PLANES;
+constexpr int kEmitCapW = 512 * kEmitPlanes;
+
+template <int NPL>
+__global__ void __launch_bounds__(64)
+    tiles_emit_wide_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
+                           const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
+                           const uint2* __restrict__ rows, const uint32_t* __restrict__ O,
+                           uint32_t* __restrict__ point_list) {
+    constexpr uint32_t kCap = 512 * NPL;
+    // LDS: NPL x [gx] masks, [gx] running slots, [gx] chunk offsets, [gx] write bases, kCap ids and tiles
+    extern __shared__ unsigned long long s_dyn[];
+    unsigned long long* s_cov = s_dyn;
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + NPL * gx);
+    uint32_t* s_off = s_run + gx;
+    uint32_t* s_base = s_off + gx;
+    uint32_t* s_id = s_base + gx;
+    uint16_t* s_x = reinterpret_cast<uint16_t*>(s_id + kCap);
+    const int lane = threadIdx.x;
+    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
+    const unsigned long long bit = 1ull << lane, below = bit - 1ull;
+    for_xcd_segments(segbase[gy], [&](uint32_t l) {
+        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
+        const size_t base = (size_t)gx * segbase[S.y];
+        __syncthreads();  // previous segment done with the LDS
+        for (uint32_t x = lane; x < gx; x += 64) s_run[x] = O[base + (size_t)x * S.nk + S.k];
+        for (uint32_t x = lane; x < NPL * gx; x += 64) s_cov[x] = 0ull;
+        __syncthreads();
+        for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64 * NPL) {
+            bool on[NPL];
+            uint32_t id[NPL], lo[NPL], hi[NPL];
+#pragma unroll
+            for (int h = 0; h < NPL; h++) {
+                const uint32_t e = c0 + 64 * h + lane;
+                on[h] = e < S.e1;
+                const uint2 ent = on[h] ? rows[e] : make_uint2(0u, 1u);  // empty span when off
+                id[h] = ent.x;
+                lo[h] = ent.y & 0xffffu;
+                hi[h] = on[h] ? (ent.y >> 16) : 0u;
+            }
+#pragma unroll
+            for (int h = 0; h < NPL; h++)
+                for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++) atomicOr(&s_cov[h * gx + x], bit);
+            __syncthreads();
+            // per tile: count (all planes), base among the chunk's instances, write base (chunk_bases)
+            uint32_t carry = 0;
+            for (uint32_t b0 = 0; b0 < gx; b0 += 64) {
+                const uint32_t b = b0 + lane;
+                uint32_t cnt = 0;
+                if (b < gx) {
+#pragma unroll
+                    for (int h = 0; h < NPL; h++) cnt += (uint32_t)__popcll(s_cov[h * gx + b]);
+                }
+                const uint32_t incl = wave_incl_scan(cnt);
+                if (b < gx) {
+                    const uint32_t o = carry + incl - cnt;
+                    const uint32_t r = s_run[b];
+                    s_off[b] = o;
+                    s_base[b] = r - o;
+                    s_run[b] = r + cnt;
+                }
+                carry += __shfl(incl, 63, 64);
+            }
+            __syncthreads();
+            // rank of plane h's entry at tile x: the chunk's earlier planes, then the lower lanes
+            auto rank = [&](int h, uint32_t x) {
+                uint32_t r = (uint32_t)__popcll(s_cov[h * gx + x] & below);
+                for (int k = 0; k < h; k++) r += (uint32_t)__popcll(s_cov[k * gx + x]);
+                return r;
+            };
+            if (carry <= kCap) {
+#pragma unroll
+                for (int h = 0; h < NPL; h++)
+                    for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++) {
+                        const uint32_t p = s_off[x] + rank(h, x);
+                        s_id[p] = id[h];
+                        s_x[p] = (uint16_t)x;
+                    }
+                __syncthreads();
+                for (uint32_t p = lane; p < carry; p += 64) point_list[s_base[s_x[p]] + p] = s_id[p];
+            } else {
+#pragma unroll
+                for (int h = 0; h < NPL; h++)
+                    for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++)
+                        point_list[s_base[x] + s_off[x] + rank(h, x)] = id[h];
+            }
+            __syncthreads();
+            for (uint32_t x = lane; x < NPL * gx; x += 64) s_cov[x] = 0ull;
+            __syncthreads();
+        }
+    });
+}
+
 __global__ void __launch_bounds__(256)
     list_ranges_kernel(uint32_t gx, uint32_t gy, const uint32_t* __restrict__ segbase, const uint32_t* __restrict__ O,
                        uint2* __restrict__ ranges) {
@@ -641,7 +743,11 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     if ((e = launch_scan_excl(bs.tiles_count, bs.tiles_off, (size_t)gx * L.nseg_tiles_max, 0u, bs.segbase + gy, gx,
                               sums, stream)) != hipSuccess)
         return e;
-    if (GSR_TILES_EMIT_SORTED)
+    if (GSR_TILES_EMIT_SORTED == 2)
+        hipLaunchKernelGGL(tiles_emit_wide_kernel<kEmitPlanes>, dim3(kTileBlocks), dim3(64),
+                           (8 * kEmitPlanes + 12) * gx + 6 * kEmitCapW, stream, gx,
+                           gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
+    else if (GSR_TILES_EMIT_SORTED)
         hipLaunchKernelGGL(tiles_emit_sorted_kernel, dim3(kTileBlocks), dim3(64), 20 * gx + 6 * kEmitCap, stream, gx,
                            gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
     else
