@@ -34,7 +34,8 @@ def stage_of(name: str) -> str | None:
     if "tile_ranges_kernel" in n:
         return "tile_ranges"
     if any(k in n for k in ("rows_count_kernel", "rows_emit_kernel", "tiles_setup_kernel", "tiles_count_kernel",
-                            "tiles_emit_kernel", "tiles_emit_sorted_kernel", "list_ranges_kernel")):
+                            "tiles_emit_kernel", "tiles_emit_sorted_kernel", "tiles_emit_wide_kernel",
+                            "list_ranges_kernel")):
         return "tile_lists"
     if "render_fwd_kernel" in n:
         return "render_fwd"
