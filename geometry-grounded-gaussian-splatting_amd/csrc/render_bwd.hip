@@ -258,16 +258,34 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
     int toDo = max_contrib;
     for (int i = 0; i < rounds; i++, toDo -= kBwdBatch) {
         __syncthreads();
-        for (int k = tid; k < kBwdBatch; k += kThreads) {
-            const int c = i * kBwdBatch + k;
-            if (c < max_contrib) {
-                const uint32_t g = a.point_list[range.x + max_contrib - c - 1];
-                const Splat* sp = a.splats + g;
-                s_id[k] = g;
-                s_w0[k] = sp->w0;
-                s_w1[k] = sp->w1;
-                s_w2[k] = sp->w2;
-                s_w3[k] = sp->w3;
+        {
+            // every list entry of the batch, then every record, requested before
+            // any is stored (left to itself the compiler waited on each of the
+            // four record loads in turn, reusing one register quad)
+            constexpr int kPer = kBwdBatch / kThreads;
+            uint32_t g[kPer];
+#pragma unroll
+            for (int u = 0; u < kPer; u++) {
+                const int c = i * kBwdBatch + tid + u * kThreads;
+                g[u] = c < max_contrib ? a.point_list[range.x + max_contrib - c - 1] : 0u;
+            }
+            float4 r[kPer][4];
+#pragma unroll
+            for (int u = 0; u < kPer; u++) {
+                const float4* sp = reinterpret_cast<const float4*>(a.splats + g[u]);
+#pragma unroll
+                for (int w = 0; w < 4; w++) r[u][w] = sp[w];
+            }
+#pragma unroll
+            for (int u = 0; u < kPer; u++) {
+                const int k = tid + u * kThreads;
+                if (i * kBwdBatch + k < max_contrib) {
+                    s_id[k] = g[u];
+                    s_w0[k] = r[u][0];
+                    s_w1[k] = r[u][1];
+                    s_w2[k] = r[u][2];
+                    s_w3[k] = r[u][3];
+                }
             }
         }
         __syncthreads();
