@@ -97,6 +97,43 @@ def test_sample_parity(case):
     _run(c, pts)
 
 
+def test_sample_scratch_split_is_exact(monkeypatch):
+    """gsr_sample_depth_forward_ex (the binding's forward) with its
+    forward-only scratch outside the saved buffers against
+    gsr_sample_depth_forward's layout (a NULL scratch allocator): the same
+    points, flags and counts bit for bit, the same gradients to the atomics'
+    summation order, and smaller geometry / binning buffers."""
+    from diff_gaussian_rasterization import _C
+
+    c = Hh.small_case(P=2000, W=160, H=96, seed=2, log_scale=math.log(0.05))
+    pts = sample_points(c, 20000, 102)
+    ga = [_gpu(x) for x in sample_args(c, pts)] + [False]
+    g = _gpu(torch.randn(pts.shape, generator=torch.Generator().manual_seed(3)) * 1e-2)
+
+    def run():
+        out = _C.sample_rasterized_depth(*ga)
+        K, RN, TN, _, inside = out[:5]
+        gb = _C.sample_rasterized_depth_backward(*ga[:9], inside, g, c["tanx"], c["tany"], 0.0, c["H"], c["W"],
+                                                 _gpu(c["cam"].camera_center), *out[5:11], K, RN, TN, False, False)
+        return out, gb
+
+    split = run()
+
+    class _NoScratch:  # a NULL scratch allocator: gsr_sample_depth_forward's layout
+        def __init__(self, _dev):
+            self.cb = _C._ALLOC()
+
+    monkeypatch.setattr(_C, "_ScratchBlocks", _NoScratch)
+    whole = run()
+    assert split[0][:3] == whole[0][:3]
+    assert torch.equal(split[0][3], whole[0][3]) and torch.equal(split[0][4], whole[0][4])
+    for name, a, b in zip(GRADS, split[1], whole[1]):
+        if b.numel():
+            assert float((a - b).abs().max()) <= 1e-5 * max(float(b.abs().max()), 1e-30), name
+    assert split[0][5].numel() < whole[0][5].numel()  # geometry buffer
+    assert split[0][6].numel() < whole[0][6].numel()  # binning buffer
+
+
 def test_sample_parity_batched_shape_and_kernel_size():
     """points3D of shape [H, W, 3] (the training call); forward with kernel
     size 0.0 and backward with the settings' 0.1, as the reference wrapper
