@@ -104,6 +104,31 @@ __device__ inline void sh_basis(int D, float x, float y, float z, float* Y) {
 
 __device__ inline int sh_count(int D) { return (D + 1) * (D + 1); }
 
+// A lobe row (21 or 7 floats, 84 / 28 B) is only 4-B aligned; gfx950 serves
+// unaligned dwordx4 accesses, so a row moves as 16-B pieces: 6 + 6 + 2 load
+// instructions per Gaussian instead of 49 single dwords, each of which made
+// the L1 look up 64 distinct lines (the rows of a wave's lanes are 84 B apart).
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+template <int N>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, float (&v)[N]) {
+#pragma unroll
+    for (int k = 0; k + 4 <= N; k += 4) {
+        const f4u t = *reinterpret_cast<const f4u*>(p + k);
+        v[k] = t.x;
+        v[k + 1] = t.y;
+        v[k + 2] = t.z;
+        v[k + 3] = t.w;
+    }
+#pragma unroll
+    for (int k = N / 4 * 4; k < N; k++) v[k] = p[k];
+}
+template <int N>
+__device__ __forceinline__ void store_row(float* __restrict__ p, const float (&v)[N]) {
+#pragma unroll
+    for (int k = 0; k + 4 <= N; k += 4) *reinterpret_cast<f4u*>(p + k) = f4u{v[k], v[k + 1], v[k + 2], v[k + 3]};
+#pragma unroll
+    for (int k = N / 4 * 4; k < N; k++) p[k] = v[k];
+}
 // One Gaussian's SH row ([SHM][3] floats, coefficient-major) in registers.
 // The training layout (SHM = 16, 16-B aligned rows of 192 B) moves as 12
 // dwordx4 per lane; other layouts element by element (entries >= 3 n read 0).

@@ -81,17 +81,15 @@ __device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
 // contiguous accesses issued together, instead of 7 dependent iterations of
 // 3-float pieces.  Same arithmetic in the same order as the generic loop.
 constexpr int kSG7 = 7;
+// (lobe rows move as unaligned 16-B pieces: load_row / store_row, gsr_math.h)
 struct SG7Rows {
     float ax[3 * kSG7], gc[3 * kSG7], sharp[kSG7];
 };
 __device__ __forceinline__ void sg7_load(const PreprocessBwdArgs& a, int idx, SG7Rows& r) {
     const size_t o0 = (size_t)idx * kSG7;
-#pragma unroll
-    for (int k = 0; k < 3 * kSG7; k++) r.ax[k] = a.sg_axis[3 * o0 + k];
-#pragma unroll
-    for (int k = 0; k < 3 * kSG7; k++) r.gc[k] = a.sg_color[3 * o0 + k];
-#pragma unroll
-    for (int k = 0; k < kSG7; k++) r.sharp[k] = a.sg_sharpness[o0 + k];
+    load_row(a.sg_axis + 3 * o0, r.ax);
+    load_row(a.sg_color + 3 * o0, r.gc);
+    load_row(a.sg_sharpness + o0, r.sharp);
 }
 __device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, const SG7Rows& rows, float x, float y,
                                         float z, float dR0, float dR1, float dR2, float& ddx, float& ddy, float& ddz) {
@@ -120,12 +118,9 @@ __device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, con
         ddy += dL_daux * axs[1];
         ddz += dL_daux * axs[2];
     }
-#pragma unroll
-    for (int k = 0; k < 3 * kSG7; k++) a.dL_dsg_color[3 * o0 + k] = dcol[k];
-#pragma unroll
-    for (int k = 0; k < kSG7; k++) a.dL_dsg_sharpness[o0 + k] = dsh[k];
-#pragma unroll
-    for (int k = 0; k < 3 * kSG7; k++) a.dL_dsg_axis[3 * o0 + k] = dax[k];
+    store_row(a.dL_dsg_color + 3 * o0, dcol);
+    store_row(a.dL_dsg_sharpness + o0, dsh);
+    store_row(a.dL_dsg_axis + 3 * o0, dax);
 }
 
 #ifndef GSR_PBWD_WAVES
