@@ -604,7 +604,10 @@ __global__ void __launch_bounds__(64)
 #define GSR_EMIT_PLANES 2
 #endif
 constexpr int kEmitPlanes = GSR_EMIT_PLANES;
-constexpr int kEmitCapW = 512 * kEmitPlanes;
+#ifndef GSR_EMIT_CAP
+#define GSR_EMIT_CAP (512 * GSR_EMIT_PLANES)
+#endif
+constexpr int kEmitCapW = GSR_EMIT_CAP;  // instances staged per chunk (more: direct writes)
 
 template <int NPL>
 __global__ void __launch_bounds__(64)
@@ -612,7 +615,7 @@ __global__ void __launch_bounds__(64)
                            const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
                            const uint2* __restrict__ rows, const uint32_t* __restrict__ O,
                            uint32_t* __restrict__ point_list) {
-    constexpr uint32_t kCap = 512 * NPL;
+    constexpr uint32_t kCap = kEmitCapW;
     // LDS: NPL x [gx] masks, [gx] running slots, [gx] chunk offsets, [gx] write bases, kCap ids and tiles
     extern __shared__ unsigned long long s_dyn[];
     unsigned long long* s_cov = s_dyn;
