@@ -8,7 +8,11 @@ view of 1M synthetic Gaussians (SH degree 3, require_depth=True, the state
 after iteration 7000).  Inputs are activated tensors already resident in HBM;
 losses, optimiser and the Python getters are outside the step.
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W] [--config C2|C3|C5] [--no-depth] [--forward-only]
+
+--config C2 is BASELINE.json configs[1] (100k Gaussians, one 800x800 view,
+forward only); --no-depth is require_depth=False (training iterations <
+7000); --forward-only times the forward alone (no autograd graph).
 
 With N > 1 (launched by torch.distributed.run, one rank per GPU) every rank
 renders its own view (C4: cameras orbiting the scene) of the same Gaussians
@@ -45,6 +49,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+CLOCK_HZ = 2.4e9  # max clock (MI355X_MICROARCH.md chip table)
+SIMDS = 256 * 4  # 256 CUs x 4 SIMD-32
+VALU_ISSUE_CYCLES = 4  # one wave64 VALU instruction per 4 cycles per SIMD (the valu_busy convention)
 
 
 def log(*a):
@@ -56,11 +63,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", choices=["C3", "C5"], default="C3",
-                    help="C3: 1M Gaussians, SH 3 (the metric's config); C5: 5M Gaussians, SH 3 + SG 7")
+    ap.add_argument("--config", choices=["C2", "C3", "C5"], default="C3",
+                    help="C3: 1M Gaussians, SH 3 (the metric's config); C5: 5M Gaussians, SH 3 + SG 7; "
+                         "C2: 100k Gaussians, 800x800, forward only")
     ap.add_argument("--P", type=int, default=None)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--forward-only", action="store_true", help="time the forward alone (C2's workload)")
     ap.add_argument("--sh-degree", type=int, default=3)
     ap.add_argument("--sg-degree", type=int, default=None)
     ap.add_argument("--no-depth", action="store_true", help="require_depth=False (iterations < 7000)")
@@ -74,12 +83,16 @@ def parse():
                     help="bracket every stage with hipEvents inside the timed region too (each event pair "
                          "idles the stream ~10 us; default: only the dominant stage)")
     a = ap.parse_args()
-    preset = {"C3": (1_000_000, 0), "C5": (5_000_000, 7)}[a.config]
+    preset = {"C2": (100_000, 0, 800, 800), "C3": (1_000_000, 0, 1920, 1080), "C5": (5_000_000, 7, 1920, 1080)}[a.config]
     a.P = preset[0] if a.P is None else a.P
     a.sg_degree = preset[1] if a.sg_degree is None else a.sg_degree
-    # PMC traffic in profiles/ is measured on the default workload only
-    a.default_workload = (a.config == "C3" and a.P == 1_000_000 and a.sg_degree == 0 and a.width == 1920
-                          and a.height == 1080 and a.sh_degree == 3 and not a.no_depth)
+    a.width = preset[2] if a.width is None else a.width
+    a.height = preset[3] if a.height is None else a.height
+    a.forward_only = a.forward_only or a.config == "C2"
+    # PMC counters in profiles/ are per workload: pmc_<key>.json written by tools/pmc_summary.py
+    a.preset_workload = (a.P, a.sg_degree, a.width, a.height) == preset and a.sh_degree == 3
+    a.workload_key = a.config + ("-nodepth" if a.no_depth else "") + (
+        "-fwd" if a.forward_only and a.config != "C2" else "")
     return a
 
 
@@ -109,27 +122,62 @@ def stage_bytes(P, K, K_live, HW, shm, sgm, geom):
     }
 
 
-def load_pmc_traffic(kernel_stage):
-    """(HBM bytes per launch, VALU busy fraction) of `kernel_stage` from
-    profiles/pmc_summary.json (written by tools/profile.sh from separate
-    rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2 correction applied)."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def load_pmc(workload_key, kernel_stage):
+    """(HBM bytes per launch, VALU instructions per launch, file) of
+    `kernel_stage` from profiles/pmc_<workload_key>.json (written by
+    tools/profile.sh + tools/pmc_summary.py from separate rocprofv3 --pmc
+    passes of this same workload, gfx950 FETCH_SIZE x2 correction applied)."""
+    name = f"pmc_{workload_key}.json"
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
             st = json.load(f)["stages"][kernel_stage]
-        return st["hbm_bytes_per_launch"], st.get("valu_busy")
-    except Exception:  # noqa: BLE001 - absent or stale summary -> null
-        return None, None
+        return st["hbm_bytes_per_launch"], st.get("sq_per_call", {}).get("SQ_INSTS_VALU"), name
+    except Exception:  # noqa: BLE001 - absent summary -> null
+        return None, None, None
 
 
-def cpu_baseline(args, inputs_cpu, cam, tanx, tany, grads_cpu):
-    """Time the C oracle (tests' checker) on this host: full per-Gaussian work
-    and binning, every s-th tile rendered forward and backward, tile time
-    extrapolated x s."""
+def host_cores():
+    """The CPU cores this process may use: its affinity set, capped by the
+    cgroup CPU quota (a GPU box shares a larger machine; os.cpu_count() shows
+    every CPU of the machine)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except Exception:  # noqa: BLE001 - no cgroup v2 quota
+        pass
+    return (min(n, quota) if quota else n), {"nproc": os.cpu_count(), "affinity": n, "cgroup_quota_cores": quota}
+
+
+def getter_baseline(raw, cores):
+    """The reference's Python preprocess path on the host cores: the
+    GaussianModel getters (scene/gaussian_model.py:146-212, restated in
+    gsr_scene.activated_inputs) over the workload's Gaussians in torch on
+    the CPU, median of 5 calls."""
+    import gsr_scene as S
+
+    torch.set_num_threads(cores)
+    times = []
+    with torch.no_grad():
+        for _ in range(6):
+            t0 = time.perf_counter()
+            S.activated_inputs(raw)
+            times.append(time.perf_counter() - t0)
+    ms = sorted(times[1:])[2] * 1e3
+    return {"ms_per_call": round(ms, 3), "calls_per_s": round(1e3 / ms, 3), "threads": cores,
+            "what": "torch-CPU GaussianModel getters (gaussian_model.py:146-212) over all P Gaussians"}
+
+
+def cpu_baseline(args, inputs_cpu, cam, tanx, tany, grads_cpu, raw):
+    """Time the C oracle (tests' checker) on this host's cores: full
+    per-Gaussian work and binning, every s-th tile rendered forward and
+    backward, tile time extrapolated x s; plus the torch-CPU getter leg."""
     sys.path.insert(0, ROOT)
     from oracle import gsr_oracle as O
 
-    cores = min(16, os.cpu_count() or 1)
+    cores, host = host_cores()
     O.set_threads(cores)
     tiles = ((args.width + 15) // 16) * ((args.height + 15) // 16)
     stride = args.cpu_tile_stride or 1  # default: the whole iteration, no extrapolation
@@ -142,18 +190,22 @@ def cpu_baseline(args, inputs_cpu, cam, tanx, tany, grads_cpu):
     t0 = time.time()
     o = O.forward(*a, args.height, args.width, cam.camera_center, False, geom)
     tf = O.last_times()
-    O.backward(o["state"], *a, grads_cpu["color"], grads_cpu["mdepth"], grads_cpu["alpha"], grads_cpu["normal"],
-               o["alpha"], o["normal"], o["mdepth"], cam.camera_center, o["radii"])
-    tb = O.last_times()
+    tb = dict(render_bwd=0.0, preprocess_bwd=0.0)
+    if not args.forward_only:
+        O.backward(o["state"], *a, grads_cpu["color"], grads_cpu["mdepth"], grads_cpu["alpha"], grads_cpu["normal"],
+                   o["alpha"], o["normal"], o["mdepth"], cam.camera_center, o["radii"])
+        tb = O.last_times()
     wall = time.time() - t0
     O.set_tile_stride(1)
     per_iter = tf["preprocess_binning"] + stride * tf["render"] + stride * tb["render_bwd"] + tb["preprocess_bwd"]
-    return {"value": round(1.0 / per_iter, 6), "unit": "iters/s", "cores": cores, "kind": "port",
-            "sample": (f"C oracle (oracle/gsr_oracle.c), full {args.config} scene: per-Gaussian preprocess, binning/sort and "
-                       f"per-Gaussian backward measured in full; forward+backward tile rendering on every "
-                       f"{stride}th of {tiles} tiles, extrapolated x{stride}; {wall:.1f} s wall; "
+    what = "forward" if args.forward_only else "forward+backward"
+    return {"value": round(1.0 / per_iter, 6), "unit": "iters/s", "cores": cores, "kind": "port", "host": host,
+            "sample": (f"C oracle (oracle/gsr_oracle.c, OpenMP, {cores} threads), full {args.config} scene, {what}: "
+                       f"per-Gaussian preprocess, binning/sort and per-Gaussian backward measured in full; tile "
+                       f"rendering on every {stride}th of {tiles} tiles, extrapolated x{stride}; {wall:.1f} s wall; "
                        f"split s: {tf['preprocess_binning']:.2f} pre+bin, {tf['render'] * stride:.2f} render, "
-                       f"{tb['render_bwd'] * stride:.2f} render_bwd, {tb['preprocess_bwd']:.2f} pre_bwd")}
+                       f"{tb['render_bwd'] * stride:.2f} render_bwd, {tb['preprocess_bwd']:.2f} pre_bwd"),
+            "getters": getter_baseline(raw, cores)}
 
 
 def main():
@@ -178,7 +230,9 @@ def main():
         workload = f"{tag}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), one {W}x{H} view per GPU (orbit), fwd+bwd + RCCL gradient exchange ({args.exchange})"
     else:
         cam_cpu = S.make_camera(W, H)
-        workload = f"{args.config}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), {W}x{H}, fwd+bwd"
+        what = "forward only" if args.forward_only else "fwd+bwd"
+        workload = (f"{args.config}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), {W}x{H}, {what}, "
+                    f"require_depth={geom}")
     raw = S.make_gaussians(P, sh_degree=args.sh_degree, sg_degree=args.sg_degree, aspect=H / W)
     inputs_cpu = {k: v.detach().contiguous() for k, v in S.activated_inputs(raw).items()}
     grads_cpu = S.upstream_grads(H, W)
@@ -207,6 +261,13 @@ def main():
     state = {}
 
     def step():
+        if args.forward_only:  # the forward alone: no autograd graph, nothing saved for a backward
+            with torch.no_grad():
+                state["radii"] = rasterizer(
+                    means3D=params["means3D"], means2D=means2D, opacities=params["opacities"], shs=params["shs"],
+                    sg_axis=params["sg_axis"], sg_sharpness=params["sg_sharpness"], sg_color=params["sg_color"],
+                    scales=params["scales"], rotations=params["rotations"])[1]
+            return
         for t in list(params.values()) + [means2D]:
             t.grad = None
         color, radii, mdepth, alpha, normal = rasterizer(
@@ -283,24 +344,34 @@ def main():
     if not args.all_stage_events:  # the other stages from the untimed table
         per_launch = {k: (per_launch[k] if k == dom else v) for k, v in table_ms.items()}
     achieved = algo[dom] / (per_launch[dom] * 1e-3) / 1e9
-    traffic, valu = load_pmc_traffic(dom) if args.default_workload else (None, None)
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+    traffic, valu_insts, pmc_file = load_pmc(args.workload_key, dom) if args.preset_workload else (None, None, None)
+    hbm_frac = achieved / HBM_PEAK_GBPS
+    # VALU-issue fraction of the same launch: the PMC pass's VALU instruction count for this kernel
+    # (a per-launch constant of the workload) at 4 issue cycles each, over the SIMD-cycles of the
+    # launch duration measured live here
+    valu_frac = (valu_insts * VALU_ISSUE_CYCLES / (per_launch[dom] * 1e-3 * CLOCK_HZ * SIMDS)
+                 if valu_insts else None)
+    bound = "valu" if valu_frac is not None and valu_frac > hbm_frac else "hbm"
+    roofline = {"bound": bound, "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(hbm_frac, 5),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(algo[dom]),
                 "avg_launch_ms": round(per_launch[dom], 4),
-                "stage_ms": {k: round(v, 4) for k, v in per_launch.items()},
-                "valu_busy": valu}
-    total_algo = sum(algo.values())
+                "valu": None if valu_frac is None else {
+                    "frac": round(valu_frac, 4), "insts_per_launch": int(valu_insts),
+                    "issue_cycles_per_inst": VALU_ISSUE_CYCLES, "clock_hz": CLOCK_HZ, "simds": SIMDS},
+                "pmc_source": None if pmc_file is None else f"profiles/{pmc_file}",
+                "stage_ms": {k: round(v, 4) for k, v in per_launch.items()}}
+    total_algo = sum(v for k, v in algo.items() if per_launch.get(k, 0.0) > 0.0)  # the stages this step ran
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(args, inputs_cpu, cam_cpu, tanx, tany, grads_cpu)
+            cpu = cpu_baseline(args, inputs_cpu, cam_cpu, tanx, tany, grads_cpu, raw)
         except Exception as e:  # noqa: BLE001 - report, never hide
             cpu = {"value": None, "error": repr(e)}
     if rank == 0:
         line = {
             "metric": "train iters/sec (fwd+bwd raster) at 1080p, 1M Gaussians; HBM GB/s vs peak",
-            "value": round(value, 3), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 3), "unit": "forward iters/s" if args.forward_only else "iters/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": workload, "P": P, "width": W, "height": H, "sh_degree": args.sh_degree,

@@ -24,35 +24,72 @@ thread_local std::string g_last_error;
 // rasterizer_impl.cu:384) waits on an event recorded right after the counts
 // are copied into pinned host memory, not on the whole stream: work queued
 // behind the event (the depth sort) keeps the GPU busy while the host reads
-// K and allocates.  One slot per (thread, device), created on first use and
-// kept: a thread that alternates devices never frees and re-allocates pinned
-// memory (hipHostFree / hipHostMalloc both synchronise).
+// K and allocates.  The pinned words and the event come from a process-wide
+// per-device pool: a forward leases a slot for its readback and returns it,
+// so slots are created only up to the number of concurrent forwards and are
+// reused by every thread (no per-thread slots left behind by short-lived
+// threads; no hipHostMalloc / hipHostFree, which synchronise, per call).
 struct HostReadback {
     uint32_t* pinned = nullptr;  // 8 words
     hipEvent_t ev = nullptr;
+    int dev = 0;
 };
 constexpr int kMaxReadbackDevices = 64;
-thread_local HostReadback g_readback[kMaxReadbackDevices];
 
-hipError_t readback_slot(HostReadback*& rb) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= kMaxReadbackDevices) return hipErrorInvalidDevice;
-    rb = &g_readback[dev];
-    if (rb->pinned && rb->ev) return hipSuccess;
-    if (!rb->pinned &&
-        (e = hipHostMalloc(reinterpret_cast<void**>(&rb->pinned), 8 * sizeof(uint32_t), hipHostMallocDefault)) !=
-            hipSuccess) {
-        rb->pinned = nullptr;
-        return e;
+class ReadbackPool {
+  public:
+    hipError_t acquire(HostReadback*& rb) {
+        rb = nullptr;
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        if (dev < 0 || dev >= kMaxReadbackDevices) return hipErrorInvalidDevice;
+        {
+            std::lock_guard<std::mutex> lock(m_);
+            if (!free_[dev].empty()) {
+                rb = free_[dev].back();
+                free_[dev].pop_back();
+                return hipSuccess;
+            }
+        }
+        auto* slot = new HostReadback();
+        slot->dev = dev;
+        if ((e = hipHostMalloc(reinterpret_cast<void**>(&slot->pinned), 8 * sizeof(uint32_t),
+                               hipHostMallocDefault)) != hipSuccess) {
+            delete slot;
+            return e;
+        }
+        if ((e = hipEventCreateWithFlags(&slot->ev, hipEventDisableTiming)) != hipSuccess) {
+            (void)hipHostFree(slot->pinned);
+            delete slot;
+            return e;
+        }
+        rb = slot;
+        return hipSuccess;
     }
-    if (!rb->ev && (e = hipEventCreateWithFlags(&rb->ev, hipEventDisableTiming)) != hipSuccess) {
-        rb->ev = nullptr;
-        return e;
+    void release(HostReadback* rb) {
+        std::lock_guard<std::mutex> lock(m_);
+        free_[rb->dev].push_back(rb);
     }
-    return hipSuccess;
-}
+
+  private:
+    std::mutex m_;
+    std::vector<HostReadback*> free_[kMaxReadbackDevices];
+};
+ReadbackPool g_readback_pool;
+
+// a slot leased for one forward's readback, returned on every exit path
+struct ReadbackLease {
+    HostReadback* rb = nullptr;
+    ReadbackLease() = default;
+    ReadbackLease(const ReadbackLease&) = delete;
+    ReadbackLease& operator=(const ReadbackLease&) = delete;
+    ~ReadbackLease() {
+        if (!rb) return;
+        (void)hipEventSynchronize(rb->ev);  // an error path may leave the copy in flight: drain it first
+        g_readback_pool.release(rb);
+    }
+};
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
     char buf[512];
@@ -407,6 +444,17 @@ int gsr_debug_sample_points(const void* point_buffer, int PN, float* median_dept
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "debug sample points", e);
 }
 
+int gsr_debug_image(const void* image_buffer, int width, int height, uint32_t* n_contrib_out, void* stream_ptr) {
+    if (!image_buffer || width <= 0 || height <= 0 || !n_contrib_out) return fail(GSR_ERR_ARGS, "invalid arguments");
+    ImageState is;
+    carve_image(aligned_base(const_cast<void*>(image_buffer)), width * height, is);
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    hipError_t e = hipMemcpyAsync(n_contrib_out, is.n_contrib, sizeof(uint32_t) * (size_t)width * height,
+                                  hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "debug image", e);
+}
+
 int gsr_set_option(int opt, int value) {
     if (opt < 0 || opt >= gsr::kNumOptions) return fail(GSR_ERR_ARGS, "unknown option");
     gsr::g_options[opt] = value;
@@ -414,7 +462,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 11; }
+int gsr_abi_version(void) { return 12; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -532,8 +580,9 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
     uint2 Ks = make_uint2(0u, 0u);
     if (path != kBinInstanceSort) {
         // K depends on preprocess only: one readback
-        HostReadback* rb = nullptr;
-        GSR_TRY(readback_slot(rb), "pinned readback buffer");
+        ReadbackLease lease;
+        GSR_TRY(g_readback_pool.acquire(lease.rb), "pinned readback buffer");
+        HostReadback* rb = lease.rb;
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_k_hist(gs, P, path == kBinLists, stream), "count K");
         GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
         if (prefiltered)
@@ -766,8 +815,9 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     if (path != kBinInstanceSort) {
         // K, the tile list sizes and the point totals depend on preprocess and
         // the points only: one readback (HostReadback)
-        HostReadback* rb = nullptr;
-        GSR_TRY(readback_slot(rb), "pinned readback buffer");
+        ReadbackLease lease;
+        GSR_TRY(g_readback_pool.acquire(lease.rb), "pinned readback buffer");
+        HostReadback* rb = lease.rb;
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_k_hist(gs, P, path == kBinLists, stream), "count K");
         GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_points(p, PN, points3D, ps, pb, st, stream), "sample points");
         GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_setup(PN, tiles, pb, st, stream), "sample setup");

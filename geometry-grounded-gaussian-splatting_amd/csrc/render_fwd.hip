@@ -47,6 +47,9 @@ constexpr int kResident = GSR_RESIDENT;  // LDS-resident contributing prefix (C3
 constexpr int kMaskWords = kResident / 32;
 constexpr int kBatch = GSR_BATCH;        // records per composite staging batch
 constexpr int kRecSlots = 3 * kResident > 4 * kBatch ? 3 * kResident : 4 * kBatch;
+// the non-resident median-depth path stages kTilePixels-record chunks at offsets 0, kResident and
+// 2 kResident of s_rec: a resident cache smaller than a chunk would overlap them and overrun s_rec
+static_assert(kResident >= kTilePixels, "GSR_RESIDENT must be >= kTilePixels (256)");
 
 struct RenderFwdArgs {
     const uint2* ranges;

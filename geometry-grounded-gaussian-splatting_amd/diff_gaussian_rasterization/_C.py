@@ -43,7 +43,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 def _load():
@@ -92,6 +92,7 @@ def _load():
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     L.gsr_set_option.argtypes = [i, i]
     L.gsr_debug_binning.argtypes = [vp, vp, i, i, i, vp, vp, vp]
+    L.gsr_debug_image.argtypes = [vp, i, i, vp, vp]
     L.gsr_debug_sample_points.argtypes = [vp, i, vp, vp, vp]
     L.gsr_debug_render_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i]
     L.gsr_timing_enable.argtypes = [i]
@@ -149,6 +150,19 @@ def debug_binning(binningBuffer, tileBuffer, R: int, image_height: int, image_wi
                                      int(image_height), plist.ctypes.data_as(ctypes.c_void_p) if with_list else None,
                                      ranges.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream)))
     return plist, ranges
+
+
+def debug_n_contrib(imgBuffer, image_height: int, image_width: int):
+    """Per-pixel last contributor [H, W] uint32 of a forward's image buffer
+    (gsr_debug_image): 1-based positions in the culled per-tile lists of
+    debug_binning."""
+    import numpy as np
+
+    out = np.zeros((image_height, image_width), np.uint32)
+    stream = torch.cuda.current_stream(imgBuffer.device).cuda_stream
+    _check(_load().gsr_debug_image(ctypes.c_void_p(imgBuffer.data_ptr()), int(image_width), int(image_height),
+                                   out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream)))
+    return out
 
 
 def debug_sample_points(pointBuffer, PN: int):
@@ -557,8 +571,21 @@ def view_color_grads(gathered, n_views: int, means3D, sh_degree: int, dL_dsh, sg
     for t, name in need:
         if t is None or not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
             raise RuntimeError(f"gsr view_color_grads: `{name}` must be a contiguous fp32 HIP tensor")
-    if gathered.numel() != n_views * (3 * P + 4) or dL_dsh.shape[0] != P:
-        raise RuntimeError("gsr view_color_grads: shape mismatch")
+    if gathered.numel() != n_views * (3 * P + 4):
+        raise RuntimeError("gsr view_color_grads: `gathered` must hold n_views * (3 P + 4) floats")
+    want = {"means3D": (means3D, (P, 3)), "dL_dsh": (dL_dsh, (P, SHM, 3))}
+    if SGM:
+        want.update(dL_dsg_axis=(dL_dsg_axis, (P, SGM, 3)), dL_dsg_sharpness=(dL_dsg_sharpness, (P, SGM)),
+                    dL_dsg_color=(dL_dsg_color, (P, SGM, 3)))
+    if sg_degree:
+        want.update(sg_axis=(sg_axis, (P, SGM, 3)), sg_sharpness=(sg_sharpness, (P, SGM)),
+                    sg_color=(sg_color, (P, SGM, 3)))
+    for name, (t, shape) in want.items():
+        if tuple(t.shape) != shape:
+            raise RuntimeError(f"gsr view_color_grads: `{name}` has shape {tuple(t.shape)}, expected {shape}")
+    if not 0 <= int(sh_degree) <= 3 or SHM < (int(sh_degree) + 1) ** 2 or not 0 <= int(sg_degree) <= SGM:
+        raise RuntimeError(f"gsr view_color_grads: degrees (SH {sh_degree}, SG {sg_degree}) do not fit "
+                           f"{SHM} SH rows and {SGM} SG lobes")
     dev = means3D.device
     p = lambda t: _ptr(t) if t is not None and t.numel() else None  # noqa: E731
     with torch.cuda.device(dev):

@@ -22,6 +22,15 @@ import torch.nn as nn
 
 from . import _C
 
+# Rasterizer colour backwards (SH path) run in this process; gsr_dist.FactoredViewGrads
+# checks that exactly one ran between two gradient exchanges (its contract).
+_colour_backward_calls = 0
+
+
+def colour_backward_count() -> int:
+    """Number of _RasterizeGaussians backwards that produced SH gradients."""
+    return _colour_backward_calls
+
 
 def cpu_deep_copy_tuple(input_tuple):
     copied_tensors = [item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple]
@@ -67,6 +76,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_color, grad_radii, grad_mdepth, grad_alpha, grad_normal):
+        global _colour_backward_calls
         num_rendered = ctx.num_rendered
         s = ctx.raster_settings
         (means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis, sg_sharpness, sg_color,
@@ -88,6 +98,8 @@ class _RasterizeGaussians(torch.autograd.Function):
             g = _C.rasterize_gaussians_backward(*args)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
          grad_sg_axis, grad_sg_sharpness, grad_sg_color, grad_scales, grad_rotations) = g
+        if sh.numel():
+            _colour_backward_calls += 1
         return (grad_means3D, grad_means2D, grad_sh, grad_sg_axis, grad_sg_sharpness, grad_sg_color,
                 grad_colors_precomp, grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None)
 

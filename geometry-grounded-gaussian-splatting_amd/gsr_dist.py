@@ -158,24 +158,70 @@ class FactoredViewGrads:
     dL/dshs).  SG tensors must be the rasterizer inputs (the SG activations
     are not linear in the rows, so raw SG parameters go in `extra`, which is
     all-reduced with the geometry rows).
+
+    Contract: between two exchanges this rank's SH / SG gradients come from
+    exactly ONE rasterizer colour backward for the camera `campos` names —
+    no accumulation over several renders, no gradients left over from a
+    missing zero_grad, and no other loss or regularizer on the SH / SG rows.
+    The rows are rebuilt from the DC row, so anything else that wrote into
+    them would be silently replaced.  Two guards:
+      * `guard` (default on with the HIP kernel): raise unless exactly one
+        rasterizer SH backward ran since the previous exchange (a counter in
+        diff_gaussian_rasterization; catches several renders per step);
+      * `verify` (opt-in, one extra kernel per exchange): rebuild this rank's
+        own rows from its own DC row and raise unless they equal the rows in
+        .grad (catches stale gradients and extra SH / SG losses too).
     """
 
     def __init__(self, means3D: torch.Tensor, opacities: torch.Tensor, scales: torch.Tensor,
                  rotations: torch.Tensor, shs, sg_axis: Optional[torch.Tensor] = None,
                  sg_sharpness: Optional[torch.Tensor] = None, sg_color: Optional[torch.Tensor] = None,
-                 group: Optional[dist.ProcessGroup] = None, expand=None, extra: Iterable[torch.Tensor] = ()):
+                 group: Optional[dist.ProcessGroup] = None, expand=None, extra: Iterable[torch.Tensor] = (),
+                 guard: Optional[bool] = None, verify: bool = False):
         self.means3D = means3D
         self.split = isinstance(shs, (tuple, list))
         self.shs = tuple(shs) if self.split else shs
         self.sg = [t if t is not None and t.numel() else None for t in (sg_axis, sg_sharpness, sg_color)]
         self.group = group
         self.geometry = ViewParallelGrads([means3D, opacities, scales, rotations, *extra], group=group)
+        self.guard = (expand is None) if guard is None else guard
+        self.verify = verify
         if expand is None:
             from diff_gaussian_rasterization import _C
             expand = _C.view_color_grads
         self.expand = expand
         self._buf = None
         self._gathered = None
+        self._calls = self._backward_count() if self.guard else 0
+
+    @staticmethod
+    def _backward_count() -> int:
+        import diff_gaussian_rasterization as dgr
+        return dgr.colour_backward_count()
+
+    def _check_contract(self, sh_degree: int, sg_degree: int) -> None:
+        if self.guard:
+            n = self._backward_count()
+            ran, self._calls = n - self._calls, n
+            if ran != 1:
+                raise RuntimeError(f"FactoredViewGrads: {ran} rasterizer SH backwards since the last exchange; the "
+                                   "factored exchange needs exactly one per step (use ViewParallelGrads otherwise)")
+        if not self.verify:
+            return
+        mine = torch.cat([t.grad for t in self.shs], 1) if self.split else self.shs.grad
+        rows = torch.empty_like(mine)
+        sgo = [None if t is None else torch.empty_like(t) for t in self.sg]
+        self.expand(self._buf, 1, self.means3D.detach(), sh_degree, rows, sg_degree,
+                    *[None if t is None else t.detach() for t in self.sg], *sgo)
+        pairs = [("sh", mine, rows)]
+        for name, t, o in zip(("sg_axis", "sg_sharpness", "sg_color"), self.sg, sgo):
+            if t is not None:
+                pairs.append((name, torch.zeros_like(t) if t.grad is None else t.grad, o))
+        for name, want, got in pairs:
+            tol = 1e-5 * max(float(want.abs().max()), 1e-30) if want.numel() else 0.0
+            if want.numel() and float((want - got).abs().max()) > tol:
+                raise RuntimeError(f"FactoredViewGrads(verify): this rank's {name} gradient rows are not those of "
+                                   "its one rasterizer backward (stale .grad or another loss on them?)")
 
     def exchange(self, campos: torch.Tensor, sh_degree: int, sg_degree: int = 0) -> None:
         world = dist.get_world_size(self.group)
@@ -191,6 +237,7 @@ class FactoredViewGrads:
         dc = self.shs[0].grad if self.split else self.shs.grad
         self._buf[:3 * P].view(P, 3).copy_(dc[:, 0, :])
         self._buf[3 * P:3 * P + 3].copy_(campos.reshape(3))
+        self._check_contract(sh_degree, sg_degree)
         work = dist.all_gather_into_tensor(self._gathered, self._buf, group=self.group, async_op=True)
         self.geometry.all_reduce()
         work.wait()

@@ -179,8 +179,12 @@ def compute_filter_3D(xyz: torch.Tensor, cameras) -> torch.Tensor:
 
 def make_gaussians(P: int, sh_degree: int = 3, sg_degree: int = 0, seed: int = 0, fovx_deg: float = 60.0,
                    aspect: float = 1080 / 1920, z_range=(2.0, 10.0), log_scale_mean: float = math.log(0.02),
-                   log_scale_std: float = 0.5, opacity_std: float = 1.5) -> RawGaussians:
-    """SURVEY §8(d) synthetic scene (seed 0 by default)."""
+                   log_scale_std: float = 0.5, opacity_std: float = 1.5,
+                   sh_max_degree: int | None = None) -> RawGaussians:
+    """SURVEY §8(d) synthetic scene (seed 0 by default).  `sh_max_degree`
+    sizes the SH rows as GaussianModel does ((max_sh_degree + 1)^2 rows,
+    gaussian_model.py:264-266) while `sh_degree` is the active degree: the
+    reference's SH warm-up (train.py:130) renders 16-row SH at degree 0..3."""
     g = torch.Generator().manual_seed(seed)
     tanx = math.tan(math.radians(fovx_deg) / 2)
     tany = tanx * aspect
@@ -188,7 +192,7 @@ def make_gaussians(P: int, sh_degree: int = 3, sg_degree: int = 0, seed: int = 0
     u = torch.empty(P).uniform_(-1, 1, generator=g)
     v = torch.empty(P).uniform_(-1, 1, generator=g)
     xyz = torch.stack([u * z * 1.1 * tanx, v * z * 1.1 * tany, z], 1)
-    shm = (sh_degree + 1) ** 2
+    shm = ((sh_degree if sh_max_degree is None else sh_max_degree) + 1) ** 2
     dc = torch.randn(P, 1, 3, generator=g) * 0.5
     rest = torch.randn(P, shm - 1, 3, generator=g) * 0.05
     scaling = torch.randn(P, 3, generator=g) * log_scale_std + log_scale_mean

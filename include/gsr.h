@@ -430,6 +430,14 @@ int gsr_debug_binning(const void* binning_buffer, const void* tile_buffer, int R
                       uint32_t* point_list_out, uint32_t* ranges_out, void* stream);
 
 /*
+ * Introspection of a forward's image buffer (test hook): the per-pixel last
+ * contributor (1-based index into the pixel's tile list, which holds only the
+ * instances that survive tile culling, see gsr_debug_binning), W x H uint32
+ * row-major; synchronises `stream`.
+ */
+int gsr_debug_image(const void* image_buffer, int width, int height, uint32_t* n_contrib_out, void* stream);
+
+/*
  * Introspection of a sample_depth forward's point buffer (test hook): the
  * per-point median depth along the ray and last contributor (index into the
  * culled per-tile list) for PN points; synchronises `stream`.

@@ -67,6 +67,8 @@ def lib():
         L.gsro_get_binning.argtypes = [ctypes.c_void_p, _u64, _u32]
         L.gsro_get_tiles.argtypes = [ctypes.c_void_p, _u32, _u32]
         L.gsro_get_n_contrib.argtypes = [ctypes.c_void_p, _u32]
+        L.gsro_set_n_contrib.argtypes = [ctypes.c_void_p, _u32]
+        L.gsro_set_exp_mode.argtypes = [ctypes.c_int]
         L.gsro_get_bwd_accum.argtypes = [ctypes.c_void_p, _d, _d, _d]
         L.gsro_sample_forward.restype = ctypes.c_void_p
         L.gsro_sample_forward.argtypes = ([ctypes.c_int] * 4 + [_f] * 4 + [ctypes.c_float] + [_f] * 5
@@ -92,6 +94,12 @@ def lib():
 
 def set_threads(n: int) -> None:
     lib().gsro_set_threads(int(n))
+
+
+def set_exp_mode(mode: int) -> None:
+    """0: libm expf (default); 1: exp2f(x * log2e) in fp32, the form the
+    reference's --use_fast_math build compiles expf to (gsr_oracle.c header)."""
+    lib().gsro_set_exp_mode(int(mode))
 
 
 def set_tile_stride(n: int) -> None:
@@ -166,6 +174,13 @@ class State:
         n = np.zeros(self.W * self.H, np.uint32)
         lib().gsro_get_n_contrib(self.ptr, _p(n, _u32))
         return n.reshape(self.H, self.W)
+
+    def set_n_contrib(self, n_contrib) -> None:
+        """Make the backward run with these per-pixel last contributors
+        (positions in THIS state's per-tile lists; per-tile max recomputed)."""
+        n = np.ascontiguousarray(np.asarray(n_contrib, np.uint32).reshape(-1))
+        assert n.size == self.W * self.H
+        lib().gsro_set_n_contrib(self.ptr, _p(n, _u32))
 
     def bwd_accum(self) -> dict:
         P = self.P

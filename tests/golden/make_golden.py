@@ -21,6 +21,12 @@ reference's CUDA rasterizer, which cannot build in this image):
   boundary_query.json   DGR/diff_gaussian_rasterization/__init__.py:338-468 —
                    the same for GaussianRasterizer.integrate / evaluate_sdf
                    (_C.integrate_gaussians_to_points, _C.evaluate_sdf_from_signle_view).
+  losses.npz       utils/loss_utils.py:36-72 create_window / _ssim (the SSIM
+                   map the reference defines, captured from inside _ssim; its
+                   mean in "same" padding and cropped by 5 for "valid", the
+                   mode loss_utils.ssim asks fused_ssim for, :48-49) and
+                   utils/graphics_utils.py:103-119 depth_to_normal, with the
+                   reference's own fp32 torch autograd gradients (CPU).
 """
 from __future__ import annotations
 
@@ -296,6 +302,71 @@ def boundary_fixture():
         json.dump(qcalls, f, indent=1)
 
 
+def loss_fixture(rng):
+    """SSIM and depth->normal from the reference's own functions (fp32 torch, CPU)."""
+    scene = sys.modules["scene"]
+    scene.GaussianModel, scene.Camera = object, object  # `from scene import GaussianModel, Camera`
+    _stub("fused_ssim", fused_ssim=lambda *a, **k: None)
+    _stub("warp_patch_ncc")
+    _stub("gaussian_renderer", sample_depth=lambda *a, **k: None, render=lambda *a, **k: None)
+    lu = importlib.import_module("utils.loss_utils")
+    gu = importlib.import_module("utils.graphics_utils")
+    out = {}
+    for i, (n, c, h, w) in enumerate([(1, 3, 37, 53), (1, 3, 64, 80), (2, 1, 17, 11)]):
+        a = rng.random((n, c, h, w)).astype(np.float32)
+        b = np.clip(a + 0.1 * rng.standard_normal(a.shape), 0, 1).astype(np.float32)
+        maps = []
+        real_mean = torch.Tensor.mean
+
+        def capture(self, *args, **kw):  # the first .mean() of _ssim is ssim_map.mean()
+            if not maps and not args and not kw:
+                maps.append(self)
+            return real_mean(self, *args, **kw)
+
+        x = torch.tensor(a, requires_grad=True)
+        torch.Tensor.mean = capture
+        try:
+            same = lu._ssim(x, torch.tensor(b), lu.create_window(11, c), 11, c)
+        finally:
+            torch.Tensor.mean = real_mean
+        (g_same,) = torch.autograd.grad(same, x, retain_graph=True)
+        valid = maps[0][:, :, 5:-5, 5:-5].mean()
+        (g_valid,) = torch.autograd.grad(valid, x)
+        out.update({f"ssim_img1_{i}": a, f"ssim_img2_{i}": b, f"ssim_same_{i}": same.detach().numpy(),
+                    f"ssim_same_grad_{i}": g_same.numpy(), f"ssim_valid_{i}": valid.detach().numpy(),
+                    f"ssim_valid_grad_{i}": g_valid.numpy()})
+
+    real_arange = torch.arange
+
+    def arange_cpu(*args, **kw):  # depth_to_normal builds its pixel grid on "cuda"
+        kw.pop("device", None)
+        return real_arange(*args, **kw)
+
+    class _View:
+        def __init__(self, W, H):
+            self.image_width, self.image_height = W, H
+            self.Fx, self.Fy, self.Cx, self.Cy = 0.9 * W, 0.85 * W, W / 2 - 0.5, H / 2 + 0.25
+
+    for i, (W, H) in enumerate([(40, 30), (64, 48)]):
+        base = torch.tensor(rng.random((1, 1, H // 8 + 2, W // 8 + 2)).astype(np.float32)) * 3 + 2
+        depth = torch.nn.functional.interpolate(base, size=(H, W), mode="bicubic", align_corners=True)[0]
+        depth[:, : H // 7, : W // 5] = 0.0  # holes (median depth 0 where undefined)
+        depth = depth.contiguous()
+        v = _View(W, H)
+        d = depth.clone().requires_grad_(True)
+        torch.arange = arange_cpu
+        try:
+            normal, valid = gu.depth_to_normal(v, d)
+        finally:
+            torch.arange = real_arange
+        gn = torch.tensor(rng.standard_normal((3, H, W)).astype(np.float32)) * valid
+        (normal * gn).sum().backward()
+        out.update({f"dn_depth_{i}": depth.numpy(), f"dn_view_{i}": np.array([W, H, v.Fx, v.Fy, v.Cx, v.Cy]),
+                    f"dn_normal_{i}": normal.detach().numpy(), f"dn_valid_{i}": valid.numpy(),
+                    f"dn_upstream_{i}": gn.numpy(), f"dn_grad_{i}": d.grad.numpy()})
+    np.savez(os.path.join(OUT, "losses.npz"), **out)
+
+
 def main():
     _install_stubs()
     rng = np.random.default_rng(1234)
@@ -303,6 +374,7 @@ def main():
     camera_fixture(rng)
     getters_fixture(rng)
     boundary_fixture()
+    loss_fixture(np.random.default_rng(4321))
     print("wrote", sorted(os.listdir(OUT)))
 
 

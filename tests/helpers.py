@@ -11,15 +11,19 @@ import gsr_scene as S
 
 def small_case(P=40, W=40, H=24, seed=0, sh_degree=3, sg_degree=0, sgm=None, log_scale=math.log(0.12),
                opacity_max_logit=2.0, z_range=(2.0, 4.0), kernel_size=0.0, require_depth=True, cam=None,
-               bg=(0.0, 0.0, 0.0), flat=1.0):
+               bg=(0.0, 0.0, 0.0), flat=1.0, opacity_std=1.0, sh_max_degree=None):
     """A small random scene plus every argument of _C.rasterize_gaussians.
 
-    Opacity logits are capped (sigmoid(2) = 0.88) so o*G < 0.99 and the
-    reference's pass-through gradient of the 0.99 clamp never matters."""
+    Opacity logits are capped at `opacity_max_logit` (default 2: sigmoid(2) =
+    0.88, so o*G < 0.99); the clamp cases raise the cap (logit 6: o = 0.9975)
+    so alpha = min(0.99, o*G) clamps and the reference's pass-through gradient
+    of the clamp (render_backward.cu:931-933, 1012) is exercised.
+    `sh_max_degree` > `sh_degree` gives the SH warm-up layout: 16 SH rows
+    rendered at a lower active degree (train.py:130)."""
     cam = cam or S.make_camera(W, H)
     raw = S.make_gaussians(P, sh_degree=sh_degree, sg_degree=sgm if sgm is not None else sg_degree, seed=seed,
                            aspect=H / W, z_range=z_range, log_scale_mean=log_scale, log_scale_std=0.3,
-                           opacity_std=1.0)
+                           opacity_std=opacity_std, sh_max_degree=sh_max_degree)
     raw.opacity.clamp_(max=opacity_max_logit)
     if flat != 1.0:  # surfel-like Gaussians: one axis `flat` times thinner (steep vacancy steps)
         raw.scaling[:, 2] -= math.log(flat)
@@ -55,3 +59,35 @@ def frac_bad(a, b, rtol, atol) -> float:
     if a.size == 0:
         return 0.0
     return float(np.mean(np.abs(a - b) > atol + rtol * np.abs(b)))
+
+
+def gpu_n_contrib_for_oracle(out, o, H, W):
+    """The GPU forward's per-pixel last contributors as positions in the
+    oracle's per-tile lists.  The GPU lists are the oracle's (the reference's)
+    minus the tile-culled instances, in the same order, so the
+    last contributor's Gaussian is looked up in the oracle's list of its tile.
+    With it (State.set_n_contrib) the oracle backward runs on exactly the GPU
+    forward's state: its images and its contributor ranges."""
+    from diff_gaussian_rasterization import _C
+
+    plist, ranges = _C.debug_binning(out[7], out[9], out[0], H, W)
+    last = _C.debug_n_contrib(out[8], H, W).astype(np.int64)
+    ob = o["state"].binning()["point_list"].astype(np.int64)
+    orng = o["state"].tile_state()["ranges"].astype(np.int64)
+    gx = (W + 15) // 16
+    ys, xs = np.mgrid[0:H, 0:W]
+    tile = (ys // 16) * gx + (xs // 16)
+    res = np.zeros((H, W), np.int64)
+    has = last > 0
+    g = plist.astype(np.int64)[ranges[tile[has], 0].astype(np.int64) + last[has] - 1]
+    # per tile, the oracle positions of its Gaussians: search (tile, gaussian) keys in the oracle's list,
+    # which is sorted per tile by depth, not id, so look up through a sorted copy
+    otile = np.repeat(np.arange(orng.shape[0], dtype=np.int64), orng[:, 1] - orng[:, 0])
+    okey = (otile << 32) | ob[np.concatenate([np.arange(a, b) for a, b in orng]) if len(ob) else np.zeros(0, np.int64)]
+    opos = np.concatenate([np.arange(b - a) for a, b in orng]) if len(ob) else np.zeros(0, np.int64)
+    srt = np.argsort(okey, kind="stable")
+    want = (tile[has].astype(np.int64) << 32) | g
+    at = np.searchsorted(okey[srt], want)
+    assert np.array_equal(okey[srt][at], want), "GPU contributor missing from the oracle's tile list"
+    res[has] = opos[srt][at] + 1
+    return res.astype(np.uint32)

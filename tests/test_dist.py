@@ -145,8 +145,21 @@ def _factored_worker(rank, world, port, outdir):
     for k in names:
         ps[k].grad = inp[k].grad.float().clone()
     campos = S.orbit_cameras(2, 32, 24, center_z=3.0, max_deg=10.0)[rank].camera_center.float()
+    # the contract guards (gsr_dist.FactoredViewGrads docstring), checked on both ranks before any collective:
+    # no rasterizer backward ran in this process -> the backward-count guard refuses the exchange
+    import pytest
+    with pytest.raises(RuntimeError, match="rasterizer SH backwards"):
+        FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"],
+                          expand=_expand_ref, guard=True).exchange(campos, sh_degree=3)
+    # an extra contribution to the SH rest rows (a stale .grad / another loss) -> verify refuses it
+    stale = ps["shs"].detach().clone().requires_grad_(True)
+    stale.grad = ps["shs"].grad.clone()
+    stale.grad[:, 5] += 1e-3
+    with pytest.raises(RuntimeError, match="verify"):
+        FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], stale,
+                          expand=_expand_ref, verify=True).exchange(campos, sh_degree=3)
     ex = FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"],
-                           expand=_expand_ref)
+                           expand=_expand_ref, verify=True)
     # the reference's split SH parameters (features_dc, features_rest) before the exchange above overwrites shs.grad
     dc = ps["shs"][:, :1].detach().clone().requires_grad_(True)
     rest = ps["shs"][:, 1:].detach().clone().requires_grad_(True)

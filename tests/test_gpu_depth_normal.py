@@ -54,3 +54,27 @@ def test_depth_to_normal_matches_reference(W, H):
     err = float((d.grad.cpu().double() - d64.grad).norm() / d64.grad.norm())
     err32 = float((d32.grad.double() - d64.grad).norm() / d64.grad.norm())
     assert err <= max(2 * err32, 1e-5), (err, err32)
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_depth_to_normal_matches_reference_fixture(i):
+    """Against utils/graphics_utils.py:103-119 run by the reference itself
+    (fp32 torch, tests/golden/make_golden.py): valid exact, normals within
+    1e-5, the gradient of <normal, upstream> within 1e-5 relative L2."""
+    import os
+
+    import numpy as np
+
+    import gsr_geometry as G
+
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "losses.npz"))
+    W, H, Fx, Fy, Cx, Cy = d[f"dn_view_{i}"]
+    view = View(int(W), int(H))
+    view.Fx, view.Fy, view.Cx, view.Cy = float(Fx), float(Fy), float(Cx), float(Cy)
+    depth = torch.tensor(d[f"dn_depth_{i}"], device=DEV).requires_grad_(True)
+    n, valid = G.depth_to_normal(view, depth)
+    (n * torch.tensor(d[f"dn_upstream_{i}"], device=DEV)).sum().backward()
+    assert np.array_equal(valid.cpu().numpy(), d[f"dn_valid_{i}"])
+    assert np.abs(n.detach().cpu().numpy() - d[f"dn_normal_{i}"]).max() <= 1e-5
+    g = d[f"dn_grad_{i}"].astype(np.float64)
+    assert np.linalg.norm(depth.grad.cpu().double().numpy() - g) / np.linalg.norm(g) <= 1e-5

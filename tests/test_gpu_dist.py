@@ -129,13 +129,65 @@ def test_rccl_factored_exchange_one_rank(tmp_path):
         ps = {k: t.clone().requires_grad_(True) for k, t in inp.items()}
         for k in ps:
             ps[k].grad = per_view[0][k].clone()
+        # (the backward ran before this exchanger existed: its count guard is off, its verify check on)
         ex = FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"],
-                               ps["sg_axis"], ps["sg_sharpness"], ps["sg_color"])
+                               ps["sg_axis"], ps["sg_sharpness"], ps["sg_color"], guard=False, verify=True)
         ex.exchange(campos[0], 3, 7)
         torch.cuda.synchronize()
         for k in ps:
             want, got = per_view[0][k].double(), ps[k].grad.double()
             err = float((got - want).norm() / want.norm().clamp_min(1e-30))
             assert err <= 1e-5, (k, err)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_factored_exchange_contract_guards(tmp_path):
+    """FactoredViewGrads refuses a step whose SH rows are not those of
+    exactly one rasterizer backward: two renders per step (the backward-count
+    guard, on by default) and an extra SH-row gradient (verify)."""
+    import math
+
+    import gsr_scene as S
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gsr_dist import FactoredViewGrads
+
+    dev = torch.device("cuda", 0)
+    P, W, H = 4000, 128, 96
+    raw = S.make_gaussians(P, seed=3, aspect=H / W, z_range=(2.0, 6.0))
+    ps = {k: v.detach().contiguous().to(dev).requires_grad_(True) for k, v in S.activated_inputs(raw).items()}
+    cam = S.make_camera(W, H).to(dev)
+    settings = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2),
+        kernel_size=0.0, bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam.world_view_transform,
+        projmatrix=cam.full_proj_transform, sh_degree=3, sg_degree=0, campos=cam.camera_center, prefiltered=False,
+        require_depth=True, debug=False)
+
+    def render_backward():
+        color = GaussianRasterizer(settings)(
+            means3D=ps["means3D"], means2D=torch.zeros(P, 3, device=dev, requires_grad=True),
+            opacities=ps["opacities"], shs=ps["shs"], sg_axis=ps["sg_axis"], sg_sharpness=ps["sg_sharpness"],
+            sg_color=ps["sg_color"], scales=ps["scales"], rotations=ps["rotations"])[0]
+        color.square().sum().backward()
+
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        ex = FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"],
+                               verify=True)
+        render_backward()
+        ex.exchange(cam.camera_center, 3)  # one render: accepted
+        for t in ps.values():
+            t.grad = None
+        render_backward()
+        render_backward()
+        with pytest.raises(RuntimeError, match="2 rasterizer SH backwards"):
+            ex.exchange(cam.camera_center, 3)
+        for t in ps.values():
+            t.grad = None
+        render_backward()
+        ps["shs"].grad[:, 4] += 1e-3  # another loss on the SH rest rows
+        with pytest.raises(RuntimeError, match="verify"):
+            ex.exchange(cam.camera_center, 3)
     finally:
         dist.destroy_process_group()

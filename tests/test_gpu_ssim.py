@@ -42,6 +42,27 @@ def test_fused_ssim_matches_reference(shape, padding):
     assert err <= 1e-5, err
 
 
+@pytest.mark.parametrize("i", [0, 1, 2])
+@pytest.mark.parametrize("padding", ["same", "valid"])
+def test_fused_ssim_matches_reference_fixture(i, padding):
+    """Against the reference's own _ssim (utils/loss_utils.py:36-72, run in
+    fp32 torch by tests/golden/make_golden.py): mean within 1e-6, dSSIM/dimg1
+    within 1e-5 relative L2."""
+    import os
+
+    import numpy as np
+
+    import fused_ssim as FS
+
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "losses.npz"))
+    x = torch.tensor(d[f"ssim_img1_{i}"], device=DEV).requires_grad_(True)
+    v = FS.fused_ssim(x, torch.tensor(d[f"ssim_img2_{i}"], device=DEV), padding=padding)
+    v.backward()
+    want, g = float(d[f"ssim_{padding}_{i}"]), d[f"ssim_{padding}_grad_{i}"].astype(np.float64)
+    assert abs(v.item() - want) <= 1e-6, (v.item(), want)
+    assert np.linalg.norm(x.grad.cpu().double().numpy() - g) / np.linalg.norm(g) <= 1e-5
+
+
 def test_fused_ssim_loss_term_and_no_grad():
     """1 - ssim(...) as train.py:189 uses it; train=False gives the value only."""
     import fused_ssim as FS

@@ -100,6 +100,12 @@ CASES = [
     dict(P=50, W=37, H=29, seed=5, sgm=2, sg_degree=2),
     dict(P=45, W=40, H=24, seed=7, require_depth=False),
     dict(P=45, W=40, H=24, seed=9, bg=(0.2, 0.5, 1.0)),
+    # the alpha = 0.99 clamp (logits up to 6: o up to 0.9975) with its pass-through gradient
+    dict(P=60, W=40, H=32, seed=40, opacity_max_logit=6.0, opacity_std=3.0),
+    # the SH warm-up layout (train.py:130): 16 SH rows rendered at active degree 0, 1, 2
+    dict(P=45, W=40, H=24, seed=41, sh_degree=0, sh_max_degree=3),
+    dict(P=45, W=40, H=24, seed=42, sh_degree=1, sh_max_degree=3),
+    dict(P=45, W=40, H=24, seed=43, sh_degree=2, sh_max_degree=3),
 ]
 
 
@@ -141,6 +147,11 @@ def test_oracle_matches_float64_autograd(case):
                       dsg_color=(b["dsg_color"], inp["sg_color"].grad.numpy()))
     for k, (mine, ref) in checks.items():
         assert Hh.rel_err(mine, ref) < 2e-4, (k, Hh.rel_err(mine, ref))
+    if case.get("opacity_max_logit", 2.0) > 4.6:  # the case must reach the clamp
+        assert int((c["inp"]["opacities"] > 0.99).sum()) > 0
+    if case.get("sh_max_degree"):  # rows past the active degree get exactly zero
+        n = (c["sh_degree"] + 1) ** 2
+        assert not np.any(b["dsh"][:, n:]) and b["dsh"].shape[1] == 16
 
 
 def test_oracle_colors_precomp_path():
@@ -600,3 +611,45 @@ def test_warp_patch_ncc_matches_float64_autograd(seed):
     ncc.sum().backward()
     assert Hh.rel_err(o["grad_depths"], dd.grad.numpy()) < 1e-3
     assert Hh.rel_err(o["grad_normals"], nd.grad.numpy()) < 1e-3
+
+
+# ------------------------------------- loss restatements vs the reference's own Python
+def _losses():
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "losses.npz"))
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+@pytest.mark.parametrize("padding", ["same", "valid"])
+def test_ssim_ref_matches_reference_fixture(i, padding):
+    """oracle/ssim_ref.ssim (float64) against utils/loss_utils.py:36-72 _ssim
+    run by the reference itself (fp32 torch; "valid" = its SSIM map cropped
+    by 5): mean within 1e-6, dSSIM/dimg1 within 1e-5 relative L2."""
+    from oracle import ssim_ref
+
+    d = _losses()
+    a = torch.tensor(d[f"ssim_img1_{i}"]).double().requires_grad_(True)
+    b = torch.tensor(d[f"ssim_img2_{i}"]).double()
+    v = ssim_ref.ssim(a, b, padding=padding)
+    v.backward()
+    want, gwant = float(d[f"ssim_{padding}_{i}"]), d[f"ssim_{padding}_grad_{i}"].astype(np.float64)
+    assert abs(v.item() - want) <= 1e-6, (v.item(), want)
+    assert np.linalg.norm(a.grad.numpy() - gwant) / np.linalg.norm(gwant) <= 1e-5
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_depth_to_normal_ref_matches_reference_fixture(i):
+    """oracle/ssim_ref.depth_to_normal against utils/graphics_utils.py:103-119
+    run by the reference itself: valid exact, normals within 1e-5, the
+    gradient of <normal, upstream> within 1e-5 relative L2 (the reference
+    computes in fp32, the restatement here in float64)."""
+    from oracle import ssim_ref
+
+    d = _losses()
+    W, H, Fx, Fy, Cx, Cy = d[f"dn_view_{i}"]
+    depth = torch.tensor(d[f"dn_depth_{i}"]).double().requires_grad_(True)
+    n, valid = ssim_ref.depth_to_normal(depth, Fx, Fy, Cx, Cy)
+    (n * torch.tensor(d[f"dn_upstream_{i}"]).double()).sum().backward()
+    assert np.array_equal(valid.numpy(), d[f"dn_valid_{i}"])
+    assert np.abs(n.detach().numpy() - d[f"dn_normal_{i}"]).max() <= 1e-5
+    g = d[f"dn_grad_{i}"].astype(np.float64)
+    assert np.linalg.norm(depth.grad.numpy() - g) / np.linalg.norm(g) <= 1e-5

@@ -15,7 +15,8 @@ of its forward, this file reproduces the reference and says so:
       vacancy transmittance at T = 1/2 (render_backward.cu:835-880, 983-999)
       -> `_median_depth_surrogate` (uses the same T = 1/2 assumption).
   Q3  alpha = min(0.99, o*G) passes gradient through the clamp
-      (render_backward.cu:1012) -> tests keep o*G < 0.99.
+      (render_backward.cu:931-933, 1012; sample_backward.cu:284-327): dL/dG
+      = o * dL/dalpha even where alpha is clamped -> `_clamp_st`.
   Q4  rsigma = sqrt(vb / |uvh|^2): the backward omits d rsigma / d(u, v)
       through vb (render_backward.cu:484-490) -> `vb_rs` below.
   Q5  Mip-filter coefficient coef = sqrt(det0/det1): the backward uses
@@ -72,6 +73,12 @@ class _QuirkCoef(torch.autograd.Function):
         coef, det1 = ctx.saved_tensors
         d0 = g * 0.5 / (coef + 1e-6) / det1
         return d0, -d0 * coef
+
+
+def _clamp_st(x):
+    """min(0.99, x) whose gradient is 1 everywhere (Q3: the reference
+    differentiates alpha = o*G through the clamp)."""
+    return x - (x - torch.clamp(x, max=0.99)).detach()
 
 
 def _sh_color(shs, sg_axis, sg_sharp, sg_color, means, campos, deg, sgd):
@@ -240,7 +247,7 @@ def render(pre, lists, W, H, bg, require_depth=True, split=8, iters=5, sample_ra
             co = pre["conic"][g]
             power = -0.5 * (co[0] * d[:, 0] ** 2 + co[2] * d[:, 1] ** 2) - co[1] * d[:, 0] * d[:, 1]
             G = torch.exp(power)
-            al = torch.clamp(pre["opac"][g] * G, max=0.99)
+            al = _clamp_st(pre["opac"][g] * G)
             ok = (~done) & (power <= 0).detach() & (al >= 1.0 / 255.0).detach()
             test_T = T * (1 - al)
             stop = ok & (test_T < 1e-4).detach()
@@ -389,7 +396,7 @@ def sample(pre, lists, points3D, view, proj, W, H, split=8, iters=5, sample_rang
             d = pre["xy"][g][None] - pxy
             co = pre["conic"][g]
             power = -0.5 * (co[0] * d[:, 0] ** 2 + co[2] * d[:, 1] ** 2) - co[1] * d[:, 0] * d[:, 1]
-            al = torch.clamp(pre["opac"][g] * torch.exp(power), max=0.99)
+            al = _clamp_st(pre["opac"][g] * torch.exp(power))
             ok = (~done) & (power <= 0).detach() & (al >= 1.0 / 255.0).detach()
             test_T = T * (1 - al)
             stop = ok & (test_T < 1e-4).detach()
@@ -505,7 +512,7 @@ def integrate(pre, lists, points3D, view, proj, W, H):
                 d = pre["xy"][g][None] - pxy
                 co = pre["conic"][g]
                 power = -0.5 * (co[0] * d[:, 0] ** 2 + co[2] * d[:, 1] ** 2) - co[1] * d[:, 0] * d[:, 1]
-                al = torch.clamp(pre["opac"][g] * torch.exp(power), max=0.99)
+                al = _clamp_st(pre["opac"][g] * torch.exp(power))
                 ok = (~done) & (power <= 0) & (al >= 1.0 / 255.0)
                 test_T = T * (1 - al)
                 stop = ok & (test_T < 1e-4)

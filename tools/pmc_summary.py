@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output of tools/profile.sh into profiles/.
 
-  python tools/pmc_summary.py gpurun_out/prof_r1 profiles r1
+  python tools/pmc_summary.py gpurun_out/prof_r1 profiles r1 [workload_key]
 
 Writes
   profiles/<tag>_kernel_stats.csv   (rocprofv3 --kernel-trace --stats summary, copied)
   profiles/<tag>_stages.json        per-stage average duration and HBM bytes per launch
-  profiles/pmc_summary.json         same content; bench.py reads `traffic` from it
+  profiles/pmc_<workload_key>.json  same content (key: bench.py's workload key, default C3);
+                                    bench.py reads `traffic` and the VALU instruction count from it
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come
 from separate --pmc passes, in KiB; on gfx950 FETCH_SIZE reports half the bytes
@@ -87,6 +88,7 @@ def launches(path: str, counter: str) -> dict:
 
 def main():
     src, dst, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    key = sys.argv[4] if len(sys.argv) > 4 else "C3"
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
@@ -141,9 +143,9 @@ def main():
             if c.get("GRBM_GUI_ACTIVE"):
                 simd_cycles = 256 * 4 * c["GRBM_GUI_ACTIVE"] / 8.0
                 stages[st]["valu_busy"] = round(4.0 * c.get("SQ_INSTS_VALU", 0.0) / simd_cycles, 4)
-    out = {"tag": tag, "source": src, "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950)",
-           "stages": stages}
-    for name in (f"{tag}_stages.json", "pmc_summary.json"):
+    out = {"tag": tag, "workload_key": key, "source": src,
+           "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950)", "stages": stages}
+    for name in (f"{tag}_stages.json", f"pmc_{key}.json"):
         with open(os.path.join(dst, name), "w") as fh:
             json.dump(out, fh, indent=1)
     for st, v in sorted(stages.items(), key=lambda kv: -kv[1]["avg_call_ms"]):

@@ -5,18 +5,23 @@
 #   5. kernel trace + stats of tools/bench_sample.py (sample_depth kernels)
 # (counters in their own passes; never combined with other trace domains).
 # Output: gpurun_out/prof_<tag>/..., summarised by tools/pmc_summary.py.
+#   bash tools/profile.sh <tag> [bench.py workload args, e.g. --config C5 | --no-depth]
+# (the sample_depth pass runs only for the default workload)
 set -o pipefail
 TAG=${1:-r1}
+shift
+WL="$*"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline"
+BENCH="$ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline $WL"
+SHORT="$ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --stage-steps 1 $WL"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $BENCH > $OUT/trace.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/fetch.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/write.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/sq.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sample -o run -- python3 $ROOT/tools/bench_sample.py 10 > $OUT/sample.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $SHORT > $OUT/fetch.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $SHORT > $OUT/write.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- python3 $SHORT > $OUT/sq.log 2>&1 && \
+if [ -z "$WL" ]; then timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sample -o run -- python3 $ROOT/tools/bench_sample.py 10 > $OUT/sample.log 2>&1; fi
 rc=$?
 cd $ROOT
 find $OUT -name "*.csv" | head -20
