@@ -17,10 +17,13 @@ forward only); --no-depth is require_depth=False (training iterations <
 With N > 1 (launched by torch.distributed.run, one rank per GPU) every rank
 renders its own view (C4: cameras orbiting the scene) of the same Gaussians
 and the per-Gaussian gradients are summed over the ranks every step (the only
-exchange of view-parallel training): by default gsr_dist.FactoredViewGrads —
-the geometry rows all-reduced over RCCL, the SH / SG rows rebuilt on every
-rank from the all-gathered per-view DC rows and camera centres (2.6x fewer
-xGMI bytes at SH 3); `--exchange allreduce` all-reduces every row.  `value` =
+exchange of view-parallel training): by default gsr_dist.OverlappedViewGrads —
+inside the rasterizer backward, range by range as the per-Gaussian backward
+produces them, the geometry rows all-reduced and the DC rows all-gathered over
+RCCL while the next range computes, then the SH / SG rows rebuilt on every rank
+from the per-view DC rows and camera centres (2.6x fewer xGMI bytes at SH 3);
+`--exchange factored` runs that exchange after the backward, `--exchange
+allreduce` all-reduces every row.  `value` =
 views/s over all ranks, time = max over ranks.
 
 Rank 0 prints one JSON line: the contract fields, a `roofline` object for the
@@ -74,8 +77,10 @@ def parse():
     ap.add_argument("--sg-degree", type=int, default=None)
     ap.add_argument("--no-depth", action="store_true", help="require_depth=False (iterations < 7000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--exchange", choices=["factored", "allreduce"], default="factored",
-                    help="N > 1: gradient exchange (gsr_dist.FactoredViewGrads, or an all-reduce of every row)")
+    ap.add_argument("--exchange", choices=["overlap", "factored", "allreduce"], default="overlap",
+                    help="N > 1: gradient exchange: gsr_dist.OverlappedViewGrads (inside the backward, range by "
+                         "range), FactoredViewGrads (after it), or an all-reduce of every row")
+    ap.add_argument("--chunks", type=int, default=4, help="--exchange overlap: Gaussian ranges per backward")
     ap.add_argument("--cpu-tile-stride", type=int, default=0, help="0 = auto")
     ap.add_argument("--stage-steps", type=int, default=5,
                     help="untimed steps with every stage bracketed by hipEvents (the per-stage table)")
@@ -251,7 +256,10 @@ def main():
     rasterizer = GaussianRasterizer(settings)
     grad_keys = ["means3D", "shs", "sg_axis", "sg_sharpness", "sg_color", "opacities", "scales", "rotations"]
     reducer = exchanger = None
-    if world > 1 and args.exchange == "allreduce":
+    if world > 1 and args.exchange == "overlap":  # the exchange rides inside every rasterizer backward
+        from gsr_dist import OverlappedViewGrads
+        OverlappedViewGrads(chunks=args.chunks).install()
+    elif world > 1 and args.exchange == "allreduce":
         from gsr_dist import ViewParallelGrads
         reducer = ViewParallelGrads([params[k] for k in grad_keys])
     elif world > 1:  # colour rows rebuilt from the all-gathered DC rows (gsr_dist.FactoredViewGrads)

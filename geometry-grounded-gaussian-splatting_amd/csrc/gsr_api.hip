@@ -462,7 +462,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 12; }
+int gsr_abi_version(void) { return 13; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -658,8 +658,8 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
                                     nullptr, nullptr);
 }
 
-int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
-                           int sg_degree, int SGM, int R, const float* background, int width, int height,
+int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
+                              int sg_degree, int SGM, int R, const float* background, int width, int height,
                            const float* means3D, const float* colors_precomp, const float* opacities,
                            const float* scales, const float* rotations, const float* cov3D_precomp,
                            const float* shs, const float* sg_axis, const float* sg_sharpness,
@@ -672,7 +672,8 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
                            float* dL_dmean3D, float* dL_dmean2D, float* dL_dcolor, float* dL_dopacity,
                            float* dL_dscale, float* dL_drot, float* dL_dcov3D, float* dL_dsh, float* dL_dsg_axis,
                            float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
-                           void* stream_ptr) {
+                           int chunks, gsr_chunk_fn on_chunk, void* chunk_ctx, float* dc_rows,
+                              void* stream_ptr) {
     hipStream_t stream = (hipStream_t)stream_ptr;
     BwdParams b;
     b.f = make_params(P, sh_degree, SHM, sg_degree, SGM, background, width, height, means3D, colors_precomp,
@@ -691,6 +692,8 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
     if (shs && !dL_dsh) return fail(GSR_ERR_ARGS, "missing SH gradient");
     if (SGM > 0 && shs && (!dL_dsg_axis || !dL_dsg_sharpness || !dL_dsg_color))
         return fail(GSR_ERR_ARGS, "missing SG gradients");
+    if (chunks < 1) return fail(GSR_ERR_ARGS, "chunks must be >= 1");
+    if (dc_rows && !shs) return fail(GSR_ERR_ARGS, "dc_rows needs the SH colour path");
     b.R = R;
     b.radii = radii;
     b.alphas = alphas;
@@ -740,8 +743,44 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
         ws.tile_order = nullptr;
     }
     GSR_STAGE(GSR_STAGE_RENDER_BWD, launch_render_bwd(b, gs, bs, is, ts, ws, stream), "render backward");
-    GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_bwd(b, gs, ws, stream), "preprocess backward");
+    // the per-Gaussian backward over `chunks` consecutive Gaussian ranges; after each range's launch
+    // the host callback may post work on other streams that waits for it (gsr_dist.OverlappedViewGrads:
+    // the range's gradient exchange runs while the next range computes)
+    // (ranges of whole 256-Gaussian workgroups; gsr_dist.OverlappedViewGrads.chunk_size mirrors this)
+    const int cs = ((P + chunks - 1) / chunks + 255) / 256 * 256;
+    for (int b0 = 0; b0 < P; b0 += cs) {
+        const int b1 = min(P, b0 + cs);
+        GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_bwd(b, gs, ws, stream, b0, b1, dc_rows),
+                  "preprocess backward");
+        if (on_chunk) on_chunk(chunk_ctx, b0, b1);
+    }
     return GSR_OK;
+}
+
+int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
+                           int sg_degree, int SGM, int R, const float* background, int width, int height,
+                           const float* means3D, const float* colors_precomp, const float* opacities,
+                           const float* scales, const float* rotations, const float* cov3D_precomp,
+                           const float* shs, const float* sg_axis, const float* sg_sharpness,
+                           const float* sg_color, float scale_modifier, const float* viewmatrix,
+                           const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                           float kernel_size, const int* radii, const float* alphas, const float* normalmap,
+                           const float* mdepth, const void* geom_buffer, const void* binning_buffer,
+                           const void* image_buffer, const void* tile_buffer, const float* dL_dpix,
+                           const float* dL_dpix_mdepth, const float* dL_dalphas, const float* dL_dpixel_normals,
+                           float* dL_dmean3D, float* dL_dmean2D, float* dL_dcolor, float* dL_dopacity,
+                           float* dL_dscale, float* dL_drot, float* dL_dcov3D, float* dL_dsh, float* dL_dsg_axis,
+                           float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
+                           void* stream_ptr) {
+    return gsr_rasterize_backward_ex(geom_bwd_alloc, geom_bwd_ctx, P, sh_degree, SHM, sg_degree, SGM, R, background,
+                                     width, height, means3D, colors_precomp, opacities, scales, rotations,
+                                     cov3D_precomp, shs, sg_axis, sg_sharpness, sg_color, scale_modifier, viewmatrix,
+                                     projmatrix, campos, tan_fovx, tan_fovy, kernel_size, radii, alphas, normalmap,
+                                     mdepth, geom_buffer, binning_buffer, image_buffer, tile_buffer, dL_dpix,
+                                     dL_dpix_mdepth, dL_dalphas, dL_dpixel_normals, dL_dmean3D, dL_dmean2D, dL_dcolor,
+                                     dL_dopacity, dL_dscale, dL_drot, dL_dcov3D, dL_dsh, dL_dsg_axis,
+                                     dL_dsg_sharpness, dL_dsg_color, require_depth, debug, 1, nullptr, nullptr,
+                                     nullptr, stream_ptr);
 }
 
 // The point-query forwards (sample_depth, integrate, evaluate_sdf) share
@@ -1070,6 +1109,24 @@ int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_ra
         return fail(GSR_ERR_ARGS, "densify stats: invalid arguments");
     hipError_t e = launch_densify_stats(P, vgrad, radii, max_radii2D, accum, accum_abs, denom, (hipStream_t)stream_ptr);
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "densify stats", e);
+}
+
+int gsr_view_color_grads_chunked(int P, int sh_degree, int SHM, int sg_degree, int SGM, int n_views, int chunk,
+                                 const float* gathered, const float* campos, const float* means3D,
+                                 const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                                 float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness, float* dL_dsg_color,
+                                 void* stream_ptr) {
+    if (P < 0 || n_views < 1 || chunk < 1 || sh_degree < 0 || sh_degree > 3 ||
+        SHM < (sh_degree + 1) * (sh_degree + 1) || SGM < 0 || sg_degree < 0 || sg_degree > 7 || sg_degree > SGM)
+        return fail(GSR_ERR_ARGS, "view colour grads: invalid arguments");
+    if (P > 0 && (!gathered || !campos || !means3D || !dL_dsh ||
+                  (SGM > 0 && (!dL_dsg_axis || !dL_dsg_sharpness || !dL_dsg_color)) ||
+                  (sg_degree > 0 && (!sg_axis || !sg_sharpness || !sg_color))))
+        return fail(GSR_ERR_ARGS, "view colour grads: missing buffer");
+    hipError_t e = launch_view_color_grads(P, sh_degree, SHM, sg_degree, SGM, n_views, gathered, means3D, sg_axis,
+                                           sg_sharpness, sg_color, dL_dsh, dL_dsg_axis, dL_dsg_sharpness,
+                                           dL_dsg_color, (hipStream_t)stream_ptr, chunk, campos);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "view colour grads", e);
 }
 
 int gsr_view_color_grads(int P, int sh_degree, int SHM, int sg_degree, int SGM, int n_views, const float* gathered,

@@ -8,7 +8,7 @@ namespace gsr {
 
 // Run-time switches for A/B variants of one kernel in one process
 // (gsr_set_option in include/gsr.h); defaults are the shipped paths.
-enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptSortbin = 7, kOptBwdNarrow = 8, kOptRocprimDsort = 9, kNumOptions = 10 };
+enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptSortbin = 7, kOptBwdNarrow = 8, kOptRocprimDsort = 9, kOptPbwdStage = 10, kNumOptions = 11 };
 int option(int which);
 hipError_t read_render_stats(unsigned long long* out, bool reset);
 
@@ -107,7 +107,10 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
                              const TileState& ts, const BwdState& ws, hipStream_t stream);
 
 // preprocess_bwd.hip
-hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const BwdState& ws, hipStream_t stream);
+// Gaussians [begin, end) (end < 0: all P); dc_rows non-null: factored view-parallel mode
+// (preprocess_bwd.hip PreprocessBwdArgs::dc_rows)
+hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const BwdState& ws, hipStream_t stream,
+                                 int begin = 0, int end = -1, float* dc_rows = nullptr);
 
 // render_fwd.hip: the forward raster in SAMPLE mode (median depth at points)
 // point queries answered by the forward raster in SAMPLE mode
@@ -153,7 +156,8 @@ hipError_t launch_adam(int n_groups, const AdamGroup* groups, const double* lr, 
 hipError_t launch_view_color_grads(int P, int D, int SHM, int SGD, int SGM, int n_views, const float* gathered,
                                    const float* means3D, const float* sg_axis, const float* sg_sharpness,
                                    const float* sg_color, float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness,
-                                   float* dL_dsg_color, hipStream_t stream);
+                                   float* dL_dsg_color, hipStream_t stream, int chunk = 0,
+                                   const float* campos = nullptr);
 hipError_t launch_densify_stats(int P, const float* vgrad, const int* radii, float* max_radii2D, float* accum,
                                 float* accum_abs, float* denom, hipStream_t stream);
 

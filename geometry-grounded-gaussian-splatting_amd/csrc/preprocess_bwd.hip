@@ -49,8 +49,14 @@ struct PreprocessBwdArgs {
     float* dL_dsg_axis;
     float* dL_dsg_sharpness;
     float* dL_dsg_color;
+    int begin, end;  // the Gaussians of this launch: [begin, end)
+    // factored view-parallel mode (gsr_dist.OverlappedViewGrads): the DC row
+    // dL/dsh[:, 0, :] goes to dc_rows [P][3] and no SH / SG gradient row is
+    // written (gsr_view_color_grads_chunked rebuilds them from every view's DC rows)
+    float* dc_rows;
 };
 
+template <bool ROWS = true>
 __device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
     for (int k = 0; k < 3; k++) a.dL_dmean3D[3 * idx + k] = 0.f;
     a.dL_dopacity[idx] = 0.f;
@@ -60,6 +66,11 @@ __device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
         for (int k = 0; k < 4; k++) a.dL_drot[4 * idx + k] = 0.f;
     if (a.dL_dcov3D)
         for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = 0.f;
+    if (a.dc_rows) {
+        for (int c = 0; c < 3; c++) a.dc_rows[3 * idx + c] = 0.f;
+        return;
+    }
+    if (!ROWS) return;
     if (a.dL_dsh)
         for (int k = 0; k < 3 * a.SHM; k++) a.dL_dsh[(size_t)idx * 3 * a.SHM + k] = 0.f;
     for (int k = 0; k < a.SGM; k++) {
@@ -91,8 +102,14 @@ __device__ __forceinline__ void sg7_load(const PreprocessBwdArgs& a, int idx, SG
     load_row(a.sg_color + 3 * o0, r.gc);
     load_row(a.sg_sharpness + o0, r.sharp);
 }
+// Staged row stores (GSR_OPT_PBWD_STAGE): per wave, LDS rows for its 64
+// Gaussians — the SG-7 gradient rows (colour 21, sharpness 7, axis 21 floats
+// each), then, reusing the space, the SH gradient rows (48 floats each) —
+// written out by wave_store_rows.
+constexpr int kStageColor = 0, kStageSharp = 64 * 21, kStageAxis = 64 * 28, kStageFloats = 64 * 49;
 __device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, const SG7Rows& rows, float x, float y,
-                                        float z, float dR0, float dR1, float dR2, float& ddx, float& ddy, float& ddz) {
+                                        float z, float dR0, float dR1, float dR2, float& ddx, float& ddy, float& ddz,
+                                        float* stage = nullptr, int lane = 0) {
     const size_t o0 = (size_t)idx * kSG7;
     const float* ax = rows.ax;
     const float* gc = rows.gc;
@@ -118,22 +135,57 @@ __device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, con
         ddy += dL_daux * axs[1];
         ddz += dL_daux * axs[2];
     }
+    if (a.dc_rows) return;  // (rows rebuilt by the view exchange)
+    if (stage) {  // this lane's slots of the wave's LDS rows (stage_rows)
+#pragma unroll
+        for (int k = 0; k < 3 * kSG7; k++) stage[kStageColor + 3 * kSG7 * lane + k] = dcol[k];
+#pragma unroll
+        for (int k = 0; k < kSG7; k++) stage[kStageSharp + kSG7 * lane + k] = dsh[k];
+#pragma unroll
+        for (int k = 0; k < 3 * kSG7; k++) stage[kStageAxis + 3 * kSG7 * lane + k] = dax[k];
+        return;
+    }
     store_row(a.dL_dsg_color + 3 * o0, dcol);
     store_row(a.dL_dsg_sharpness + o0, dsh);
     store_row(a.dL_dsg_axis + 3 * o0, dax);
 }
 
+// A wave's n consecutive rows of nf floats each, staged in LDS in the
+// global layout, written out as whole-wave 16-B pieces: one store
+// instruction covers 1 KB of consecutive bytes instead of 64 rows.
+__device__ __forceinline__ void wave_store_rows(float* __restrict__ g, const float* __restrict__ l, int nf, int lane) {
+    const int n4 = nf >> 2;
+    for (int c = lane; c < n4; c += 64) reinterpret_cast<float4*>(g)[c] = reinterpret_cast<const float4*>(l)[c];
+    for (int c = (n4 << 2) + lane; c < nf; c += 64) g[c] = l[c];
+}
+
 #ifndef GSR_PBWD_WAVES
 #define GSR_PBWD_WAVES 0
 #endif
+#ifndef GSR_PBWD_STAGE_DEFAULT
+#define GSR_PBWD_STAGE_DEFAULT 0
+#endif
+// STAGE (SH rows of 16 coefficients, launch ranges in whole workgroups): the
+// SH and SG-7 gradient rows go out through LDS as whole-wave stores.  Every
+// lane of a wave then takes part in the stores, so a lane past the range
+// computes Gaussian `begin` again (same values to the same addresses) and
+// only its staged rows are left out.
+template <bool STAGE>
 #if GSR_PBWD_WAVES
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_PBWD_WAVES, 8)))
 preprocess_bwd_kernel(PreprocessBwdArgs a) {
 #else
 __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a) {
 #endif
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
+    const int idx0 = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
+    if (!STAGE && idx0 >= a.end) return;
+    const int idx = idx0 < a.end ? idx0 : a.begin;
+    const int lane = threadIdx.x & 63;
+    __shared__ float s_stage[STAGE ? 4 * kStageFloats : 1];
+    float* stage = s_stage + (STAGE ? (threadIdx.x >> 6) * kStageFloats : 0);
+    // (STAGE) what the SH rows need, left by the visible-Gaussian body: direction and clamp-masked dL/dRGB
+    float st_x = 0.f, st_y = 0.f, st_z = 0.f, st_d0 = 0.f, st_d1 = 0.f, st_d2 = 0.f;
+    bool culled = false;
     // every per-Gaussian input row is requested up front, before the culled
     // test and the dependent chains (one memory round trip instead of one per
     // phase; the kernel is latency-bound)
@@ -182,9 +234,14 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         a.dL_dcolor[3 * idx + 2] = acc[kAccColor + 2];
     }
     if (!(radius > 0)) {
-        zero_outputs(a, idx);
-        return;
+        if constexpr (!STAGE) {
+            zero_outputs(a, idx);
+            return;
+        }
+        zero_outputs<false>(a, idx);  // (rows: zero slots in the staged stores below)
+        culled = true;
     }
+    auto visible = [&]() {
     const float fx = a.focal_x, fy = a.focal_y;
     const float* V = a.view;
     const float dconx = acc[kAccConic + 0], dcony = acc[kAccConic + 1], dconz = acc[kAccConic + 2],
@@ -518,7 +575,15 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         const int n = sh_count(a.D);
         float sh[48];
         load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
-        store_sh_grad(a.dL_dsh + (size_t)idx * a.SHM * 3, a.SHM, n, Y, dR0, dR1, dR2);
+        if (STAGE) {  // the row is written by the staged stores
+            st_x = x, st_y = y, st_z = z, st_d0 = dR0, st_d1 = dR1, st_d2 = dR2;
+        } else if (a.dc_rows) {  // the DC row as store_sh_grad writes it (Y[0] dR)
+            a.dc_rows[3 * idx] = Y[0] * dR0;
+            a.dc_rows[3 * idx + 1] = Y[0] * dR1;
+            a.dc_rows[3 * idx + 2] = Y[0] * dR2;
+        } else {
+            store_sh_grad(a.dL_dsh + (size_t)idx * a.SHM * 3, a.SHM, n, Y, dR0, dR1, dR2);
+        }
         // d(colour)/d(dir) per channel: dx/dy/dz (render_backward.cu:94-153)
         float gdx[3] = {0.f, 0.f, 0.f}, gdy[3] = {0.f, 0.f, 0.f}, gdz[3] = {0.f, 0.f, 0.f};
         if (a.D > 0) {
@@ -559,12 +624,13 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         float ddz = gdz[0] * dR0 + gdz[1] * dR1 + gdz[2] * dR2;
 #if GSR_SG_UNROLL
         if (sg7) {
-            sg7_bwd(a, idx, sgr, x, y, z, dR0, dR1, dR2, ddx, ddy, ddz);
+            sg7_bwd(a, idx, sgr, x, y, z, dR0, dR1, dR2, ddx, ddy, ddz, STAGE ? stage : nullptr, lane);
         } else
 #endif
         for (int sg = 0; sg < a.SGM; sg++) {
             const size_t o = (size_t)idx * a.SGM + sg;
             if (sg >= a.SGD) {
+                if (a.dc_rows) continue;
                 a.dL_dsg_sharpness[o] = 0.f;
                 for (int c = 0; c < 3; c++) {
                     a.dL_dsg_axis[3 * o + c] = 0.f;
@@ -577,16 +643,18 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
             const float sharp = a.sg_sharpness[o];
             const float auxs = (ax[0] * x + ax[1] * y + ax[2] * z) - 1.0f;
             const float gs = expf(sharp * auxs);
-            a.dL_dsg_color[3 * o + 0] = dR0 * gs;
-            a.dL_dsg_color[3 * o + 1] = dR1 * gs;
-            a.dL_dsg_color[3 * o + 2] = dR2 * gs;
             const float dL_dgs = gc[0] * dR0 + gc[1] * dR1 + gc[2] * dR2;
             const float dL_dexp = dL_dgs * gs;
-            a.dL_dsg_sharpness[o] = dL_dexp * auxs;
             const float dL_daux = dL_dexp * sharp;
-            a.dL_dsg_axis[3 * o + 0] = dL_daux * x;
-            a.dL_dsg_axis[3 * o + 1] = dL_daux * y;
-            a.dL_dsg_axis[3 * o + 2] = dL_daux * z;
+            if (!a.dc_rows) {
+                a.dL_dsg_color[3 * o + 0] = dR0 * gs;
+                a.dL_dsg_color[3 * o + 1] = dR1 * gs;
+                a.dL_dsg_color[3 * o + 2] = dR2 * gs;
+                a.dL_dsg_sharpness[o] = dL_dexp * auxs;
+                a.dL_dsg_axis[3 * o + 0] = dL_daux * x;
+                a.dL_dsg_axis[3 * o + 1] = dL_daux * y;
+                a.dL_dsg_axis[3 * o + 2] = dL_daux * z;
+            }
             ddx += dL_daux * ax[0];
             ddy += dL_daux * ax[1];
             ddz += dL_daux * ax[2];
@@ -612,11 +680,57 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     a.dL_dmean3D[3 * idx] = dm0;
     a.dL_dmean3D[3 * idx + 1] = dm1;
     a.dL_dmean3D[3 * idx + 2] = dm2;
+    };
+    if (!culled) visible();
+    if constexpr (STAGE) {
+        // the wave's Gaussians [wbase, wbase + n): rows in LDS, then whole-wave stores
+        const int wbase = idx0 - lane;
+        const int n = max(0, min(64, a.end - wbase));
+        if (sg7) {
+            if (culled) {
+#pragma unroll
+                for (int k = 0; k < 3 * kSG7; k++) {
+                    stage[kStageColor + 3 * kSG7 * lane + k] = 0.f;
+                    stage[kStageAxis + 3 * kSG7 * lane + k] = 0.f;
+                }
+#pragma unroll
+                for (int k = 0; k < kSG7; k++) stage[kStageSharp + kSG7 * lane + k] = 0.f;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const size_t o = (size_t)wbase * kSG7;
+            wave_store_rows(a.dL_dsg_color + 3 * o, stage + kStageColor, n * 3 * kSG7, lane);
+            wave_store_rows(a.dL_dsg_sharpness + o, stage + kStageSharp, n * kSG7, lane);
+            wave_store_rows(a.dL_dsg_axis + 3 * o, stage + kStageAxis, n * 3 * kSG7, lane);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        // SH rows (Y_k dR, zero past the active degree; culled lanes have dR = 0)
+        float Y[16];
+        sh_basis(a.D, st_x, st_y, st_z, Y);
+        const int nsh = sh_count(a.D);
+        auto val = [&](int e) {
+            const int k = e / 3, c = e - 3 * (e / 3);
+            const float d = c == 0 ? st_d0 : (c == 1 ? st_d1 : st_d2);
+            return k < nsh ? Y[k] * d : 0.f;
+        };
+        float4* row = reinterpret_cast<float4*>(stage + 48 * lane);
+#pragma unroll
+        for (int i = 0; i < 12; i++) row[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_store_rows(a.dL_dsh + (size_t)wbase * 48, stage, n * 48, lane);
+    }
 }
 
-hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const BwdState& ws, hipStream_t stream) {
+hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const BwdState& ws, hipStream_t stream,
+                                 int begin, int end, float* dc_rows) {
     const FwdParams& p = b.f;
-    if (p.P == 0) return hipSuccess;
+    if (end < 0) end = p.P;
+    if (end <= begin) return hipSuccess;
     PreprocessBwdArgs a;
     a.P = p.P;
     a.D = p.D;
@@ -656,7 +770,21 @@ hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const 
     a.dL_dsg_axis = b.dL_dsg_axis;
     a.dL_dsg_sharpness = b.dL_dsg_sharpness;
     a.dL_dsg_color = b.dL_dsg_color;
-    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
+    a.begin = begin;
+    a.end = end;
+    a.dc_rows = dc_rows;
+    // staged row stores: the 16-coefficient SH layout, 16-B aligned rows, SG degree 0 or 7 (the
+    // configurations with wide rows), whole-workgroup ranges; GSR_OPT_PBWD_STAGE 1 forces it, 2 turns it off
+    const int so = option(kOptPbwdStage);
+    auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    const bool stage_ok = p.shs && !dc_rows && p.SHM == 16 && (begin & 255) == 0 && al16(b.dL_dsh) &&
+                          (p.SGM == 0 || (p.SGM == kSG7 && p.SGD == kSG7 && al16(b.dL_dsg_color) &&
+                                          al16(b.dL_dsg_sharpness) && al16(b.dL_dsg_axis)));
+    const bool stage = stage_ok && (so == 1 || (so == 0 && GSR_PBWD_STAGE_DEFAULT));
+    if (stage)
+        hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((end - begin + 255) / 256), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(preprocess_bwd_kernel<false>, dim3((end - begin + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

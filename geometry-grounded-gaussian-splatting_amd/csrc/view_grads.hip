@@ -14,6 +14,15 @@
 // all-reducing the 192-B (SH 3) or 388-B (SH 3 + SG 7) gradient rows; every
 // rank then sums the views here, in view order, so the replicas stay
 // bit-identical.  The DC row itself is summed as gathered (no division).
+//
+// Two layouts of the gathered rows:
+//  * chunk = 0 (gsr_dist.FactoredViewGrads, one all-gather after the
+//    backward): [n_views][P * 3 + 4], each view's DC rows then its camera centre;
+//  * chunk > 0 (gsr_dist.OverlappedViewGrads, one all-gather per Gaussian
+//    range as the backward produces it): the Gaussians in ranges of `chunk`
+//    (the last one shorter); range r = [b, b + len) occupies
+//    [3 n_views b, 3 n_views (b + len)) as [n_views][len][3], and the camera
+//    centres are a separate [n_views][4] array.
 #include "gsr_kernels.h"
 #include "gsr_math.h"
 
@@ -21,7 +30,7 @@ namespace gsr {
 
 struct ViewColorArgs {
     int P, D, SHM, SGD, SGM, n_views;
-    const float* gathered;  // [n_views][P * 3 + 4]: the view's dL/dsh[:, 0, :], then its camera centre
+    const float* gathered;  // the views' dL/dsh[:, 0, :] (and camera centres), layout by `chunk` (header)
     const float* means3D;
     const float* sg_axis;
     const float* sg_sharpness;
@@ -30,6 +39,8 @@ struct ViewColorArgs {
     float* dL_dsg_axis;
     float* dL_dsg_sharpness;
     float* dL_dsg_color;
+    int chunk;
+    const float* campos;  // [n_views][4] when chunk > 0
 };
 
 constexpr int kMaxSG = 7;
@@ -65,10 +76,20 @@ __global__ void __launch_bounds__(256) view_color_grads_kernel(ViewColorArgs a) 
     for (int k = 0; k < 3 * kMaxSG; k++) dcol[k] = dax[k] = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxSG; k++) dlam[k] = 0.f;
+    // (chunked layout: this Gaussian's range and its slot in it)
+    const int rb = a.chunk > 0 ? idx / a.chunk * a.chunk : 0;
+    const int rlen = a.chunk > 0 ? min(a.chunk, a.P - rb) : 0;
     for (int v = 0; v < a.n_views; v++) {
-        const float* row = a.gathered + (size_t)v * stride;
+        const float* row;
+        const float* cp;
+        if (a.chunk > 0) {
+            row = a.gathered + (size_t)3 * a.n_views * rb + (size_t)3 * v * rlen - (size_t)3 * rb;
+            cp = a.campos + 4 * v;
+        } else {
+            row = a.gathered + (size_t)v * stride;
+            cp = row + (size_t)a.P * 3;
+        }
         const float g0 = row[3 * idx], g1 = row[3 * idx + 1], g2 = row[3 * idx + 2];
-        const float* cp = row + (size_t)a.P * 3;
         // direction as the colour backward forms it (preprocess_bwd.hip)
         const float dox = mx - cp[0], doy = my - cp[1], doz = mz - cp[2];
         const float dlen = sqrtf(dox * dox + doy * doy + doz * doz);
@@ -139,10 +160,10 @@ __global__ void __launch_bounds__(256) view_color_grads_kernel(ViewColorArgs a) 
 hipError_t launch_view_color_grads(int P, int D, int SHM, int SGD, int SGM, int n_views, const float* gathered,
                                    const float* means3D, const float* sg_axis, const float* sg_sharpness,
                                    const float* sg_color, float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness,
-                                   float* dL_dsg_color, hipStream_t stream) {
+                                   float* dL_dsg_color, hipStream_t stream, int chunk, const float* campos) {
     if (P == 0) return hipSuccess;
     ViewColorArgs a{P, D, SHM, SGD, SGM, n_views, gathered, means3D, sg_axis, sg_sharpness, sg_color,
-                    dL_dsh, dL_dsg_axis, dL_dsg_sharpness, dL_dsg_color};
+                    dL_dsh, dL_dsg_axis, dL_dsg_sharpness, dL_dsg_color, chunk, campos};
     hipLaunchKernelGGL(view_color_grads_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }

@@ -33,6 +33,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSR_LIB") or os.path.join(_HERE, "libgsr.so")  # GSR_LIB: development A/B builds
 
 _ALLOC = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_CHUNK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int)  # gsr_chunk_fn
 _lib = None
 
 
@@ -43,7 +44,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 def _load():
@@ -67,6 +68,8 @@ def _load():
     L.gsr_rasterize_backward.restype = i
     L.gsr_rasterize_backward.argtypes = ([_ALLOC, vp] + [i] * 6 + [vp, i, i] + [vp] * 10 + [f] + [vp] * 3
                                          + [f] * 3 + [vp] * 4 + [vp] * 4 + [vp] * 4 + [vp] * 11 + [i, i, vp])
+    L.gsr_rasterize_backward_ex.restype = i
+    L.gsr_rasterize_backward_ex.argtypes = L.gsr_rasterize_backward.argtypes[:-1] + [i, _CHUNK, vp, vp, vp]
     L.gsr_sample_depth_forward.restype = i
     L.gsr_sample_depth_forward.argtypes = ([_ALLOC, vp] * 6 + [i] * 4 + [vp] * 4 + [f] + [vp] * 5 + [f] * 3 + [i]
                                            + [vp, vp, i, vp] + [ctypes.POINTER(i)] * 3)
@@ -88,6 +91,8 @@ def _load():
     L.gsr_densify_stats.argtypes = [i] + [vp] * 7
     L.gsr_view_color_grads.restype = i
     L.gsr_view_color_grads.argtypes = [i] * 6 + [vp] * 10
+    L.gsr_view_color_grads_chunked.restype = i
+    L.gsr_view_color_grads_chunked.argtypes = [i] * 7 + [vp] * 11
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     L.gsr_set_option.argtypes = [i, i]
@@ -125,6 +130,7 @@ OPT_BWD_NO_CACHE = 6
 OPT_SORTBIN = 7
 OPT_BWD_NARROW = 8
 OPT_ROCPRIM_DSORT = 9
+OPT_PBWD_STAGE = 10
 
 
 def debug_render_stats(reset: bool = True) -> list:
@@ -326,7 +332,15 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
                                  sg_axis, sg_sharpness, sg_color, sh_degree, sg_degree, scale_modifier, viewmatrix,
                                  projmatrix, tan_fovx, tan_fovy, kernel_size, dL_dout_color, dL_dout_mdepth,
                                  dL_dout_alpha, dL_dout_normal, alphas, normalmap, mdepth, campos, radii,
-                                 geomBuffer, R, binningBuffer, imageBuffer, tileBuffer, require_depth, debug):
+                                 geomBuffer, R, binningBuffer, imageBuffer, tileBuffer, require_depth, debug,
+                                 exchange=None):
+    """The reference's 35 arguments and 11 gradients (rasterize_points.cu:141-258).
+    `exchange` (not in the reference; gsr_dist.OverlappedViewGrads) runs the
+    per-Gaussian backward in exchange.chunks Gaussian ranges through
+    gsr_rasterize_backward_ex and calls exchange.on_chunk(begin, end, grads)
+    after each range is queued; with exchange.dc_rows(...) a buffer, only the
+    DC gradient rows are written there (the SH / SG rows are the exchange's to
+    rebuild before the gradients are used)."""
     L = _load()
     P = means3D.size(0)
     img = dL_dout_color if dL_dout_color is not None else alphas  # (a None upstream gradient is zero)
@@ -349,8 +363,24 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
             dL_dout_alpha=dL_dout_alpha, dL_dout_normal=dL_dout_normal).items()}
         radii = radii.contiguous()
         scratch = _ByteBuffer(dev)
+        grads = (outs["dmeans2D"], outs["dcolors"], outs["dopacity"], outs["dmeans3D"], outs["dcov3D"], outs["dsh"],
+                 outs["dsg_axis"], outs["dsg_sharpness"], outs["dsg_color"], outs["dscales"], outs["drotations"])
+        chunks, dc, errors = 1, None, []
+        hook = _CHUNK()  # NULL
+        if exchange is not None:
+            chunks = max(1, int(exchange.chunks))
+            dc = exchange.dc_rows(P, dev) if SHM else None
+
+            def on_chunk(_ctx, b, e):
+                try:
+                    if not errors:
+                        exchange.on_chunk(b, e, grads)
+                except BaseException as ex:  # noqa: BLE001 - re-raised after the C call returns
+                    errors.append(ex)
+
+            hook = _CHUNK(on_chunk)
         with torch.cuda.device(dev):
-            rc = L.gsr_rasterize_backward(
+            rc = L.gsr_rasterize_backward_ex(
                 scratch.cb, None, P, int(sh_degree), SHM, int(sg_degree), SGM, int(R), _ptr(a["background"]), W, H,
                 _ptr(a["means3D"]), _ptr(a["colors"]), _ptr(a["opacity"]), _ptr(a["scales"]), _ptr(a["rotations"]),
                 _ptr(a["cov3D_precomp"]), _ptr(a["sh"]), _ptr(a["sg_axis"]), _ptr(a["sg_sharpness"]),
@@ -361,8 +391,11 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
                 _ptr(a["dL_dout_alpha"]), _ptr(a["dL_dout_normal"]), _ptr(outs["dmeans3D"]), _ptr(outs["dmeans2D"]),
                 _ptr(outs["dcolors"]), _ptr(outs["dopacity"]), _ptr(outs["dscales"]), _ptr(outs["drotations"]),
                 _ptr(outs["dcov3D"]), _ptr(outs["dsh"]), _ptr(outs["dsg_axis"]), _ptr(outs["dsg_sharpness"]),
-                _ptr(outs["dsg_color"]), int(bool(require_depth)), int(bool(debug)), _stream(dev))
+                _ptr(outs["dsg_color"]), int(bool(require_depth)), int(bool(debug)), chunks, hook, None,
+                None if dc is None else _ptr(dc), _stream(dev))
         _check(rc)
+        if errors:
+            raise errors[0]
         if KEEP_BWD_SCRATCH:
             global last_bwd_scratch
             last_bwd_scratch = scratch.tensor
@@ -551,6 +584,40 @@ def densify_stats(viewspace_grad, radii, max_radii2D, accum, accum_abs, denom) -
     with torch.cuda.device(dev):
         _check(L.gsr_densify_stats(P, _ptr(viewspace_grad), _ptr(r), _ptr(max_radii2D), _ptr(accum), _ptr(accum_abs),
                                    _ptr(denom), _stream(dev)))
+
+
+def view_color_grads_chunked(gathered, campos, n_views: int, chunk: int, means3D, sh_degree: int, dL_dsh,
+                             sg_degree: int = 0, sg_axis=None, sg_sharpness=None, sg_color=None, dL_dsg_axis=None,
+                             dL_dsg_sharpness=None, dL_dsg_color=None) -> None:
+    """gsr_view_color_grads_chunked: view_color_grads for the range-by-range
+    gathered layout (include/gsr.h): gathered [n_views * P * 3] DC rows in
+    ranges of `chunk` Gaussians, campos [n_views, 4]."""
+    L = _load()
+    P = means3D.shape[0]
+    SHM = dL_dsh.shape[1]
+    SGM = dL_dsg_color.shape[1] if dL_dsg_color is not None and dL_dsg_color.numel() else 0
+    if gathered.numel() != n_views * P * 3 or campos.numel() != 4 * n_views or chunk < 1:
+        raise RuntimeError("gsr view_color_grads_chunked: `gathered` must hold n_views * 3 P floats, `campos` "
+                           "n_views * 4, chunk >= 1")
+    want = {"means3D": (means3D, (P, 3)), "dL_dsh": (dL_dsh, (P, SHM, 3))}
+    if SGM:
+        want.update(dL_dsg_axis=(dL_dsg_axis, (P, SGM, 3)), dL_dsg_sharpness=(dL_dsg_sharpness, (P, SGM)),
+                    dL_dsg_color=(dL_dsg_color, (P, SGM, 3)))
+    if sg_degree:
+        want.update(sg_axis=(sg_axis, (P, SGM, 3)), sg_sharpness=(sg_sharpness, (P, SGM)),
+                    sg_color=(sg_color, (P, SGM, 3)))
+    for name, (t, shape) in list(want.items()) + [("gathered", (gathered, tuple(gathered.shape))),
+                                                  ("campos", (campos, tuple(campos.shape)))]:
+        if tuple(t.shape) != shape or not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError(f"gsr view_color_grads_chunked: `{name}` must be a contiguous fp32 HIP tensor "
+                               f"of shape {shape}")
+    dev = means3D.device
+    p = lambda t: _ptr(t) if t is not None and t.numel() else None  # noqa: E731
+    with torch.cuda.device(dev):
+        _check(L.gsr_view_color_grads_chunked(P, int(sh_degree), SHM, int(sg_degree), SGM, int(n_views), int(chunk),
+                                              _ptr(gathered), _ptr(campos), _ptr(means3D), p(sg_axis),
+                                              p(sg_sharpness), p(sg_color), _ptr(dL_dsh), p(dL_dsg_axis),
+                                              p(dL_dsg_sharpness), p(dL_dsg_color), _stream(dev)))
 
 
 def view_color_grads(gathered, n_views: int, means3D, sh_degree: int, dL_dsh, sg_degree: int = 0, sg_axis=None,

@@ -32,6 +32,16 @@ def colour_backward_count() -> int:
     return _colour_backward_calls
 
 
+# The view-parallel gradient exchange run inside every rasterizer backward
+# (gsr_dist.OverlappedViewGrads.install); None: the reference's single-view backward.
+_view_exchange = None
+
+
+def set_view_exchange(exchange) -> None:
+    global _view_exchange
+    _view_exchange = exchange
+
+
 def cpu_deep_copy_tuple(input_tuple):
     copied_tensors = [item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple]
     return tuple(copied_tensors)
@@ -86,16 +96,23 @@ class _RasterizeGaussians(torch.autograd.Function):
                 s.tanfovx, s.tanfovy, s.kernel_size, grad_color, grad_mdepth, grad_alpha, grad_normal, alpha, normal,
                 mdepth, s.campos, radii, geomBuffer, num_rendered, binningBuffer, imgBuffer, tileBuffer,
                 s.require_depth, s.debug)
+        ex = _view_exchange
+        kw = {}
+        if ex is not None:  # gsr_dist.OverlappedViewGrads: the exchange rides on the backward's Gaussian ranges
+            ex.begin(s.campos, means3D.shape[0], scales.numel() > 0, sh.numel() > 0)
+            kw["exchange"] = ex
         if s.debug:
             cpu_args = cpu_deep_copy_tuple(args)
             try:
-                g = _C.rasterize_gaussians_backward(*args)
-            except Exception as ex:
+                g = _C.rasterize_gaussians_backward(*args, **kw)
+            except Exception as ex_:
                 torch.save(cpu_args, "snapshot_bw.dump")
                 print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
-                raise ex
+                raise ex_
         else:
-            g = _C.rasterize_gaussians_backward(*args)
+            g = _C.rasterize_gaussians_backward(*args, **kw)
+        if ex is not None:
+            ex.finish(g, means3D, sg_axis, sg_sharpness, sg_color, s.sh_degree, s.sg_degree)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
          grad_sg_axis, grad_sg_sharpness, grad_sg_color, grad_scales, grad_rotations) = g
         if sh.numel():

@@ -259,6 +259,127 @@ class FactoredViewGrads:
             rest_t.grad.copy_(rows[:, k:])
 
 
+class OverlappedViewGrads:
+    """The view-parallel gradient exchange run INSIDE each rasterizer
+    backward, overlapped with its per-Gaussian tail ("chunk the
+    preprocess-bwd over Gaussian ranges and post per-chunk all-reduces on a
+    side stream").
+
+    Installed (`install()` or `with OverlappedViewGrads(...):`), every
+    _RasterizeGaussians backward runs its per-Gaussian backward in `chunks`
+    Gaussian ranges (gsr_rasterize_backward_ex).  As each range is queued,
+    this posts, asynchronously (RCCL runs them on its own stream, after the
+    range's kernel, while the next range computes):
+      * one coalesced all-reduce of the range's geometry gradients (means3D,
+        opacity, scales + rotations or cov3D; colours when no SH is given);
+      * one all-gather of the range's DC gradient rows (12 B per Gaussian;
+        the kernel writes them to a compact [P][3] buffer and skips the SH /
+        SG rows).
+    Before the backward returns, its stream waits for the collectives and
+    gsr_view_color_grads_chunked rebuilds every SH / SG row as the sum over
+    the views (FactoredViewGrads' factorisation, the views summed in rank
+    order on every rank, so the replicas stay bit-identical).  The gradients
+    the rasterizer hands to autograd are then already summed over the
+    ranks' views; autograd carries them through the getters as usual.
+
+    Semantics: each rasterizer backward exchanges its own gradients, so
+    several renders per step and gradient accumulation sum correctly (the
+    exchange is linear).  Gradients of other loss terms on the same
+    parameters are NOT exchanged: reduce those yourself (or compute them on
+    every rank identically and scale).  means2D gradients (densification
+    statistics) stay per view.  `expand` replaces the HIP rebuild kernel (same
+    signature as _C.view_color_grads_chunked; CPU tests only).
+    """
+
+    def __init__(self, group: Optional[dist.ProcessGroup] = None, chunks: int = 4, expand=None):
+        self.group = group
+        self.chunks = max(1, int(chunks))
+        self.world = dist.get_world_size(group)
+        if expand is None:
+            from diff_gaussian_rasterization import _C
+            expand = _C.view_color_grads_chunked
+        self.expand = expand
+        self._dc = self._gathered = None
+        self._campos_local = self._campos_all = None
+        self._works = []
+        self._scales = self._sh = True
+        self._P = 0
+
+    # ---- installation -------------------------------------------------
+    def install(self) -> "OverlappedViewGrads":
+        import diff_gaussian_rasterization as dgr
+        dgr.set_view_exchange(self)
+        return self
+
+    def uninstall(self) -> None:
+        import diff_gaussian_rasterization as dgr
+        if dgr._view_exchange is self:
+            dgr.set_view_exchange(None)
+
+    def __enter__(self):
+        return self.install()
+
+    def __exit__(self, *exc):
+        self.uninstall()
+
+    # ---- the rasterizer backward's protocol ---------------------------
+    def dc_rows(self, P: int, device) -> torch.Tensor:
+        """The compact [P * 3] DC-row buffer the kernel writes (allocated once)."""
+        n = 3 * P
+        if self._dc is None or self._dc.numel() != n or self._dc.device != torch.device(device):
+            self._dc = torch.empty(n, dtype=torch.float32, device=device)
+            self._gathered = torch.empty(self.world * n, dtype=torch.float32, device=device)
+        return self._dc
+
+    def chunk_size(self, P: int) -> int:
+        return ((P + self.chunks - 1) // self.chunks + 255) // 256 * 256  # as gsr_rasterize_backward_ex
+
+    def begin(self, campos: torch.Tensor, P: int, scales_path: bool, sh_path: bool) -> None:
+        self._works = []
+        self._P, self._scales, self._sh = P, scales_path, sh_path
+        dev = campos.device
+        if self._campos_local is None or self._campos_local.device != dev:
+            self._campos_local = torch.zeros(4, dtype=torch.float32, device=dev)
+            self._campos_all = torch.empty(4 * self.world, dtype=torch.float32, device=dev)
+        self._campos_local[:3].copy_(campos.reshape(3))
+        if sh_path:
+            self._works.append(dist.all_gather_into_tensor(self._campos_all, self._campos_local, group=self.group,
+                                                           async_op=True))
+
+    def on_chunk(self, b: int, e: int, grads) -> None:
+        (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dsg_axis, dsg_sharpness, dsg_color, dscales,
+         drotations) = grads
+        rows = [dmeans3D[b:e], dopacity[b:e]]
+        rows += [dscales[b:e], drotations[b:e]] if self._scales else [dcov3D[b:e]]
+        if not self._sh:
+            rows.append(dcolors[b:e])
+        cm_fn = getattr(dist, "_coalescing_manager", None)
+        if cm_fn is None:
+            self._works += [dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True) for t in rows]
+        else:
+            with cm_fn(group=self.group, async_ops=True) as cm:
+                for t in rows:
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            self._works.append(cm)
+        if self._sh:
+            W = self.world
+            self._works.append(dist.all_gather_into_tensor(self._gathered[3 * W * b:3 * W * e], self._dc[3 * b:3 * e],
+                                                           group=self.group, async_op=True))
+
+    def finish(self, grads, means3D, sg_axis, sg_sharpness, sg_color, sh_degree: int, sg_degree: int) -> None:
+        for w in self._works:
+            w.wait()  # (RCCL: the backward's stream waits for the collective; no host synchronisation)
+        self._works = []
+        if not self._sh or self._P == 0:
+            return
+        (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dsg_axis, dsg_sharpness, dsg_color, dscales,
+         drotations) = grads
+        sg = [None if t is None or not t.numel() else t.detach() for t in (sg_axis, sg_sharpness, sg_color)]
+        self.expand(self._gathered, self._campos_all.view(self.world, 4), self.world, self.chunk_size(self._P),
+                    means3D.detach(), sh_degree, dsh, sg_degree, *sg,
+                    *[None if t is None or not t.numel() else t for t in (dsg_axis, dsg_sharpness, dsg_color)])
+
+
 def reduce_densification_stats(grad_norm_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
                                group: Optional[dist.ProcessGroup] = None) -> None:
     """Densification statistics of the views seen since the last densify step

@@ -52,6 +52,9 @@ enum gsr_status {
 
 /* Replaces std::function<char*(size_t)> (rasterizer.h:30-33, rasterize_points.cu:27-37). */
 typedef void* (*gsr_alloc_fn)(void* ctx, size_t bytes);
+/* Host callback of gsr_rasterize_backward_ex after each Gaussian range [begin, end) of the
+ * per-Gaussian backward has been queued on the call's stream. */
+typedef void (*gsr_chunk_fn)(void* ctx, int begin, int end);
 
 /*
  * Replaces CudaRasterizer::Rasterizer::forward (rasterizer.h:29-61,
@@ -119,6 +122,36 @@ int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int 
                            float* dL_dscale, float* dL_drot, float* dL_dcov3D, float* dL_dsh, float* dL_dsg_axis,
                            float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
                            void* stream);
+
+/*
+ * gsr_rasterize_backward with the per-Gaussian backward split into `chunks`
+ * consecutive Gaussian ranges (no reference equivalent: the view-parallel
+ * training step).  After each range's kernel is queued on
+ * `stream`, on_chunk(chunk_ctx, begin, end) runs on the calling thread, so
+ * the caller can post that range's gradient exchange on another stream while
+ * the next range computes (gsr_dist.OverlappedViewGrads).  The ranges hold
+ * ceil(ceil(P / chunks) / 256) * 256 Gaussians each (the last one fewer).  With dc_rows
+ * non-NULL ([P][3] floats, SH colour path only) the kernel writes each
+ * Gaussian's DC gradient row dL/dsh[:, 0, :] there and leaves dL_dsh and the
+ * SG gradient rows unwritten: gsr_view_color_grads_chunked rebuilds them from
+ * every view's DC rows.  chunks = 1, on_chunk = NULL, dc_rows = NULL is
+ * gsr_rasterize_backward.
+ */
+int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
+                              int sg_degree, int SGM, int R, const float* background, int width, int height,
+                              const float* means3D, const float* colors_precomp, const float* opacities,
+                              const float* scales, const float* rotations, const float* cov3D_precomp,
+                              const float* shs, const float* sg_axis, const float* sg_sharpness,
+                              const float* sg_color, float scale_modifier, const float* viewmatrix,
+                              const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                              float kernel_size, const int* radii, const float* alphas, const float* normalmap,
+                              const float* mdepth, const void* geom_buffer, const void* binning_buffer,
+                              const void* image_buffer, const void* tile_buffer, const float* dL_dpix,
+                              const float* dL_dpix_mdepth, const float* dL_dalphas, const float* dL_dpixel_normals,
+                              float* dL_dmean3D, float* dL_dmean2D, float* dL_dcolor, float* dL_dopacity,
+                              float* dL_dscale, float* dL_drot, float* dL_dcov3D, float* dL_dsh, float* dL_dsg_axis,
+                              float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
+                              int chunks, gsr_chunk_fn on_chunk, void* chunk_ctx, float* dc_rows, void* stream);
 
 /* Replaces CudaRasterizer::Rasterizer::markVisible (rasterizer.h:21-27,
  * rasterizer_impl.cu:186-197): present[i] = (view-space z > 0.2). */
@@ -281,6 +314,18 @@ int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_ra
  * when SGM > 0 dL_dsg_axis [P, SGM, 3], dL_dsg_sharpness [P, SGM],
  * dL_dsg_color [P, SGM, 3] (lobes past sg_degree zero); sg_degree <= 7.
  */
+/*
+ * gsr_view_color_grads for the layout gsr_dist.OverlappedViewGrads gathers
+ * range by range: the Gaussians in ranges of `chunk` (the last shorter);
+ * range [b, b + len) occupies gathered[3 n_views b, 3 n_views (b + len)) as
+ * [n_views][len][3] DC rows; the camera centres are campos [n_views][4].
+ */
+int gsr_view_color_grads_chunked(int P, int sh_degree, int SHM, int sg_degree, int SGM, int n_views, int chunk,
+                                 const float* gathered, const float* campos, const float* means3D,
+                                 const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                                 float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness, float* dL_dsg_color,
+                                 void* stream);
+
 int gsr_view_color_grads(int P, int sh_degree, int SHM, int sg_degree, int SGM, int n_views, const float* gathered,
                          const float* means3D, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
                          float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness, float* dL_dsg_color,
@@ -401,6 +446,9 @@ const char* gsr_stage_name(int stage);
  * (render_bwd.hip). */
 /* GSR_OPT_ROCPRIM_DSORT (A/B, default 0): the depth order by rocPRIM's onesweep
  * radix sort instead of dsort.hip's (same order). */
+/* GSR_OPT_PBWD_STAGE (A/B): the per-Gaussian backward's SH / SG-7 gradient rows
+ * written through LDS as whole-wave stores (1) or per lane (2); 0 = the build's
+ * default (GSR_PBWD_STAGE_DEFAULT). */
 /* GSR_OPT_NO_REFINE (A/B, default 0): find the median depth with the reference's
  * five bisection passes only, instead of two passes plus the bracketed Halley
  * refinement (render_fwd.hip; results agree to ~1e-7 of the depth, not bitwise). */
@@ -414,7 +462,8 @@ enum gsr_option {
     GSR_OPT_BWD_NO_CACHE = 6,
     GSR_OPT_SORTBIN = 7,
     GSR_OPT_BWD_NARROW = 8,
-    GSR_OPT_ROCPRIM_DSORT = 9
+    GSR_OPT_ROCPRIM_DSORT = 9,
+    GSR_OPT_PBWD_STAGE = 10
 };
 int gsr_set_option(int opt, int value);
 /* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (8 values, see render_fwd.hip). */

@@ -97,8 +97,8 @@ def set_threads(n: int) -> None:
 
 
 def set_exp_mode(mode: int) -> None:
-    """0: libm expf (default); 1: exp2f(x * log2e) in fp32, the form the
-    reference's --use_fast_math build compiles expf to (gsr_oracle.c header)."""
+    """1 (default): exp2f(x * log2e) in fp32, the form the reference's
+    --use_fast_math build compiles expf to; 0: libm expf (gsr_oracle.c header)."""
     lib().gsro_set_exp_mode(int(mode))
 
 

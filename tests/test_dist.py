@@ -191,3 +191,60 @@ def test_factored_exchange_sums_views(tmp_path):
         want = (g0[name].grad + g1[name].grad).float()
         assert torch.equal(f0[name], f1[name]), name
         torch.testing.assert_close(f0[name], want, rtol=1e-5, atol=1e-7)
+
+
+# ---- the exchange inside the backward, range by range (gsr_dist.OverlappedViewGrads) ----
+def _expand_chunked_ref(gathered, campos, n_views, chunk, means3D, sh_degree, dL_dsh, sg_degree=0, *_sg):
+    """_expand_ref for the range-by-range gathered layout (include/gsr.h
+    gsr_view_color_grads_chunked): range [b, b+len) holds [n_views][len][3]."""
+    P = means3D.shape[0]
+    dc = torch.empty(n_views, P, 3, dtype=gathered.dtype)
+    for b in range(0, P, chunk):
+        e = min(P, b + chunk)
+        dc[:, b:e] = gathered[3 * n_views * b:3 * n_views * e].view(n_views, e - b, 3)
+    legacy = torch.cat([torch.cat([dc[v].reshape(-1), campos[v]]) for v in range(n_views)])
+    _expand_ref(legacy, n_views, means3D, sh_degree, dL_dsh)
+
+
+def _overlap_worker(rank, world, port, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd"), HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gsr_scene as S
+    from gsr_dist import OverlappedViewGrads
+
+    inp = _view_grads(rank)
+    P = 30
+    campos = S.orbit_cameras(2, 32, 24, center_z=3.0, max_deg=10.0)[rank].camera_center.float()
+    g = {k: inp[k].grad.float().clone() for k in ("means3D", "opacities", "scales", "rotations", "shs")}
+    z = lambda *s: torch.zeros(*s)  # noqa: E731
+    # the rasterizer's 11 outputs as _C.rasterize_gaussians_backward returns them (dsh left for the rebuild)
+    grads = (z(P, 3), z(P, 3), g["opacities"].clone(), g["means3D"].clone(), z(P, 6), torch.full((P, 16, 3), 7.0),
+             z(P, 0, 3), z(P, 0), z(P, 0, 3), g["scales"].clone(), g["rotations"].clone())
+    ex = OverlappedViewGrads(chunks=4, expand=_expand_chunked_ref)
+    ex.chunk_size = lambda P_: 8  # (the HIP backward's ranges are whole 256-Gaussian workgroups; 30 Gaussians here)
+    ex.begin(campos, P, True, True)
+    ex.dc_rows(P, "cpu").copy_(g["shs"][:, 0, :].reshape(-1))  # what the kernel writes in DC-row mode
+    cs = ex.chunk_size(P)
+    for b in range(0, P, cs):  # as gsr_rasterize_backward_ex calls on_chunk
+        ex.on_chunk(b, min(P, b + cs), grads)
+    ex.finish(grads, inp["means3D"].detach().float(), None, None, None, 3, 0)
+    torch.save({"means3D": grads[3], "opacities": grads[2], "scales": grads[9], "rotations": grads[10],
+                "shs": grads[5]}, os.path.join(outdir, f"o{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_exchange_sums_views(tmp_path):
+    """OverlappedViewGrads' range-by-range protocol (geometry rows all-reduced
+    and DC rows all-gathered per Gaussian range, colour rows rebuilt at the
+    end) gives both ranks the sum over views of every gradient, identically."""
+    port = _free_port()
+    mp.start_processes(_overlap_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    o0 = torch.load(tmp_path / "o0.pt", weights_only=True)
+    o1 = torch.load(tmp_path / "o1.pt", weights_only=True)
+    g0, g1 = _view_grads(0), _view_grads(1)
+    for name in ("means3D", "opacities", "scales", "rotations", "shs"):
+        want = (g0[name].grad + g1[name].grad).float()
+        assert torch.equal(o0[name], o1[name]), name
+        torch.testing.assert_close(o0[name], want, rtol=1e-5, atol=1e-7)

@@ -191,3 +191,57 @@ def test_factored_exchange_contract_guards(tmp_path):
             ex.exchange(cam.camera_center, 3)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sg_degree,chunks", [(0, 3), (7, 4), (0, 1)])
+def test_overlapped_exchange_one_rank_matches_plain_backward(tmp_path, sg_degree, chunks):
+    """gsr_dist.OverlappedViewGrads through RCCL on a one-rank group: the
+    rasterizer backward runs its per-Gaussian tail in Gaussian ranges (the
+    DC-row mode of gsr_rasterize_backward_ex), every range's geometry rows
+    all-reduced and DC rows all-gathered as it is queued, the SH / SG rows
+    rebuilt at the end — and the parameters' gradients equal those of the
+    plain backward (geometry to the render backward's atomic order, colour
+    rows to fp32 rounding of the rebuild)."""
+    import math
+
+    import gsr_scene as S
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gsr_dist import OverlappedViewGrads
+
+    dev = torch.device("cuda", 0)
+    P, W, H = 20000, 320, 240
+    raw = S.make_gaussians(P, sg_degree=sg_degree, seed=7, aspect=H / W, z_range=(2.0, 6.0))
+    inp = {k: v.detach().contiguous().to(dev) for k, v in S.activated_inputs(raw).items()}
+    cam = S.make_camera(W, H).to(dev)
+    settings = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2),
+        kernel_size=0.0, bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam.world_view_transform,
+        projmatrix=cam.full_proj_transform, sh_degree=3, sg_degree=sg_degree, campos=cam.camera_center,
+        prefiltered=False, require_depth=True, debug=False)
+    g = {k: v.to(dev) for k, v in S.upstream_grads(H, W, seed=4).items()}
+
+    def step():
+        ps = {k: t.clone().requires_grad_(True) for k, t in inp.items()}
+        color, radii, mdepth, alpha, normal = GaussianRasterizer(settings)(
+            means3D=ps["means3D"], means2D=torch.zeros(P, 3, device=dev, requires_grad=True),
+            opacities=ps["opacities"], shs=ps["shs"], sg_axis=ps["sg_axis"], sg_sharpness=ps["sg_sharpness"],
+            sg_color=ps["sg_color"], scales=ps["scales"], rotations=ps["rotations"])
+        torch.autograd.backward([color, mdepth, normal], [g["color"], g["mdepth"], g["normal"]])
+        torch.cuda.synchronize()
+        return {k: t.grad for k, t in ps.items()}
+
+    plain = step()
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        with OverlappedViewGrads(chunks=chunks):
+            over = step()
+    finally:
+        dist.destroy_process_group()
+    for k in plain:
+        want, got = plain[k].double(), over[k].double()
+        if want.numel() == 0:
+            continue
+        assert bool(torch.isfinite(got).all()), k
+        err = float((got - want).norm() / want.norm().clamp_min(1e-30))
+        assert err <= 1e-5, (k, err)

@@ -4,15 +4,23 @@ API) against the C oracle on identical seeded inputs.
 Tolerances (north star: 1e-4 relative on identical inputs):
   * integer outputs (num_rendered, radii, n_contrib-driven structure): exact;
   * images (color, alpha, normal, median depth): max|a-b| / max|b| <= 1e-4;
-  * gradients: ||a-b|| / ||b|| <= 1e-4 and max|a-b| / max|b| <= 1e-3.  The
-    oracle backward is fed the GPU's own forward images (alpha, normal,
-    mdepth are inputs of the reference backward, rasterize_points.cu:166-168),
-    so the comparison isolates the backward kernels; per-Gaussian sums are
+  * gradients: ||a-b|| / ||b|| <= 1e-4 and max|a-b| / max|b| <= 1e-4.  The
+    oracle backward runs on the GPU forward's state: its images (alpha,
+    normal, mdepth are inputs of the reference backward,
+    rasterize_points.cu:166-168) and its per-pixel last contributors (mapped
+    into the oracle's tile lists, helpers.gpu_n_contrib_for_oracle), so the
+    comparison isolates the backward kernels; per-Gaussian sums are
     accumulated by float atomics on the GPU (order-dependent at ~1 ulp, as
-    in the reference) and in double in the oracle.
-Full-size (C3: 1M Gaussians, 1080p) checks use size-independent properties:
-determinism, radii/K equality with the oracle preprocess, tile-sampled image
-parity and linearity of the backward in the upstream gradients.
+    in the reference) and in double in the oracle.  test_float64_yardstick
+    checks on small scenes that the GPU's gradients are no further from an
+    exact float64 evaluation than the oracle's own fp32 ones.
+Scenes: opacity logits are capped at 2 except in the clamp cases (logits up
+to 6, and the uncapped bench scene at full size), where alpha = min(0.99,
+o G) clamps and the reference's pass-through gradient is exercised; the SH
+warm-up cases render 16 SH rows at active degree 0, 1, 2 (train.py:130).
+Full size (C2, C3, C5): K, radii and the per-tile lists exact, every pixel
+of every image against the oracle, every per-Gaussian gradient against the
+oracle backward on the GPU forward's state.
 """
 from __future__ import annotations
 
@@ -113,14 +121,25 @@ def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True)
         return
     g = S.upstream_grads(c["H"], c["W"])
     g["alpha"] = torch.randn(1, c["H"], c["W"], generator=torch.Generator().manual_seed(5)) * 1e-3
-    al, nm, md = alpha.cpu(), normal.cpu(), mdepth.cpu()
-    b = O.backward(o["state"], *a[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], al, nm, md,
-                   c["cam"].camera_center, o["radii"])
+    b = _oracle_backward_on_gpu_state(c, a, out, o, g)
     gb = _C.rasterize_gaussians_backward(*ga[:19], _gpu(g["color"]), _gpu(g["mdepth"]), _gpu(g["alpha"]),
                                          _gpu(g["normal"]), alpha, normal, mdepth, _gpu(c["cam"].camera_center),
                                          radii, out[6], K, out[7], out[8], out[9], geom, False)
+    _check_grads(gb, b)
+    return out, o, g, gb
+
+
+def _oracle_backward_on_gpu_state(c, a, out, o, g):
+    """The oracle backward on the GPU forward's state: its images and its
+    per-pixel last contributors (mapped into the oracle's tile lists)."""
+    o["state"].set_n_contrib(Hh.gpu_n_contrib_for_oracle(out, o, c["H"], c["W"]))
+    return O.backward(o["state"], *a[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], out[2].cpu(),
+                      out[3].cpu(), out[4].cpu(), c["cam"].camera_center, o["radii"])
+
+
+def _check_grads(gb, b, l2_bar=1e-4, max_bar=1e-4, report=None):
     for name, t in zip(GRAD_NAMES, gb):
-        mine, ref = t.cpu().numpy().astype(np.float64), b[name]
+        mine, ref = t.cpu().numpy().astype(np.float64), b[name].astype(np.float64)
         assert mine.shape == ref.shape, name
         if ref.size == 0:
             continue
@@ -128,8 +147,11 @@ def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True)
             assert not np.any(mine), name
             continue
         l2 = np.linalg.norm(mine - ref) / np.linalg.norm(ref)
-        assert l2 <= 1e-4, (name, l2)
-        assert Hh.rel_err(mine, ref) <= 1e-3, (name, Hh.rel_err(mine, ref))
+        mx = Hh.rel_err(mine, ref)
+        if report is not None:
+            report[name] = (l2, mx)
+        assert l2 <= l2_bar, (name, l2)
+        assert mx <= max_bar, (name, mx)
 
 
 SMALL = [
@@ -148,6 +170,13 @@ SMALL = [
     dict(P=2000, W=96, H=64, seed=12, flat=20.0),
     # 1025 tiles across: the instance-sort binning path (binning.hip) instead of tile lists
     dict(P=600, W=16400, H=40, seed=9, log_scale=math.log(0.01)),
+    # the alpha = 0.99 clamp: logits up to 6 (o up to 0.9975), its pass-through gradient
+    dict(P=400, W=64, H=48, seed=40, opacity_max_logit=6.0, opacity_std=3.0),
+    dict(P=10000, W=256, H=256, seed=44, log_scale=math.log(0.03), opacity_max_logit=6.0, opacity_std=3.0),
+    # the SH warm-up layout (train.py:130, gaussian_model.py:264-266): 16 SH rows at active degree 0, 1, 2
+    dict(P=400, W=64, H=48, seed=41, sh_degree=0, sh_max_degree=3),
+    dict(P=400, W=64, H=48, seed=42, sh_degree=1, sh_max_degree=3),
+    dict(P=400, W=64, H=48, seed=43, sh_degree=2, sh_max_degree=3),
 ]
 
 
@@ -155,7 +184,72 @@ SMALL = [
 def test_parity_small(case):
     case = dict(case)
     ks = case.pop("kernel_size", 0.0)
-    _run(Hh.small_case(kernel_size=ks, **case))
+    c = Hh.small_case(kernel_size=ks, **case)
+    _, _, _, gb = _run(c)
+    if case.get("opacity_max_logit", 2.0) > 4.6:  # the scene reaches the clamp
+        assert int((c["inp"]["opacities"] > 0.99).sum()) > 0
+    if case.get("sh_max_degree"):  # SH rows past the active degree get exactly zero
+        dsh = gb[5].cpu().numpy()
+        assert dsh.shape[1] == 16 and not np.any(dsh[:, (c["sh_degree"] + 1) ** 2:])
+
+
+YARDSTICK = [dict(P=300, W=64, H=48, seed=1), dict(P=400, W=64, H=48, seed=40, opacity_max_logit=6.0, opacity_std=3.0),
+             dict(P=400, W=64, H=48, seed=42, sh_degree=1, sh_max_degree=3),
+             dict(P=300, W=64, H=48, seed=10, sgm=7, sg_degree=7)]
+
+
+@pytest.mark.parametrize("case", YARDSTICK, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_float64_yardstick(case):
+    """The GPU's gradients against an exact float64 autograd evaluation of
+    the same scene (tests/torch_ref.py, the reference's quirks Q1-Q5
+    included), at the GPU's own median depths: no further from it than 2x
+    the oracle's fp32 gradients (+1e-6 of the largest gradient, the
+    float-atomic order), and within 1e-4 of it outright.  This is the
+    yardstick that says the 1e-4 bars above measure parity, not rounding."""
+    import torch_ref as R
+    from diff_gaussian_rasterization import _C
+
+    c = Hh.small_case(**case)
+    a = _fwd_args(c)
+    o = O.forward(*a)
+    ga = [_gpu(x) for x in a] + [False]
+    out = _C.rasterize_gaussians(*ga)
+    K, color, alpha, normal, mdepth, radii = out[:6]
+    g = S.upstream_grads(c["H"], c["W"])
+    b = _oracle_backward_on_gpu_state(c, a, out, o, g)
+    gb = _C.rasterize_gaussians_backward(*ga[:19], _gpu(g["color"]), _gpu(g["mdepth"]), _gpu(g["alpha"]),
+                                         _gpu(g["normal"]), alpha, normal, mdepth, _gpu(c["cam"].camera_center),
+                                         radii, out[6], K, out[7], out[8], out[9], True, False)
+    P = c["inp"]["means3D"].shape[0]
+    inp = {k: v.double().clone().requires_grad_(True) for k, v in c["inp"].items()}
+    m2d = torch.zeros(P, 3, dtype=torch.float64, requires_grad=True)
+    cam = c["cam"]
+    pre = R.preprocess(inp["means3D"], inp["scales"], inp["rotations"], inp["opacities"], inp["shs"],
+                       inp["sg_axis"], inp["sg_sharpness"], inp["sg_color"], m2d, cam.world_view_transform.double(),
+                       cam.full_proj_transform.double(), cam.camera_center.double(), c["W"], c["H"], c["tanx"],
+                       c["tany"], 0.0, c["sh_degree"], c["sg_degree"])
+    lists, _ = R.binning(pre, c["W"], c["H"])
+    ref = R.render(pre, lists, c["W"], c["H"], c["bg"].double(), mdepth_override=mdepth.cpu().double())
+    L = ((ref["color"] * g["color"].double()).sum() + (ref["normal"] * g["normal"].double()).sum()
+         + R.median_depth_surrogate(ref, g["mdepth"].double()))
+    L.backward()
+    q = c["inp"]["rotations"].double().numpy()
+    tang = lambda v: v - q * (q * v).sum(1, keepdims=True)  # noqa: E731 - dL/dq is defined up to the radial part
+    exact = {"dmeans3D": inp["means3D"].grad.numpy(), "dscales": inp["scales"].grad.numpy(),
+             "drotations": tang(inp["rotations"].grad.numpy()), "dopacity": inp["opacities"].grad.numpy(),
+             "dsh": inp["shs"].grad.numpy(), "dmeans2D": m2d.grad[:, :2].numpy()}
+    if c["sg_degree"]:
+        exact.update(dsg_axis=inp["sg_axis"].grad.numpy(), dsg_sharpness=inp["sg_sharpness"].grad.numpy(),
+                     dsg_color=inp["sg_color"].grad.numpy())
+    gpu = dict(zip(GRAD_NAMES, [t.cpu().double().numpy() for t in gb]))
+    gpu["drotations"], b["drotations"] = tang(gpu["drotations"]), tang(b["drotations"].astype(np.float64))
+    gpu["dmeans2D"], b["dmeans2D"] = gpu["dmeans2D"][:, :2], b["dmeans2D"][:, :2]
+    for name, e in exact.items():
+        e_gpu = Hh.rel_err(gpu[name], e)
+        e_orc = Hh.rel_err(b[name], e)
+        print(f"{name}: gpu-vs-f64 {e_gpu:.2e}  oracle-vs-f64 {e_orc:.2e}")
+        assert e_gpu <= 2 * e_orc + 1e-6, (name, e_gpu, e_orc)
+        assert e_gpu <= 1e-4, (name, e_gpu)
 
 
 @pytest.mark.parametrize("case", [SMALL[1], SMALL[6], SMALL[8]], ids=["geom", "nogeom", "C1"])
@@ -171,6 +265,24 @@ def test_parity_backward_narrow(case):
         _run(Hh.small_case(kernel_size=ks, **case))
     finally:
         _C.set_option(_C.OPT_BWD_NARROW, 0)
+
+
+@pytest.mark.parametrize("stage", [1, 2], ids=["staged", "per-lane"])
+@pytest.mark.parametrize("case", [dict(P=3001, W=96, H=64, seed=50, sgm=7, sg_degree=7),
+                                  dict(P=2999, W=96, H=64, seed=51), dict(P=37, W=40, H=24, seed=52, sgm=7, sg_degree=7),
+                                  dict(P=500, W=64, H=48, seed=53, sh_degree=1, sh_max_degree=3)],
+                         ids=["sg7-ragged", "sh3-ragged", "sg7-one-wave", "sh1-of-16"])
+def test_parity_row_store_paths(case, stage):
+    """The per-Gaussian backward's two ways of writing the SH / SG-7 gradient
+    rows (GSR_OPT_PBWD_STAGE: through LDS as whole-wave stores, or per lane)
+    against the oracle, on ragged Gaussian counts (partial last waves)."""
+    from diff_gaussian_rasterization import _C
+
+    _C.set_option(_C.OPT_PBWD_STAGE, stage)
+    try:
+        _run(Hh.small_case(**case))
+    finally:
+        _C.set_option(_C.OPT_PBWD_STAGE, 0)
 
 
 def _with_depth_ties(c, n_tied):

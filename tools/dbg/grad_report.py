@@ -94,7 +94,7 @@ def report(c, tag, variants=("own",)):
             results["libm_own"] = O.backward(o2["state"], *args[:19], gr["color"], gr["mdepth"], gr["alpha"],
                                              gr["normal"], o2["alpha"], o2["normal"], o2["mdepth"],
                                              c["cam"].camera_center, o2["radii"])
-    O.set_exp_mode(0)
+    O.set_exp_mode(1)
     if "spread" in variants:
         compare([results["libm_own"][n] for n in NAMES], results["fm_own"], op, radii.cpu().numpy(),
                 "SPREAD oracle(libm) vs oracle(fast-math), each on its own forward")

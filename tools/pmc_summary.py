@@ -113,6 +113,18 @@ def main():
                    "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE"):
             for st, v in per_stage_counter(sq_csv, cn, ns).items():
                 sq.setdefault(st, {})[cn] = v
+    # memory-path pass (optional): L2 requests / busy / tag stalls and TA busy
+    mem = {}
+    for sub, counters in (("tcc", ("TCC_REQ_sum", "TCC_BUSY_avr", "TCC_TAG_STALL_sum", "TCC_HIT_sum",
+                                   "GRBM_GUI_ACTIVE")),
+                          ("ta", ("TA_BUSY_avr", "TA_TA_BUSY_sum", "GRBM_GUI_ACTIVE"))):
+        path = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        nm = launches(path, "GRBM_GUI_ACTIVE")
+        for cn in counters:
+            for st, v in per_stage_counter(path, cn, nm).items():
+                mem.setdefault(st, {})[cn if cn != "GRBM_GUI_ACTIVE" else f"GRBM_GUI_ACTIVE_{sub}"] = v
     stages = {}
     ncalls_trace = defaultdict(int)
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
@@ -133,6 +145,8 @@ def main():
         stages[st] = {"avg_call_ms": round(avg_ns / 1e6, 4), "max_call_ms": round(calls[-1] / 1e6, 4),
                       "calls": len(calls), "dispatches_per_call": per_call,
                       "fetch_kib_per_call": f, "write_kib_per_call": w, "hbm_bytes_per_launch": hbm}
+        if st in mem:
+            stages[st]["mem_per_call"] = mem[st]
         if st in sq:
             c = sq[st]
             stages[st]["sq_per_call"] = c

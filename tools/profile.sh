@@ -2,7 +2,8 @@
 # rocprofv3 passes for bench.py (run on the GPU box from the repo root):
 #   1. kernel trace + stats  2. --pmc FETCH_SIZE  3. --pmc WRITE_SIZE
 #   4. --pmc SQ instruction/cycle counters (VALU busy of the VALU-bound raster)
-#   5. kernel trace + stats of tools/bench_sample.py (sample_depth kernels)
+#   5. --pmc L2 requests / busy / tag stalls / hits   6. --pmc TA busy
+#   7. kernel trace + stats of tools/bench_sample.py (sample_depth kernels; default workload only)
 # (counters in their own passes; never combined with other trace domains).
 # Output: gpurun_out/prof_<tag>/..., summarised by tools/pmc_summary.py.
 #   bash tools/profile.sh <tag> [bench.py workload args, e.g. --config C5 | --no-depth]
@@ -21,6 +22,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $SHORT > $OUT/fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $SHORT > $OUT/write.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- python3 $SHORT > $OUT/sq.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc TCC_REQ_sum TCC_BUSY_avr TCC_TAG_STALL_sum TCC_HIT_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/tcc -o run -- python3 $SHORT > $OUT/tcc.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc TA_BUSY_avr TA_TA_BUSY_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/ta -o run -- python3 $SHORT > $OUT/ta.log 2>&1 && \
 if [ -z "$WL" ]; then timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sample -o run -- python3 $ROOT/tools/bench_sample.py 10 > $OUT/sample.log 2>&1; fi
 rc=$?
 cd $ROOT
