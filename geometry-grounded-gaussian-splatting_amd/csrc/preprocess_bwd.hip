@@ -102,14 +102,14 @@ __device__ __forceinline__ void sg7_load(const PreprocessBwdArgs& a, int idx, SG
     load_row(a.sg_color + 3 * o0, r.gc);
     load_row(a.sg_sharpness + o0, r.sharp);
 }
-// Staged row stores (GSR_OPT_PBWD_STAGE): per wave, LDS rows for its 64
-// Gaussians — the SG-7 gradient rows (colour 21, sharpness 7, axis 21 floats
-// each), then, reusing the space, the SH gradient rows (48 floats each) —
-// written out by wave_store_rows.
+// Staged rows (GSR_OPT_PBWD_STAGE): per wave, LDS rows for its 64 Gaussians
+// in the global layout — the SG-7 lobe rows (colour 21, sharpness 7, axis 21
+// floats each), loaded by LDS-DMA, replaced in place by their gradient rows
+// and written out by wave_store_rows; then, reusing the space, the SH
+// gradient rows (48 floats each).
 constexpr int kStageColor = 0, kStageSharp = 64 * 21, kStageAxis = 64 * 28, kStageFloats = 64 * 49;
 __device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, const SG7Rows& rows, float x, float y,
-                                        float z, float dR0, float dR1, float dR2, float& ddx, float& ddy, float& ddz,
-                                        float* stage = nullptr, int lane = 0) {
+                                        float z, float dR0, float dR1, float dR2, float& ddx, float& ddy, float& ddz) {
     const size_t o0 = (size_t)idx * kSG7;
     const float* ax = rows.ax;
     const float* gc = rows.gc;
@@ -136,18 +136,59 @@ __device__ __forceinline__ void sg7_bwd(const PreprocessBwdArgs& a, int idx, con
         ddz += dL_daux * axs[2];
     }
     if (a.dc_rows) return;  // (rows rebuilt by the view exchange)
-    if (stage) {  // this lane's slots of the wave's LDS rows (stage_rows)
-#pragma unroll
-        for (int k = 0; k < 3 * kSG7; k++) stage[kStageColor + 3 * kSG7 * lane + k] = dcol[k];
-#pragma unroll
-        for (int k = 0; k < kSG7; k++) stage[kStageSharp + kSG7 * lane + k] = dsh[k];
-#pragma unroll
-        for (int k = 0; k < 3 * kSG7; k++) stage[kStageAxis + 3 * kSG7 * lane + k] = dax[k];
-        return;
-    }
     store_row(a.dL_dsg_color + 3 * o0, dcol);
     store_row(a.dL_dsg_sharpness + o0, dsh);
     store_row(a.dL_dsg_axis + 3 * o0, dax);
+}
+
+// (STAGE) SG-7 backward on the wave's LDS rows: slot `slot` of the lobe rows
+// loaded by wave_load_rows; the gradient rows replace them in place (every
+// input is read before the first write, in the same lockstep instructions).
+__device__ __forceinline__ void sg7_bwd_slots(float* stage, int slot, float x, float y, float z, float dR0, float dR1,
+                                              float dR2, float& ddx, float& ddy, float& ddz) {
+    float* col = stage + kStageColor + 3 * kSG7 * slot;
+    float* shp = stage + kStageSharp + kSG7 * slot;
+    float* axs = stage + kStageAxis + 3 * kSG7 * slot;
+    float dcol[3 * kSG7], dax[3 * kSG7], dsh[kSG7];
+#pragma unroll
+    for (int sg = 0; sg < kSG7; sg++) {
+        const float a0 = axs[3 * sg], a1 = axs[3 * sg + 1], a2 = axs[3 * sg + 2];
+        const float sharp = shp[sg];
+        const float auxs = (a0 * x + a1 * y + a2 * z) - 1.0f;
+        const float gs = expf(sharp * auxs);
+        dcol[3 * sg + 0] = dR0 * gs;
+        dcol[3 * sg + 1] = dR1 * gs;
+        dcol[3 * sg + 2] = dR2 * gs;
+        const float dL_dgs = col[3 * sg] * dR0 + col[3 * sg + 1] * dR1 + col[3 * sg + 2] * dR2;
+        const float dL_dexp = dL_dgs * gs;
+        dsh[sg] = dL_dexp * auxs;
+        const float dL_daux = dL_dexp * sharp;
+        dax[3 * sg + 0] = dL_daux * x;
+        dax[3 * sg + 1] = dL_daux * y;
+        dax[3 * sg + 2] = dL_daux * z;
+        ddx += dL_daux * a0;
+        ddy += dL_daux * a1;
+        ddz += dL_daux * a2;
+    }
+#pragma unroll
+    for (int k = 0; k < 3 * kSG7; k++) col[k] = dcol[k];
+#pragma unroll
+    for (int k = 0; k < kSG7; k++) shp[k] = dsh[k];
+#pragma unroll
+    for (int k = 0; k < 3 * kSG7; k++) axs[k] = dax[k];
+}
+
+// A wave's nf consecutive floats (rows of its Gaussians) into LDS by LDS-DMA
+// (global_load_lds_dwordx4: one instruction moves 1 KB of consecutive bytes,
+// no VGPR destination); the tail past the last whole 16-B piece by plain loads.
+__device__ __forceinline__ void wave_load_rows(const float* __restrict__ g, float* l, int nf, int lane) {
+    const int n4 = nf >> 2;
+    for (int c0 = 0; c0 < n4; c0 += 64) {
+        if (c0 + lane < n4)
+            __builtin_amdgcn_global_load_lds((const void*)(g + 4 * (c0 + lane)),
+                                             (__attribute__((address_space(3))) void*)(l + 4 * c0), 16, 0, 0);
+    }
+    for (int c = (n4 << 2) + lane; c < nf; c += 64) l[c] = g[c];
 }
 
 // A wave's n consecutive rows of nf floats each, staged in LDS in the
@@ -162,8 +203,11 @@ __device__ __forceinline__ void wave_store_rows(float* __restrict__ g, const flo
 #ifndef GSR_PBWD_WAVES
 #define GSR_PBWD_WAVES 0
 #endif
+#ifndef GSR_PBWD_STAGE_WAVES
+#define GSR_PBWD_STAGE_WAVES 3
+#endif
 #ifndef GSR_PBWD_STAGE_DEFAULT
-#define GSR_PBWD_STAGE_DEFAULT 0
+#define GSR_PBWD_STAGE_DEFAULT 1  // staged row stores: C5 preprocess_bwd 1.18-1.22 -> 0.91-0.93 ms, C3 0.151 -> 0.122
 #endif
 // STAGE (SH rows of 16 coefficients, launch ranges in whole workgroups): the
 // SH and SG-7 gradient rows go out through LDS as whole-wave stores.  Every
@@ -175,12 +219,19 @@ template <bool STAGE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_PBWD_WAVES, 8)))
 preprocess_bwd_kernel(PreprocessBwdArgs a) {
 #else
-__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a) {
+// (STAGE: the lobe rows live in LDS, not VGPRs: 3 waves per SIMD fit (168 VGPRs, 6 spilled); LDS 49 KB
+// per block, 3 blocks per CU)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGE ? GSR_PBWD_STAGE_WAVES : 1, 8)))
+preprocess_bwd_kernel(PreprocessBwdArgs a) {
 #endif
     const int idx0 = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
-    if (!STAGE && idx0 >= a.end) return;
-    const int idx = idx0 < a.end ? idx0 : a.begin;
     const int lane = threadIdx.x & 63;
+    const int wbase = idx0 - lane;  // the wave's first Gaussian
+    if (!STAGE && idx0 >= a.end) return;
+    if (STAGE && wbase >= a.end) return;  // (a whole wave past the range takes no part in anything)
+    // (STAGE: a lane past the range duplicates the wave's first Gaussian: same values, same addresses)
+    const int idx = idx0 < a.end ? idx0 : (STAGE ? wbase : a.begin);
+    const int slot = idx - wbase;  // (STAGE) the Gaussian's row slot in the wave's LDS rows
     __shared__ float s_stage[STAGE ? 4 * kStageFloats : 1];
     float* stage = s_stage + (STAGE ? (threadIdx.x >> 6) * kStageFloats : 0);
     // (STAGE) what the SH rows need, left by the visible-Gaussian body: direction and clamp-masked dL/dRGB
@@ -219,7 +270,15 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     // (SG degree 7: the 196-B lobe rows as well; 2 waves per SIMD fit them)
     const bool sg7 = a.shs && a.SGM == kSG7 && a.SGD == kSG7;
     SG7Rows sgr;
-    if (sg7) sg7_load(a, idx, sgr);
+    if (STAGE && sg7) {  // the wave's lobe rows into its LDS slots, by LDS-DMA (read after the geometry chain)
+        const int n = min(64, a.end - wbase);
+        const size_t o = (size_t)wbase * kSG7;
+        wave_load_rows(a.sg_color + 3 * o, stage + kStageColor, n * 3 * kSG7, lane);
+        wave_load_rows(a.sg_sharpness + o, stage + kStageSharp, n * kSG7, lane);
+        wave_load_rows(a.sg_axis + 3 * o, stage + kStageAxis, n * 3 * kSG7, lane);
+    } else if (sg7) {
+        sg7_load(a, idx, sgr);
+    }
 #endif
     // extension outputs straight from the accumulator (zero for culled
     // Gaussians); sample_depth returns neither (rasterize_points.cu:633)
@@ -624,7 +683,12 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         float ddz = gdz[0] * dR0 + gdz[1] * dR1 + gdz[2] * dR2;
 #if GSR_SG_UNROLL
         if (sg7) {
-            sg7_bwd(a, idx, sgr, x, y, z, dR0, dR1, dR2, ddx, ddy, ddz, STAGE ? stage : nullptr, lane);
+            if constexpr (STAGE) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA row loads have landed
+                sg7_bwd_slots(stage, slot, x, y, z, dR0, dR1, dR2, ddx, ddy, ddz);
+            } else {
+                sg7_bwd(a, idx, sgr, x, y, z, dR0, dR1, dR2, ddx, ddy, ddz);
+            }
         } else
 #endif
         for (int sg = 0; sg < a.SGM; sg++) {
@@ -684,17 +748,17 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     if (!culled) visible();
     if constexpr (STAGE) {
         // the wave's Gaussians [wbase, wbase + n): rows in LDS, then whole-wave stores
-        const int wbase = idx0 - lane;
-        const int n = max(0, min(64, a.end - wbase));
+        const int n = min(64, a.end - wbase);
         if (sg7) {
             if (culled) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA must not land after the zeros)
 #pragma unroll
                 for (int k = 0; k < 3 * kSG7; k++) {
-                    stage[kStageColor + 3 * kSG7 * lane + k] = 0.f;
-                    stage[kStageAxis + 3 * kSG7 * lane + k] = 0.f;
+                    stage[kStageColor + 3 * kSG7 * slot + k] = 0.f;
+                    stage[kStageAxis + 3 * kSG7 * slot + k] = 0.f;
                 }
 #pragma unroll
-                for (int k = 0; k < kSG7; k++) stage[kStageSharp + kSG7 * lane + k] = 0.f;
+                for (int k = 0; k < kSG7; k++) stage[kStageSharp + kSG7 * slot + k] = 0.f;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -716,7 +780,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
             const float d = c == 0 ? st_d0 : (c == 1 ? st_d1 : st_d2);
             return k < nsh ? Y[k] * d : 0.f;
         };
-        float4* row = reinterpret_cast<float4*>(stage + 48 * lane);
+        float4* row = reinterpret_cast<float4*>(stage + 48 * slot);
 #pragma unroll
         for (int i = 0; i < 12; i++) row[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -116,7 +116,7 @@ def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True)
         if not geom and name in ("normal", "mdepth"):
             assert float(t.abs().max()) == 0.0
             continue
-        assert Hh.rel_err(t.cpu().numpy(), o[name]) <= 1e-4, name
+        _check_image(name, t.cpu().numpy(), o[name])
     if not check_bwd:
         return
     g = S.upstream_grads(c["H"], c["W"])
@@ -127,6 +127,22 @@ def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True)
                                          radii, out[6], K, out[7], out[8], out[9], geom, False)
     _check_grads(gb, b)
     return out, o, g, gb
+
+
+def _check_image(name, mine, ref):
+    """max|a-b| / max|b| <= 1e-4 — except for the median depth's decision
+    flips: the reference picks the bisection cell by T(t_s) >= 1/2 at 8
+    samples (render_forward.cu:625-635), and where T stays within fp32
+    rounding of 1/2 over a stretch (a pixel between two splats) two fp32
+    evaluations of the same product pick different cells.  Those pixels may
+    differ, at most 1e-4 of the image (C1 clamp scene: 1 of 65536, where the
+    GPU's bisection mode OPT_NO_REFINE gives the GPU's value too)."""
+    err = Hh.rel_err(mine, ref)
+    if name != "mdepth" or err <= 1e-4:
+        assert err <= 1e-4, (name, err)
+        return
+    bad = np.abs(mine.astype(np.float64) - ref) > 1e-4 * np.abs(ref).max()
+    assert bad.sum() <= 1e-4 * bad.size, (name, err, int(bad.sum()))
 
 
 def _oracle_backward_on_gpu_state(c, a, out, o, g):
@@ -584,37 +600,55 @@ def c3():
     return c
 
 
-def test_c3_full_size_properties(c3):
+def _full_parity(c, dead_sample):
+    """Every pixel and every per-Gaussian gradient of a full-size scene
+    against the oracle (16 threads), the oracle backward on the GPU
+    forward's state.  Returns the per-gradient (relative L2, max) report."""
     from diff_gaussian_rasterization import _C
 
-    args = Hh.oracle_args(c3)
+    H, W = c["H"], c["W"]
+    args = _fwd_args(c)
     ga = [_gpu(x) for x in args] + [False]
-    out1 = _C.rasterize_gaussians(*ga)
+    out = _C.rasterize_gaussians(*ga)
     out2 = _C.rasterize_gaussians(*ga)
     for k in range(1, 6):  # forward is deterministic (no atomics)
-        assert torch.equal(out1[k], out2[k])
-    K, color, alpha, normal, mdepth, radii = out1[:6]
-    assert torch.isfinite(color).all() and float(alpha.min()) >= 0 and float(alpha.max()) < 1
+        assert torch.equal(out[k], out2[k])
+    del out2
+    K, color, alpha, normal, mdepth, radii = out[:6]
     O.set_threads(16)
-    stride = 97  # bounded sample of tiles
-    O.set_tile_stride(stride)
-    try:
-        o = O.forward(*args)
-    finally:
-        O.set_tile_stride(1)
+    o = O.forward(*args)
     assert K == o["num_rendered"]
     assert np.array_equal(radii.cpu().numpy(), o["radii"])
-    _check_binning(out1, o, 1080, 1920, dead_sample=20000)  # binning is computed in full for every tile
-    gx = (1920 + 15) // 16
-    mask = np.zeros((1080, 1920), bool)
-    for t in range(0, gx * ((1080 + 15) // 16), stride):
-        ty, tx = divmod(t, gx)
-        mask[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16] = True
+    _check_binning(out, o, H, W, dead_sample=dead_sample)
     for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
-        a = t.cpu().numpy()[:, mask]
-        b = o[name][:, mask]
-        bad = np.abs(a - b) > 1e-4 * np.abs(b).max()
+        a_, b_ = t.cpu().numpy(), o[name]
+        bad = np.abs(a_ - b_) > 1e-4 * np.abs(b_).max()
         assert bad.mean() <= 1e-4, (name, bad.mean())  # isolated float-decision flips only
+    # the clamp branch runs: visible Gaussians with o > 0.99 (alpha = min(0.99, o G) clamps at their centres)
+    assert int(((c["inp"]["opacities"][:, 0] > 0.99) & (torch.from_numpy(o["radii"]) > 0)).sum()) > 0
+    g = S.upstream_grads(H, W, seed=3)
+    g["alpha"] = torch.randn(1, H, W, generator=torch.Generator().manual_seed(5)) * 1e-3
+    b = _oracle_backward_on_gpu_state(c, args, out, o, g)
+    gb = _C.rasterize_gaussians_backward(*ga[:19], _gpu(g["color"]), _gpu(g["mdepth"]), _gpu(g["alpha"]),
+                                         _gpu(g["normal"]), alpha, normal, mdepth, _gpu(c["cam"].camera_center),
+                                         radii, out[6], K, out[7], out[8], out[9], True, False)
+    report = {}
+    try:
+        _check_grads(gb, b, report=report)
+    finally:
+        print({k: f"L2 {l2:.2e} max {mx:.2e}" for k, (l2, mx) in report.items()})
+    return report
+
+
+@pytest.mark.timeout(300)
+def test_c3_full_parity(c3):
+    """C3 (BASELINE.json configs[2]: 1M Gaussians, 1080p, forward + backward,
+    "grad check vs CUDA ref"), on the bench's own scene (uncapped opacities:
+    the alpha = 0.99 clamp is hit): K, radii and the per-tile lists exact;
+    every pixel of every image; every per-Gaussian gradient within relative
+    L2 1e-4 and max|a-b| / max|b| 1e-4 of the oracle backward run on the GPU
+    forward's state (measured: L2 <= 2.1e-5, max <= 9.3e-5)."""
+    _full_parity(c3, dead_sample=20000)
 
 
 def test_c3_bisection_shortcut_is_bit_exact(c3):
@@ -783,44 +817,26 @@ def test_c2_full_forward_parity():
         assert bad.mean() <= 1e-4, (name, bad.mean())  # isolated float-decision flips only
 
 
-def test_c5_full_size_properties():
-    """C5 (BASELINE.json configs[4]): 5M Gaussians, SH 3 + SG 7, 1080p with
-    depth/normal outputs.  K, radii and the tile lists exact; tile-sampled
-    image parity; deterministic forward; backward linear in the upstream
-    gradients and zero for culled Gaussians."""
+@pytest.mark.timeout(400)
+def test_c5_full_parity():
+    """C5 (BASELINE.json configs[4]: 5M Gaussians, SH 3 + SG 7, 1080p with
+    depth / normal outputs) as test_c3_full_parity: every pixel, every
+    per-Gaussian gradient (SG rows included) against the oracle backward on
+    the GPU forward's state (measured: L2 <= 3.7e-6, max <= 9.4e-6)."""
+    _full_parity(_scene(5_000_000, 1920, 1080, sg_degree=7), dead_sample=5000)
+
+
+def test_c5_backward_linearity():
+    """C5: the backward is linear in the upstream gradients (nothing dropped or
+    double-counted in the atomic accumulation) and exactly zero for culled
+    Gaussians (the forward parity is test_c5_full_parity)."""
     from diff_gaussian_rasterization import _C
 
     W, H = 1920, 1080
     c = _scene(5_000_000, W, H, sg_degree=7)
-    args = Hh.oracle_args(c)
-    ga = [_gpu(x) for x in args] + [False]
+    ga = [_gpu(x) for x in Hh.oracle_args(c)] + [False]
     out = _C.rasterize_gaussians(*ga)
-    out2 = _C.rasterize_gaussians(*ga)
-    for k in range(1, 6):
-        assert torch.equal(out[k], out2[k])
-    del out2
-    O.set_threads(16)
-    stride = 211
-    O.set_tile_stride(stride)
-    try:
-        o = O.forward(*args)
-    finally:
-        O.set_tile_stride(1)
     K, color, alpha, normal, mdepth, radii = out[:6]
-    assert K == o["num_rendered"]
-    assert np.array_equal(radii.cpu().numpy(), o["radii"])
-    _check_binning(out, o, H, W, dead_sample=5000)
-    gx = (W + 15) // 16
-    mask = np.zeros((H, W), bool)
-    for t in range(0, gx * ((H + 15) // 16), stride):
-        ty, tx = divmod(t, gx)
-        mask[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16] = True
-    for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
-        a = t.cpu().numpy()[:, mask]
-        b = o[name][:, mask]
-        bad = np.abs(a - b) > 1e-4 * np.abs(b).max()
-        assert bad.mean() <= 1e-4, (name, bad.mean())
-    del o
     g1 = {k: v.to(DEV) for k, v in S.upstream_grads(H, W, seed=1).items()}
     g2 = {k: v.to(DEV) for k, v in S.upstream_grads(H, W, seed=2).items()}
 
