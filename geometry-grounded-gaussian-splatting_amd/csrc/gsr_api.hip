@@ -117,15 +117,12 @@ uint32_t higher_msb(uint32_t n) {
 using namespace gsr;
 
 // Binning path: the tile lists of tilelists.hip where the grid allows, else
-// the instance sort of binning.hip; the per-tile sort of sortbin.hip only on
-// request (GSR_OPT_SORTBIN: measured slower at C3).
+// the instance sort of binning.hip.
 int bin_path(uint32_t gx, uint32_t gy) {
-    if (option(kOptSortbin) && sortbin_fits(gx, gy)) return kBinSortbin;
     return list_binning(gx, gy) ? kBinLists : kBinInstanceSort;
 }
 
-// `tmp`: where the forward-only scratch (scan / depth-sort temporaries, the
-// sortbin counts) goes; NULL keeps it at the end of the buffer itself.  The
+// `tmp`: where the forward-only scratch (scan / depth-sort temporaries) goes; NULL keeps it at the end of the buffer itself.  The
 // fields the backward reads come first either way, so it re-carves without
 // knowing which layout the forward used.
 size_t carve_geom(void* base, int P, uint32_t gx, uint32_t gy, GeomState& g, Carver* tmp = nullptr) {
@@ -147,13 +144,6 @@ size_t carve_geom(void* base, int P, uint32_t gx, uint32_t gy, GeomState& g, Car
     g.scan_tmp = t.take<char>(g.scan_tmp_bytes);
     g.dsort_tmp_bytes = depth_sort_temp_bytes(P);
     g.dsort_tmp = t.take<char>(g.dsort_tmp_bytes);
-    // (last: the fields above keep their offsets whichever path a call takes)
-    const size_t tiles = (size_t)gx * gy;
-    const bool sb = option(kOptSortbin) && sortbin_fits(gx, gy) && P > 0;
-    g.bin_hist = t.take<uint32_t>(sb ? (size_t)sortbin_blocks(P) * tiles : 0);
-    g.bin_total = t.take<uint32_t>(sb ? tiles : 0);
-    g.bin_start = t.take<uint32_t>(sb ? tiles + 1 : 0);
-    g.bin_info = t.take<uint32_t>(sb ? 4 : 0);
     return c.off + 256;
 }
 
@@ -172,18 +162,7 @@ size_t carve_binning(void* base, int K, int P, uint32_t gx, uint32_t gy, int pat
     b.path = path;
     b.use_lists = path == kBinLists;
     b.key_bytes = tile_key_bytes(tile_bits);
-    b.pairs = nullptr;
-    if (path == kBinSortbin) {
-        b.pairs = t.take<uint2>(K);
-        b.rows = nullptr;
-        b.qrec = nullptr;
-        b.rows_count = b.rows_off = b.segbase = b.tiles_count = b.tiles_off = nullptr;
-        b.list_tmp = nullptr;
-        b.keys_unsorted = b.keys = nullptr;
-        b.values_unsorted = nullptr;
-        b.sort_tmp = nullptr;
-        b.sort_tmp_bytes = 0;
-    } else if (b.use_lists) {
+    if (b.use_lists) {
         b.lists = list_layout(P, K, gx, gy);
         b.rows = t.take<uint2>(K);
         b.qrec = t.take<uint4>((size_t)2 * P);
@@ -456,13 +435,13 @@ int gsr_debug_image(const void* image_buffer, int width, int height, uint32_t* n
 }
 
 int gsr_set_option(int opt, int value) {
-    if (opt < 0 || opt >= gsr::kNumOptions) return fail(GSR_ERR_ARGS, "unknown option");
+    if (opt < 0 || opt >= gsr::kNumOptions || gsr::option_retired(opt)) return fail(GSR_ERR_ARGS, "unknown option");
     gsr::g_options[opt] = value;
     return GSR_OK;
 }
 
 
-int gsr_abi_version(void) { return 13; }
+int gsr_abi_version(void) { return 14; }
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -590,8 +569,6 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
                     "memcpy prefiltered flag");
         GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
         // the GPU counts the tile lists (or sorts by depth) while the host waits
-        if (path == kBinSortbin)
-            GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_count(p, gs, radii, ts, stream), "tile counts");
         if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, true, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
         Ks.x = rb->pinned[0];
@@ -620,9 +597,7 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
         btmp = Carver(aligned_base(sbuf));
     }
     carve_binning(aligned_base(bbuf), (int)K, P, p.grid_x, p.grid_y, path, bs, scratch_alloc ? &btmp : nullptr);
-    if (path == kBinSortbin) {
-        GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_lists(p, gs, radii, bs, ts, stream), "tile lists");
-    } else if (path == kBinLists) {
+    if (path == kBinLists) {
         GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_list_binning(p, gs, radii, bs, ts, (int)K, stream), "tile lists");
     } else {
         const int tile_bits = (int)higher_msb((uint32_t)tiles);
@@ -868,8 +843,6 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
                     "memcpy prefiltered flag");
         GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
         // the GPU counts the tile lists (or sorts by depth) while the host waits
-        if (path == kBinSortbin)
-            GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_count(p, gs, gs.radii, ts, stream), "tile counts");
         if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, true, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
         Ks.x = rb->pinned[0];
@@ -906,9 +879,7 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
     void* cbuf = dup_tile_alloc(dup_tile_ctx, carve_chunks(nullptr, n_chunks, cs));
     if (!cbuf) return fail(GSR_ERR_ALLOC, "duplicated-tile buffer allocation failed");
     carve_chunks(aligned_base(cbuf), n_chunks, cs);
-    if (path == kBinSortbin) {
-        GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_sortbin_lists(p, gs, gs.radii, bs, ts, stream), "tile lists");
-    } else if (path == kBinLists) {
+    if (path == kBinLists) {
         GSR_STAGE(GSR_STAGE_TILE_LISTS, launch_list_binning(p, gs, gs.radii, bs, ts, (int)K, stream), "tile lists");
     } else {
         const int tile_bits = (int)higher_msb(tiles);

@@ -78,24 +78,13 @@ struct GeomState {
     size_t scan_tmp_bytes;
     void* dsort_tmp;
     size_t dsort_tmp_bytes;
-    // sortbin.hip (grids of at most kMaxSortbinTiles tiles)
-    uint32_t* bin_hist;   // [blocks][tiles] live instances per (Gaussian block, tile); then, in place, the
-                          // exclusive prefix over the blocks
-    uint32_t* bin_total;  // [tiles] live instances per tile
-    uint32_t* bin_start;  // [tiles + 1] exclusive scan of bin_total
-    uint32_t* bin_info;   // [4] longest tile list, tiles with 1..kSortSmall entries
 };
 // ---- per-instance state (replaces BinningState) ----
 // tile ids as 16-bit sort keys when the grid allows (<= 65536 tiles)
 inline int tile_key_bytes(int tile_bits) { return tile_bits <= 16 ? 2 : 4; }
 // Tile-list binning (tilelists.hip): grids up to kMaxGrid x kMaxGrid tiles.
 constexpr int kMaxGrid = 1024;
-// Sort binning (sortbin.hip): grids up to kMaxSortbinTiles tiles (one LDS
-// histogram), tile lists up to kSortLarge entries (one LDS sort).
-constexpr int kMaxSortbinTiles = 16384;
-constexpr int kSortSmall = 2048;   // 256 threads x 8 keys
-constexpr int kSortLarge = 12288;  // 1024 threads x 12 keys
-enum BinPath : int { kBinInstanceSort = 0, kBinLists = 1, kBinSortbin = 2 };
+enum BinPath : int { kBinInstanceSort = 0, kBinLists = 1 };
 struct ListLayout {
     int nseg_rows = 0, nseg_tiles_max = 0;
     size_t tmp_bytes = 0;
@@ -104,7 +93,6 @@ struct BinningState {
     uint32_t* point_list;  // first in the buffer: its offset depends on nothing else
     int path;              // BinPath
     bool use_lists;        // tilelists.hip path
-    uint2* pairs;          // (sortbin) (depth bits, Gaussian) per live instance, grouped by tile
     ListLayout lists;
     uint2* rows;           // (Gaussian, column span) per tile row, q order
     uint4* qrec;           // [P][2] per Gaussian in q order: id, rows y0 | y1 << 16, spans of rows y0 .. y0 + 5

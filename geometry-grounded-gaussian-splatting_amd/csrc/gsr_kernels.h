@@ -8,7 +8,10 @@ namespace gsr {
 
 // Run-time switches for A/B variants of one kernel in one process
 // (gsr_set_option in include/gsr.h); defaults are the shipped paths.
-enum Option : int { kOptBisectSkip = 0, kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptSortbin = 7, kOptBwdNarrow = 8, kOptRocprimDsort = 9, kOptPbwdStage = 10, kNumOptions = 11 };
+// ids 0, 7 and 8 belonged to retired A/B variants (bisection shortcut, per-tile
+// sort binning, two-wave backward); gsr_set_option rejects them
+enum Option : int { kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptRocprimDsort = 9, kOptPbwdStage = 10, kNumOptions = 11 };
+inline bool option_retired(int opt) { return opt == 0 || opt == 7 || opt == 8; }
 int option(int which);
 hipError_t read_render_stats(unsigned long long* out, bool reset);
 
@@ -89,13 +92,6 @@ size_t reduce_temp_bytes(int P);
 hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
                                const TileState& ts, int K, hipStream_t stream);
 
-// sortbin.hip
-bool sortbin_fits(uint32_t gx, uint32_t gy);
-int sortbin_blocks(int P);
-hipError_t launch_sortbin_count(const FwdParams& p, const GeomState& gs, const int* radii, const TileState& ts,
-                                hipStream_t stream);
-hipError_t launch_sortbin_lists(const FwdParams& p, const GeomState& gs, const int* radii, const BinningState& bs,
-                                const TileState& ts, hipStream_t stream);
 
 // render_fwd.hip
 hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const ImageState& is,

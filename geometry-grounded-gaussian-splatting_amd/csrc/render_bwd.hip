@@ -3,8 +3,7 @@
 // Replaces renderCUDA<3, GEOMETRY> backward (render_backward.cu:716-1069) and
 // BACKWARD::render (:1164-1209).
 //
-// One wave64 per 16x16 tile (four pixels per lane, in two packed pairs;
-// GSR_OPT_BWD_NARROW: two waves, one pair per lane).  Per (pixel, Gaussian)
+// One wave64 per 16x16 tile (four pixels per lane, in two packed pairs).  Per (pixel, Gaussian)
 // the kernel recomputes alpha and produces up to 17 gradient terms; they are
 // summed over the lane's pixels, then over the wave with one transposed butterfly
 // (wave_transpose_reduce16: v_permlane32_swap / v_permlane16_swap, then DPP
@@ -462,18 +461,11 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.no_cache = option(kOptBwdNoCache);
     a.tile_order = ws.tile_order;
     if (a.num_tiles == 0) return hipSuccess;
-    const bool wide = !option(kOptBwdNarrow);
-    if (p.require_depth) {
-        if (wide)
-            hipLaunchKernelGGL((render_bwd_kernel<true, 2>), dim3(a.num_tiles), dim3(64), 0, stream, a);
-        else
-            hipLaunchKernelGGL((render_bwd_kernel<true, 1>), dim3(a.num_tiles), dim3(128), 0, stream, a);
-    } else {
-        if (wide)
-            hipLaunchKernelGGL((render_bwd_kernel<false, 2>), dim3(a.num_tiles), dim3(64), 0, stream, a);
-        else
-            hipLaunchKernelGGL((render_bwd_kernel<false, 1>), dim3(a.num_tiles), dim3(128), 0, stream, a);
-    }
+    // NP = 2: one wave per tile (the two-wave NP = 1 layout measured slower, see the kernel)
+    if (p.require_depth)
+        hipLaunchKernelGGL((render_bwd_kernel<true, 2>), dim3(a.num_tiles), dim3(64), 0, stream, a);
+    else
+        hipLaunchKernelGGL((render_bwd_kernel<false, 2>), dim3(a.num_tiles), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
 

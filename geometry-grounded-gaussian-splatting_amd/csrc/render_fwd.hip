@@ -25,8 +25,8 @@
 // C3 with GSR_OPT_RENDER_STATS).  Longer lists keep the wave-uniform walk
 // with the records restaged per pass.
 // Contraction is off for this file: every fma below is written out, so each
-// template instance rounds identically (the SKIP/no-SKIP outputs are compared
-// bit for bit in tests/test_gpu_parity.py).
+// template instance (plain, GSR_OPT_RENDER_STATS, the sample queries) rounds
+// identically.
 #pragma clang fp contract(off)
 
 #include <type_traits>
@@ -107,40 +107,19 @@ struct RenderFwdArgs {
 //    few ulp of u, i.e. an absolute error of ~1e-7 in g);
 //  * a non-ball splat (rsigma <= 0, g = 0 in the reference) runs with
 //    alpha_g = 0 and sc = 0: u = 0, g = 1, 1 - 0*g = 1 exactly.
-// Exact shortcut (SKIP): when every sample of the window has |delta| > 6,
-// a*g < e^-18 < 2^-25, so 1 - a*g rounds to exactly 1.0f: B is unchanged
-// and A gains (1 - a) in front of the window, nothing behind it (the samples
-// are monotone in s, so the two window ends decide).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float kSqrtHalfLog2e = 0.84932180028801904272f;  // sqrt(0.5 log2 e)
-constexpr float kFarDelta = 6.f;  // |delta| beyond which 1 - a g == 1.0f exactly (a <= 0.99)
 
 // Samples live in packed register pairs (pair k holds samples START + 2k and
 // START + 2k + 1, so every v_pk_* operand is an aligned pair and no lane
 // moves feed them); an odd count leaves one scalar sample (A1, B1 at T1).
 // Per contributor the staged record supplies sc = rsigma sqrt(0.5 log2e)
 // and the ball flag bm (1 or 0), so a_g = alpha bm and u = fma(ts, sc, -t_peak sc).
-template <int NP, bool HAS1, bool SKIP>
+template <int NP, bool HAS1>
 __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], const f32x2 (&TS)[NP], float& A1,
                                             float& B1, float T1, float alpha, float t_peak, float rsig, float sc,
                                             float bm) {
     const float om = 1.f - alpha;
-    const f32x2 om2 = {om, om};
-    if constexpr (SKIP) {
-        const bool ball = rsig > 0.f;
-        // the samples' extremes (T1 is the last sample of a pass, the middle probe of walk 1)
-        const float s_lo = HAS1 ? fminf(TS[0].x, T1) : TS[0].x;
-        const float s_hi = HAS1 ? fmaxf(TS[NP - 1].y, T1) : TS[NP - 1].y;
-        const float d_lo = (s_lo - t_peak) * rsig;
-        const float d_hi = (s_hi - t_peak) * rsig;
-        if (ball && d_lo > kFarDelta) {
-#pragma unroll
-            for (int k = 0; k < NP; k++) A[k] *= om2;
-            if constexpr (HAS1) A1 *= om;
-            return;
-        }
-        if (ball && d_hi < -kFarDelta) return;
-    }
     const float ag = alpha * bm;
     const float q = -t_peak * sc;
     const f32x2 ag2 = {ag, ag}, sc2 = {sc, sc}, q2 = {q, q};
@@ -266,7 +245,7 @@ __device__ unsigned long long g_render_stats[8];
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
-template <bool GEOM, bool SKIP, bool STATS = false, bool SAMPLE = false>
+template <bool GEOM, bool STATS = false, bool SAMPLE = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, 8))) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 128 x 16 B = 8 KB) aliased with the
     // resident cache (3 x 256 x 16 B = 12 KB), the 8 KB of masks and the
@@ -549,7 +528,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             const float T1 = ts[END - 1];
             if (resident) {
                 lane_walk(in_range && !refined, [&](float alpha, float t_peak, float4 w2) {
-                    bisect_step<NP, HAS1, SKIP>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
+                    bisect_step<NP, HAS1>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
                 });
             } else {
                 bool bdone = !in_range;
@@ -571,7 +550,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         if (alpha < 1.0f / 255.0f) continue;
                         const float4 w2 = c_w2[j];
                         const float t_peak = splat_tpeak(w1, w2, dx, dy);
-                        bisect_step<NP, HAS1, SKIP>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
+                        bisect_step<NP, HAS1>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
                     }
                 }
             }
@@ -640,7 +619,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 if (ends && k == 0) {
                     walk(mask, plast, ppx, ppy, filter, live, [&](float alpha, float t_peak, float4 w2) {
                         refine_step(A, B, D, E, F, t, alpha, t_peak, w2.z, w2.w);
-                        bisect_step<1, false, SKIP>(AE, BE, TSE, unusedA, unusedB, 0.f, alpha, t_peak, w2.y, w2.z,
+                        bisect_step<1, false>(AE, BE, TSE, unusedA, unusedB, 0.f, alpha, t_peak, w2.y, w2.z,
                                                     w2.w);
                     });
                 } else {
@@ -720,7 +699,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             }
             float A1 = 1.f, B1 = 1.f;
             walk(mask, plast, ppx, ppy, filter, pin, [&](float alpha, float t_peak, float4 w2) {
-                bisect_step<NP, true, SKIP>(A, B, TS, A1, B1, tp[MID], alpha, t_peak, w2.y, w2.z, w2.w);
+                bisect_step<NP, true>(A, B, TS, A1, B1, tp[MID], alpha, t_peak, w2.y, w2.z, w2.w);
             });
             float Tv[kProbes];
 #pragma unroll
@@ -1039,13 +1018,11 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     if (a.num_tiles == 0) return hipSuccess;
     if (p.require_depth) {
         if (option(kOptRenderStats))
-            hipLaunchKernelGGL((render_fwd_kernel<true, true, true>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
-        else if (option(kOptBisectSkip))
             hipLaunchKernelGGL((render_fwd_kernel<true, true>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
         else
-            hipLaunchKernelGGL((render_fwd_kernel<true, false>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+            hipLaunchKernelGGL((render_fwd_kernel<true>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
     } else {
-        hipLaunchKernelGGL((render_fwd_kernel<false, false>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
+        hipLaunchKernelGGL((render_fwd_kernel<false>), dim3(a.num_tiles), dim3(kTilePixels), 0, stream, a);
     }
     return hipGetLastError();
 }
@@ -1085,10 +1062,10 @@ hipError_t launch_point_fwd(int query, const FwdParams& p, const GeomState& gs, 
     a.chunk_max = cs.chunk_max;
     if (num_chunks == 0) return hipSuccess;
     if (query == kQueryIntegrate)
-        hipLaunchKernelGGL((render_fwd_kernel<false, false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,
+        hipLaunchKernelGGL((render_fwd_kernel<false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,
                            stream, a);
     else
-        hipLaunchKernelGGL((render_fwd_kernel<true, false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,
+        hipLaunchKernelGGL((render_fwd_kernel<true, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,
                            stream, a);
     return hipGetLastError();
 }

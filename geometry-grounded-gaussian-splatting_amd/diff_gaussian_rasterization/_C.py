@@ -44,7 +44,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 
 def _load():
@@ -120,15 +120,13 @@ NUM_STAGES = 14
 # carve_bwd layout: 256-B aligned base, float acc[P][16], then float acc_abs[P])
 KEEP_BWD_SCRATCH = False
 last_bwd_scratch = None
-OPT_BISECT_SKIP = 0
+# (ids 0, 7, 8: retired A/B variants, rejected by gsr_set_option)
 OPT_RENDER_STATS = 1
 OPT_BISECT_PASSES = 2
 OPT_BWD_NO_PREPASS = 3
 OPT_NO_TILE_ORDER = 4
 OPT_NO_REFINE = 5
 OPT_BWD_NO_CACHE = 6
-OPT_SORTBIN = 7
-OPT_BWD_NARROW = 8
 OPT_ROCPRIM_DSORT = 9
 OPT_PBWD_STAGE = 10
 

@@ -425,9 +425,9 @@ const char* gsr_stage_name(int stage);
 /*
  * Process-wide switches selecting A/B variants of a kernel, for measuring one
  * against the other in the same process (all variants but GSR_OPT_NO_REFINE
- * give bit-identical results).  GSR_OPT_BISECT_SKIP (default 0): exact shortcut for bisection
- * samples far from a Gaussian's ray peak (render_fwd.hip; slower on the
- * fog-like benchmark scene, where most samples are near a peak).
+ * give bit-identical results), and diagnostics.  Ids 0, 7 and 8 belonged to
+ * retired variants (a bisection shortcut, per-tile sort binning and a two-wave
+ * backward layout, all measured slower) and are rejected with GSR_ERR_ARGS.
  */
 /* GSR_OPT_BISECT_PASSES (diagnostic, default 0 = all 5): run only n median-depth
  * bisection passes (n < 0: none) to time them; median depth is then wrong. */
@@ -438,12 +438,6 @@ const char* gsr_stage_name(int stage);
 /* GSR_OPT_BWD_NO_CACHE (A/B, default 0): the backward recomputes dT/dt_m at every
  * pixel in its pre-pass (render_backward.cu:835-880) instead of taking the
  * forward's cached value. */
-/* GSR_OPT_SORTBIN (A/B, default 0): build the per-tile lists by per-tile LDS
- * sorts of unordered bins (sortbin.hip) instead of the depth sort + stable
- * counting passes (tilelists.hip); same lists, slower at 1080p. */
-/* GSR_OPT_BWD_NARROW (A/B, default 0): the backward raster with two wave64 per
- * tile and two pixels per lane instead of one wave64 and four pixels per lane
- * (render_bwd.hip). */
 /* GSR_OPT_ROCPRIM_DSORT (A/B, default 0): the depth order by rocPRIM's onesweep
  * radix sort instead of dsort.hip's (same order). */
 /* GSR_OPT_PBWD_STAGE (A/B): the per-Gaussian backward's SH / SG-7 gradient rows
@@ -453,15 +447,12 @@ const char* gsr_stage_name(int stage);
  * five bisection passes only, instead of two passes plus the bracketed Halley
  * refinement (render_fwd.hip; results agree to ~1e-7 of the depth, not bitwise). */
 enum gsr_option {
-    GSR_OPT_BISECT_SKIP = 0,
     GSR_OPT_RENDER_STATS = 1,
     GSR_OPT_BISECT_PASSES = 2,
     GSR_OPT_BWD_NO_PREPASS = 3,
     GSR_OPT_NO_TILE_ORDER = 4,
     GSR_OPT_NO_REFINE = 5,
     GSR_OPT_BWD_NO_CACHE = 6,
-    GSR_OPT_SORTBIN = 7,
-    GSR_OPT_BWD_NARROW = 8,
     GSR_OPT_ROCPRIM_DSORT = 9,
     GSR_OPT_PBWD_STAGE = 10
 };

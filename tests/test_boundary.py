@@ -223,9 +223,20 @@ def test_library_exports_header_symbols():
     for n in names:
         assert hasattr(lib, n), n
     lib.gsr_abi_version.restype = ctypes.c_int
-    assert lib.gsr_abi_version() == 13
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 14
     lib.gsr_stage_name.restype = ctypes.c_char_p
     assert lib.gsr_stage_name(5) == b"render_fwd"
+
+
+def test_retired_options_are_rejected():
+    """Option ids 0, 7, 8 (retired A/B variants) and out-of-range ids fail
+    loudly instead of being silently ignored (host-only call, no GPU)."""
+    from diff_gaussian_rasterization import _C
+
+    for opt in (0, 7, 8, 11, -1):
+        with pytest.raises(RuntimeError, match="unknown option"):
+            _C.set_option(opt, 1)
+    _C.set_option(_C.OPT_NO_TILE_ORDER, 0)
 
 
 def test_library_targets_gfx950():

@@ -268,21 +268,6 @@ def test_float64_yardstick(case):
         assert e_gpu <= 1e-4, (name, e_gpu)
 
 
-@pytest.mark.parametrize("case", [SMALL[1], SMALL[6], SMALL[8]], ids=["geom", "nogeom", "C1"])
-def test_parity_backward_narrow(case):
-    """The backward's two-waves-per-tile layout (GSR_OPT_BWD_NARROW: 2 pixels
-    per lane) against the oracle, as the default one-wave layout above."""
-    from diff_gaussian_rasterization import _C
-
-    case = dict(case)
-    ks = case.pop("kernel_size", 0.0)
-    _C.set_option(_C.OPT_BWD_NARROW, 1)
-    try:
-        _run(Hh.small_case(kernel_size=ks, **case))
-    finally:
-        _C.set_option(_C.OPT_BWD_NARROW, 0)
-
-
 @pytest.mark.parametrize("stage", [1, 2], ids=["staged", "per-lane"])
 @pytest.mark.parametrize("case", [dict(P=3001, W=96, H=64, seed=50, sgm=7, sg_degree=7),
                                   dict(P=2999, W=96, H=64, seed=51), dict(P=37, W=40, H=24, seed=52, sgm=7, sg_degree=7),
@@ -311,18 +296,7 @@ def _with_depth_ties(c, n_tied):
     return c
 
 
-@pytest.fixture(params=[0, 1], ids=["lists", "sortbin"])
-def binning(request):
-    """Both binning paths: the depth sort + stable counting passes
-    (tilelists.hip, default) and the per-tile sorts (sortbin.hip)."""
-    from diff_gaussian_rasterization import _C
-
-    _C.set_option(_C.OPT_SORTBIN, request.param)
-    yield request.param
-    _C.set_option(_C.OPT_SORTBIN, 0)
-
-
-def test_parity_depth_ties(binning):
+def test_parity_depth_ties():
     _run(_with_depth_ties(Hh.small_case(P=600, W=64, H=48, seed=21), 250))
 
 
@@ -337,15 +311,13 @@ def test_parity_depth_sort_tiles(P):
     _run(c, check_bwd=False)
 
 
-def test_parity_binning_paths(binning):
+def test_parity_binning_paths():
     _run(Hh.small_case(P=10000, W=256, H=256, seed=7, log_scale=math.log(0.03)))
     _run(Hh.small_case(P=500, W=100, H=70, seed=2, kernel_size=0.1))
 
 
-def test_parity_long_tile_lists(binning):
-    """Tiles with ~20k live entries: longer than one workgroup's LDS sort
-    (sortbin.hip: > kSortLarge = 12288 entries, the global-memory per-tile
-    sort); with depth ties among them."""
+def test_parity_long_tile_lists():
+    """Tiles with ~20k live entries, with depth ties among them."""
     c = _with_depth_ties(Hh.small_case(P=60000, W=32, H=32, seed=22, log_scale=math.log(0.1), z_range=(2.0, 3.0)),
                          5000)
     _run(c, check_bwd=False)
@@ -488,7 +460,7 @@ def test_backward_none_upstream():
             assert err <= 1e-5, (none, name, err)
 
 
-def test_forward_scratch_split_is_exact(binning, monkeypatch):
+def test_forward_scratch_split_is_exact(monkeypatch):
     """gsr_rasterize_forward_ex (the Python binding's forward) keeps the
     forward-only scratch out of the saved buffers: same images, point list and
     gradients as gsr_rasterize_forward (scratch in the buffers, the reference's
@@ -574,8 +546,6 @@ def test_timing_api():
     _C.rasterize_gaussians(*ga)
     _C.timing_enable(False)
     st = _C.timing_collect()
-    # (the sort binning of a 1080p-class grid has no separate depth order stage:
-    # tile_lists brackets its pre- and post-synchronisation launches)
     for k in ("preprocess", "scan", "tile_lists", "render_fwd"):
         assert st[k][1] >= 1 and st[k][0] > 0, k
     _C.timing_stages(["render_fwd"])
@@ -651,23 +621,6 @@ def test_c3_full_parity(c3):
     _full_parity(c3, dead_sample=20000)
 
 
-def test_c3_bisection_shortcut_is_bit_exact(c3):
-    """The far-sample shortcut of the median-depth bisection (render_fwd.hip
-    bisect_step<SKIP>) changes no bit of any output."""
-    from diff_gaussian_rasterization import _C
-
-    ga = [_gpu(x) for x in Hh.oracle_args(c3)] + [False]
-    try:
-        _C.set_option(_C.OPT_BISECT_SKIP, 0)
-        ref = _C.rasterize_gaussians(*ga)
-        _C.set_option(_C.OPT_BISECT_SKIP, 1)
-        got = _C.rasterize_gaussians(*ga)
-    finally:
-        _C.set_option(_C.OPT_BISECT_SKIP, 0)
-    for k in range(1, 6):
-        assert torch.equal(ref[k], got[k]), k
-
-
 def _render_stats(ga):
     from diff_gaussian_rasterization import _C
 
@@ -679,6 +632,18 @@ def _render_stats(ga):
         return out, _C.debug_render_stats(reset=True)
     finally:
         _C.set_option(_C.OPT_RENDER_STATS, 0)
+
+
+def test_c3_stats_instance_is_bit_exact(c3):
+    """The counting instance of the forward raster (GSR_OPT_RENDER_STATS, used
+    by the refinement test below) changes no bit of any output."""
+    from diff_gaussian_rasterization import _C
+
+    ga = [_gpu(x) for x in Hh.oracle_args(c3)] + [False]
+    ref = _C.rasterize_gaussians(*ga)
+    got, _ = _render_stats(ga)
+    for k in range(1, 6):
+        assert torch.equal(ref[k], got[k]), k
 
 
 def test_c3_refinement_matches_bisection(c3):

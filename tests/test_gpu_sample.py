@@ -178,19 +178,12 @@ def test_sample_points_on_tile_borders():
     _run(c, pts)
 
 
-def test_sample_sortbin_path():
-    """The per-tile sort binning (sortbin.hip, GSR_OPT_SORTBIN) with the
-    sample pad: tile borders and a ragged grid."""
-    from diff_gaussian_rasterization import _C
-
-    _C.set_option(_C.OPT_SORTBIN, 1)
-    try:
-        c = Hh.small_case(P=800, W=96, H=64, seed=9, log_scale=math.log(0.05))
-        _run(c, sample_points(c, 4000, 12))
-        c = Hh.small_case(P=300, W=61, H=53, seed=3)
-        _run(c, sample_points(c, 2500, 103))
-    finally:
-        _C.set_option(_C.OPT_SORTBIN, 0)
+def test_sample_tile_borders_ragged_grid():
+    """The sample pad at tile borders, and a ragged grid."""
+    c = Hh.small_case(P=800, W=96, H=64, seed=9, log_scale=math.log(0.05))
+    _run(c, sample_points(c, 4000, 12))
+    c = Hh.small_case(P=300, W=61, H=53, seed=3)
+    _run(c, sample_points(c, 2500, 103))
 
 
 def test_sample_wide_grid_sort_path():

@@ -11,3 +11,4 @@ for lib in default ab_libs/dma2.so; do
     echo "$lib $(tail -1 gpurun_out/pbwd.log)"
   done
 done
+bash tools/ab_libs.sh 10
