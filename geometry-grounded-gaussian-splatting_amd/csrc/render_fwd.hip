@@ -218,6 +218,25 @@ __device__ __forceinline__ void refine_step(float& A, float& B, float& D, float&
     F += fabsf(e);  // bounds |H''| on either side of every splat peak (where H'' jumps)
 }
 
+// An opaque copy of v: the compiler cannot prove it equal to v, so values
+// derived from it are recomputed at the use instead of kept live (or spilled)
+// from an earlier, identical expression.
+__device__ __forceinline__ int opaque_int(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// What a walk over one pixel's blended set needs: its mask column, last
+// contributor, coordinates and the contributor filter of a lane group.  The
+// refinement takes it from a functor called at every walk, which recomputes
+// it (from an opaque lane id and LDS) instead of holding it across the walks.
+struct PixSrc {
+    const uint32_t* mask;
+    uint32_t plast;
+    float x, y;
+    uint32_t filter;
+};
+
 // Diagnostic counters (STATS builds only, option GSR_OPT_RENDER_STATS):
 // [0] per-lane walk wave-steps and [1] their active lanes; [2] composite
 // wave-steps and [3] their blending lanes;
@@ -236,8 +255,13 @@ __device__ unsigned long long g_render_stats[8];
 //    also carries the vacancy transmittance at the point's own distance.
 // Occupancy (C3, GSR_* build variants through tools/ab_libs.sh): 24.3 KB of
 // LDS per block (a 256-record resident cache, 128-record composite batches)
-// fits 6 blocks per CU, and 6 waves per SIMD (80 VGPRs, spills outside the
-// walks): 0.812 ms; the same at 5 waves per SIMD (96 VGPRs) 0.823; a
+// fits 6 blocks per CU, and 6 waves per SIMD (80 VGPRs): 0.812 ms (round 2,
+// with 28 registers spilled around the median-depth phases: 216 MB of
+// scratch written per C3 launch; round 3 recomputes what was spilled — the
+// pixel coordinates, mask column, LDS indices and bisection window — from an
+// opaque lane id at each walk (PixSrc, opaque_int), and the lane groups
+// combine through DPP quad moves instead of ds_bpermute: one spilled
+// register, WRITE_SIZE 303 -> 93 MiB per launch, 0.783 -> 0.760 ms); the same at 5 waves per SIMD (96 VGPRs) 0.823; a
 // 352-record cache with 256-record batches (31.8 KB: the LDS granule left 4
 // blocks per CU) 0.893; a 192-record cache 0.820; 64-record batches 0.825.
 // Tiles whose contributing prefix exceeds the cache take the wave-uniform
@@ -431,15 +455,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     __syncthreads();
     const uint32_t max_contrib = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
 
+    // (render path) the pixel's coordinates recomputed where they are needed
+    // after the composite, from the wave-uniform tile origin and an opaque
+    // copy of the lane id: through the median-depth phases they would
+    // otherwise stay live, with the LDS addresses derived from them, and spill
+    const int tile_x0 = SAMPLE ? 0 : (int)(tile % a.grid_x) * kTile;
+    const int tile_y0 = SAMPLE ? 0 : (int)(tile / a.grid_x) * kTile;
+    auto lane_px = [&]() -> int { return tile_x0 + (opaque_int(tid) & 15); };
+    auto lane_py = [&]() -> int { return tile_y0 + (opaque_int(tid) >> 4); };
+    auto lane_fx = [&]() -> float {
+        if constexpr (SAMPLE) return pixx;
+        else return (float)lane_px();
+    };
+    auto lane_fy = [&]() -> float {
+        if constexpr (SAMPLE) return pixy;
+        else return (float)lane_py();
+    };
+    auto lane_mask = [&]() -> const uint32_t* { return s_mask + (GEOM ? opaque_int(tid) : 0); };
     float mDepth = 0.f, md_out = 0.f, md_dT = 0.f;
     bool md_ok = false, md_in_range = false;
     if constexpr (GEOM) {
         unsigned long long st[8] = {0, 0, cst[0], cst[1], 0, 0, 0, 0};
         float Tp[kSplit + 1];
         // the reference's first window (render_forward.cu:560-562)
-        const float win_lo = fmaxf(m_init - a.sample_range, 0.f);
-        const float win_hi = fmaxf(m_init + a.sample_range, 0.f);
-        float dmin = win_lo, dmax = win_hi;
+        // (set where the passes start: only m_init stays live until then)
+        auto win_lo = [&] { return fmaxf(m_init - a.sample_range, 0.f); };
+        auto win_hi = [&] { return fmaxf(m_init + a.sample_range, 0.f); };
+        float dmin = 0.f, dmax = 0.f;
         bool in_range = T <= kMinTransmittance;
         const bool resident = max_contrib <= (uint32_t)kResident;
         float4* c_w0 = s_rec;
@@ -500,7 +542,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 body(alpha_b, splat_tpeak(b1, b2, bdx, bdy), b2);
             }
         };
-        auto lane_walk = [&](bool active, auto&& body) { walk(my_mask, last, pixx, pixy, ~0u, active, body); };
+        auto lane_walk = [&](bool active, auto&& body) {
+            walk(lane_mask(), last, lane_fx(), lane_fy(), ~0u, active, body);
+        };
         bool refined = false;   // median depth found by the root refinement
         float t_ref = 0.f;
         float ref_t = 0.f, ref_D = 0.f, ref_E = 0.f;  // the last refinement walk's depth, -H', H''
@@ -542,7 +586,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         c++;
                         bdone = c >= last;
                         const float4 w0 = c_w0[j];
-                        const float dx = w0.x - pixx, dy = w0.y - pixy;
+                        const float dx = w0.x - lane_fx(), dy = w0.y - lane_fy();
                         const float4 w1 = c_w1[j];
                         const float power = splat_power(w0, w1, dx, dy);
                         if (power > 0.0f) continue;
@@ -580,19 +624,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         // Root refinement for one pixel, shared by the phases below: probe
         // walk + bracketed Halley walks.  A pixel may be worked by a group of
         // 4 lanes (lane q walks the contributors with index % 4 == q; products
-        // and sums are combined with two xor shuffles, identical in the 4
+        // and sums are combined with two xor quad moves, identical in the 4
         // lanes as float * and + commute) — `grouped` must then be uniform.
         auto gprod = [&](float v, bool grouped) {
-            if (grouped) {
-                v *= __shfl_xor(v, 1, 64);
-                v *= __shfl_xor(v, 2, 64);
+            if (grouped) {  // (DPP quad moves: no LDS addresses to keep)
+                v *= dpp_mov<kDppXor1>(v);
+                v *= dpp_mov<kDppXor2>(v);
             }
             return v;
         };
         auto gsum = [&](float v, bool grouped) {
             if (grouped) {
-                v += __shfl_xor(v, 1, 64);
-                v += __shfl_xor(v, 2, 64);
+                v += dpp_mov<kDppXor1>(v);
+                v += dpp_mov<kDppXor2>(v);
             }
             return v;
         };
@@ -605,8 +649,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             float t_ref, ref_t, ref_D, ref_E;
             float t, lo, hi;
         };
-        auto halley = [&](const uint32_t* mask, uint32_t plast, float ppx, float ppy, uint32_t filter, bool grouped,
-                          bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
+        auto halley = [&](auto&& src, bool grouped, bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
                           int walks, float scale) {
             Refine r{false, in_range0, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             const float tol = kRefineTol * scale, tol_cond = kCondTol * scale, tol_loose = kLooseTol * scale;
@@ -616,14 +659,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 float A = 1.f, B = 1.f, D = 0.f, E = 0.f, F = 0.f;
                 f32x2 AE[1] = {f32x2{1.f, 1.f}}, BE[1] = {f32x2{1.f, 1.f}};
                 float unusedA = 1.f, unusedB = 1.f;
+                const PixSrc ps = src();
                 if (ends && k == 0) {
-                    walk(mask, plast, ppx, ppy, filter, live, [&](float alpha, float t_peak, float4 w2) {
+                    walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, live, [&](float alpha, float t_peak, float4 w2) {
                         refine_step(A, B, D, E, F, t, alpha, t_peak, w2.z, w2.w);
                         bisect_step<1, false>(AE, BE, TSE, unusedA, unusedB, 0.f, alpha, t_peak, w2.y, w2.z,
                                                     w2.w);
                     });
                 } else {
-                    walk(mask, plast, ppx, ppy, filter, live, [&](float alpha, float t_peak, float4 w2) {
+                    walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, live, [&](float alpha, float t_peak, float4 w2) {
                         refine_step(A, B, D, E, F, t, alpha, t_peak, w2.z, w2.w);
                     });
                 }
@@ -675,8 +719,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         };
         // Probe walk (window ends + m0 + kProbeOffsets * SAMPLE_RANGE), then the
         // Halley walks from the log-secant root of the bracketing probes.
-        auto probe_refine = [&](const uint32_t* mask, uint32_t plast, float ppx, float ppy, float pm0, float pT,
-                                uint32_t filter, bool grouped) {
+        auto probe_refine = [&](auto&& src, float pm0, float pT, bool grouped) {
             bool pin = pT <= kMinTransmittance;
             const float lo_w = fmaxf(pm0 - a.sample_range, 0.f), hi_w = fmaxf(pm0 + a.sample_range, 0.f);
             const float interval = (hi_w - lo_w) * (1.f / (float)kSplit);
@@ -698,7 +741,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 B[k] = f32x2{1.f, 1.f};
             }
             float A1 = 1.f, B1 = 1.f;
-            walk(mask, plast, ppx, ppy, filter, pin, [&](float alpha, float t_peak, float4 w2) {
+            const PixSrc ps = src();
+            walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, pin, [&](float alpha, float t_peak, float4 w2) {
                 bisect_step<NP, true>(A, B, TS, A1, B1, tp[MID], alpha, t_peak, w2.y, w2.z, w2.w);
             });
             float Tv[kProbes];
@@ -728,7 +772,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             float wsec = Hlo / (Hlo - Hhi);
             wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
             const float t = __builtin_fmaf(wsec, hi - lo, lo);
-            return halley(mask, plast, ppx, ppy, filter, grouped, pin, t, lo, hi, false, 0.f, 0.f, pin, kRefineWalks,
+            return halley(src, grouped, pin, t, lo, hi, false, 0.f, 0.f, pin, kRefineWalks,
                           fmaxf(t, 1.f));
         };
         bool have_out = false;  // (render path) md_out and dT/dt_m published by the pixel's worker
@@ -747,17 +791,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 //     42 active lanes per step -> 2.53M with 51).
                 // The owner lane then takes the result, or runs the reference's passes where there is
                 // none (not converged, ill-conditioned, no grid neighbour with a root).
-                const int x0 = px - (tid & 15), y0 = py - (tid >> 4);
+                const int x0 = tile_x0, y0 = tile_y0;
                 s_pub_last[tid] = last;
                 s_pub_m0[tid] = m_init;
                 s_pub_T[tid] = T;
                 __syncthreads();
-                auto publish = [&](int p, float ppx, float ppy, const Refine& r) {
+                auto publish = [&](int p, const Refine& r) {
+                    p = opaque_int(p);  // (the LDS addresses at the store, not kept from the reads)
                     uint32_t flags = r.in_range ? 0u : kPubOut;
                     float mo = 0.f, dt = 0.f;
                     if (r.in_range && r.refined) {
                         flags = kPubRefined;
-                        const float nrm = pixel_ray_norm(ppx, ppy, a.W, a.H, a.focal_x, a.focal_y);
+                        const float nrm = pixel_ray_norm((float)(x0 + (p & 15)), (float)(y0 + (p >> 4)), a.W, a.H,
+                                                         a.focal_x, a.focal_y);
                         mo = r.t_ref * (1.0f / nrm);
                         const float mb = mo * nrm;
                         if (mb != 0.f) dt = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(r.ref_E, mb - r.ref_t, -r.ref_D);
@@ -767,15 +813,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     s_pub_m0[p] = dt;
                 };
                 {  // phase 1
-                    const int g = tid >> 2, q = tid & 3;
-                    const int gp = (g >> 3) * 32 + (g & 7) * 2;  // (2 (g / 8), 2 (g % 8)) in the tile
-                    const float gpx = (float)(x0 + (gp & 15)), gpy = (float)(y0 + (gp >> 4));
-                    const uint32_t gl = s_pub_last[gp];
+                    // (2 (g / 8), 2 (g % 8)) in the tile, g = lane / 4; recomputed for the publish
+                    auto grid_pixel = [&](int lane) { return ((lane >> 2) >> 3) * 32 + ((lane >> 2) & 7) * 2; };
+                    const int gp = grid_pixel(tid), q = tid & 3;
                     const float gm0 = s_pub_m0[gp], gT = s_pub_T[gp];
-                    const Refine r = probe_refine(s_mask + gp, gl, gpx, gpy, gm0, gT, 0x11111111u << q, true);
+                    auto src = [&] {
+                        const int lane = opaque_int(tid), gq = grid_pixel(lane);
+                        return PixSrc{s_mask + gq, s_pub_last[gq], (float)(x0 + (gq & 15)), (float)(y0 + (gq >> 4)),
+                                      0x11111111u << (lane & 3)};
+                    };
+                    const Refine r = probe_refine(src, gm0, gT, true);
                     if (q == 0) {
-                        s_groot[g] = (r.in_range && r.refined) ? r.t_ref : -1.f;
-                        publish(gp, gpx, gpy, r);
+                        const int lane = opaque_int(tid);
+                        s_groot[lane >> 2] = (r.in_range && r.refined) ? r.t_ref : -1.f;
+                        publish(grid_pixel(lane), r);
                     }
                 }
                 __syncthreads();
@@ -813,8 +864,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     const float interval = (hi_w - lo_w) * (1.f / (float)kSplit);
                     const float e0 = lo_w, e8 = __builtin_fmaf(interval, (float)kSplit, lo_w);
                     const float t0 = cnt ? fminf(fmaxf(sum / (float)cnt, e0), e8) : e0;
-                    const Refine r = halley(s_mask + p, ql, qx, qy, ~0u, false, qin && cnt > 0, t0, e0, e8, true, e0,
-                                            e8, qin, 1, fmaxf(t0, 1.f));
+                    auto src = [&] { return PixSrc{s_mask + p, ql, qx, qy, ~0u}; };  // (one walk)
+                    const Refine r = halley(src, false, qin && cnt > 0, t0, e0, e8, true, e0, e8, qin, 1, fmaxf(t0, 1.f));
                     live2 = r.live;
                     if (live2) {  // continued by a lane group below
                         s_pub_last[p] = ql;
@@ -822,7 +873,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         s_pub_m0[p] = r.lo;
                         s_pub_hi[p] = r.hi;
                     } else if (cnt > 0 || !qin) {
-                        publish(p, qx, qy, r);
+                        publish(p, r);
                     } else {
                         s_pub_last[p] = 0u;  // no guess: the owner runs the passes
                     }
@@ -843,26 +894,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 if (live2) s_list[before + __popcll(bl & ((1ull << (tid & 63)) - 1ull))] = (uint8_t)p2;
                 __syncthreads();
                 for (uint32_t e = (uint32_t)(tid >> 2); e < n_live; e += kTilePixels / 4) {
-                    const int p = s_list[e], q = tid & 3;
-                    const float qx = (float)(x0 + (p & 15)), qy = (float)(y0 + (p >> 4));
+                    const int p = s_list[e];
                     const float t = s_pub_T[p];
-                    const Refine r = halley(s_mask + p, s_pub_last[p], qx, qy, 0x11111111u << q, true, true, t,
-                                            s_pub_m0[p], s_pub_hi[p], false, 0.f, 0.f, true, kRefineWalks - 1,
-                                            fmaxf(t, 1.f));
-                    if (q == 0) publish(p, qx, qy, r);
+                    auto src = [&] {
+                        const int pp = s_list[opaque_int((int)e)];
+                        return PixSrc{s_mask + pp, s_pub_last[pp], (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
+                                      0x11111111u << (opaque_int(tid) & 3)};
+                    };
+                    const Refine r = halley(src, true, true, t, s_pub_m0[p], s_pub_hi[p], false, 0.f, 0.f, true,
+                                            kRefineWalks - 1, fmaxf(t, 1.f));
+                    if ((tid & 3) == 0) publish(s_list[opaque_int((int)e)], r);
                 }
                 __syncthreads();
-                const uint32_t flags = s_pub_last[tid];
+                const int me = opaque_int(tid);
+                const uint32_t flags = s_pub_last[me];
                 if (flags & kPubRefined) {
                     refined = true;
                     have_out = true;
-                    md_out = s_pub_T[tid];
-                    md_dT = s_pub_m0[tid];
+                    md_out = s_pub_T[me];
+                    md_dT = s_pub_m0[me];
                 } else if (flags & kPubOut) {
                     in_range = false;
                 }
             } else {
-                const Refine r = probe_refine(my_mask, last, pixx, pixy, m_init, T, ~0u, false);
+                const Refine r = probe_refine([&] { return PixSrc{lane_mask(), last, lane_fx(), lane_fy(), ~0u}; },
+                                              m_init, T, false);
                 in_range = r.in_range;
                 refined = r.refined;
                 t_ref = r.t_ref;
@@ -877,13 +933,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 if constexpr (STATS) {
                     if ((tid & 63) == 0) st[5] += 1;
                 }
-                dmin = win_lo;
-                dmax = win_hi;
+                dmin = win_lo();
+                dmax = win_hi();
                 pass(std::true_type{});
 #pragma unroll 1
                 for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{});
             }
         } else {
+            dmin = win_lo();
+            dmax = win_hi();
             if (a.passes > 0) pass(std::true_type{});
 #pragma unroll 1
             for (int it = 1; it < a.passes; it++) pass(std::false_type{});
@@ -908,7 +966,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             if constexpr (SAMPLE) {
                 mDepth_b = mDepth;  // the sample backward reads the median depth itself (sample_backward.cu:135)
             } else {
-                const float nrm = pixel_ray_norm(pixx, pixy, a.W, a.H, a.focal_x, a.focal_y);
+                const float nrm = pixel_ray_norm(lane_fx(), lane_fy(), a.W, a.H, a.focal_x, a.focal_y);
                 md_out = mDepth * (1.0f / nrm);
                 mDepth_b = md_out * nrm;
             }
@@ -968,7 +1026,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         return;
     }
     if (inside) {
-        const int pix = a.W * py + px;
+        const int pix = a.W * lane_py() + lane_px();
         if constexpr (GEOM) {
             a.out_mdepth[pix] = md_out;
             a.dT_dtm[pix] = md_dT;
