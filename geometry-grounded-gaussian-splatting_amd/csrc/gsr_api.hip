@@ -138,6 +138,7 @@ size_t carve_geom(void* base, int P, uint32_t gx, uint32_t gy, GeomState& g, Car
     g.offsets = c.take<uint2>(P);
     g.radii = c.take<int>(P);
     g.clamped = c.take<uint8_t>(P);
+    g.ddir = c.take<float>((size_t)9 * P);
     g.offsets_K = c.take<uint32_t>(1);
     g.near_flag = c.take<uint32_t>(1);
     g.scan_tmp_bytes = scan_temp_bytes(P) > reduce_temp_bytes(P) ? scan_temp_bytes(P) : reduce_temp_bytes(P);

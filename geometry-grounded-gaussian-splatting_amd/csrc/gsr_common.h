@@ -74,6 +74,7 @@ struct GeomState {
     uint32_t* near_flag;          // prefiltered check: 1 if a Gaussian fails the near-plane test
     int* radii;                   // internal copy when the caller passes radii == NULL
     uint8_t* clamped;             // bit c set: colour channel c was clamped at 0
+    float* ddir;                  // SH colour's direction Jacobian (gsr_math.h sh_basis_grad): 9 planes of P floats
     void* scan_tmp;
     size_t scan_tmp_bytes;
     void* dsort_tmp;

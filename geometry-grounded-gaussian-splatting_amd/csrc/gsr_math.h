@@ -104,6 +104,35 @@ __device__ inline void sh_basis(int D, float x, float y, float z, float* Y) {
 
 __device__ inline int sh_count(int D) { return (D + 1) * (D + 1); }
 
+// dY_k / d(x, y, z) of the SH basis above (k >= 1): the terms of the
+// reference's dRGBdx / dRGBdy / dRGBdz (render_backward.cu:94-153), so that
+// d colour_c / d dir_i = sum_k dY_k/d dir_i sh[k][c].  The forward preprocess
+// accumulates that Jacobian coefficient by coefficient next to the colour
+// (each SH entry used once, its register then free) and stores it as
+// GeomState::ddir, so the backward does not read the 192-B row again
+// (preprocess_bwd.hip).
+__device__ __forceinline__ void sh_basis_grad(int k, float x, float y, float z, float& gx, float& gy, float& gz) {
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    gx = 0.f, gy = 0.f, gz = 0.f;
+    switch (k) {
+        case 1: gy = -kSH_C1; break;
+        case 2: gz = kSH_C1; break;
+        case 3: gx = -kSH_C1; break;
+        case 4: gx = kSH_C2[0] * y; gy = kSH_C2[0] * x; break;
+        case 5: gy = kSH_C2[1] * z; gz = kSH_C2[1] * y; break;
+        case 6: gx = kSH_C2[2] * 2.f * -x; gy = kSH_C2[2] * 2.f * -y; gz = kSH_C2[2] * 2.f * 2.f * z; break;
+        case 7: gx = kSH_C2[3] * z; gz = kSH_C2[3] * x; break;
+        case 8: gx = kSH_C2[4] * 2.f * x; gy = kSH_C2[4] * 2.f * -y; break;
+        case 9: gx = kSH_C3[0] * 3.f * 2.f * xy; gy = kSH_C3[0] * 3.f * (xx - yy); break;
+        case 10: gx = kSH_C3[1] * yz; gy = kSH_C3[1] * xz; gz = kSH_C3[1] * xy; break;
+        case 11: gx = kSH_C3[2] * -2.f * xy; gy = kSH_C3[2] * (-3.f * yy + 4.f * zz - xx); gz = kSH_C3[2] * 4.f * 2.f * yz; break;
+        case 12: gx = kSH_C3[3] * -3.f * 2.f * xz; gy = kSH_C3[3] * -3.f * 2.f * yz; gz = kSH_C3[3] * 3.f * (2.f * zz - xx - yy); break;
+        case 13: gx = kSH_C3[4] * (-3.f * xx + 4.f * zz - yy); gy = kSH_C3[4] * -2.f * xy; gz = kSH_C3[4] * 4.f * 2.f * xz; break;
+        case 14: gx = kSH_C3[5] * 2.f * xz; gy = kSH_C3[5] * -2.f * yz; gz = kSH_C3[5] * (xx - yy); break;
+        default: gx = kSH_C3[6] * 3.f * (xx - yy); gy = kSH_C3[6] * -3.f * 2.f * xy; break;
+    }
+}
+
 // A lobe row (21 or 7 floats, 84 / 28 B) is only 4-B aligned; gfx950 serves
 // unaligned dwordx4 accesses, so a row moves as 16-B pieces: 6 + 6 + 2 load
 // instructions per Gaussian instead of 49 single dwords, each of which made

@@ -36,6 +36,7 @@ struct PreprocessBwdArgs {
     float tan_fovx, tan_fovy, focal_x, focal_y, kernel_size;
     const int* radii;
     const uint8_t* clamped;
+    const float* ddir;  // the forward's SH colour -> direction Jacobian, 9 planes of P (GeomState::ddir)
     const float* acc;
     const float* acc_abs;
     float* dL_dmean3D;
@@ -622,6 +623,12 @@ preprocess_bwd_kernel(PreprocessBwdArgs a) {
 
     // ---------------- SH / SG colour backward ----------------
     if (a.shs) {
+        // the forward's colour -> direction Jacobian (9 coalesced plane loads instead of the 192-B SH row)
+        float jd[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (a.D > 0) {
+#pragma unroll
+            for (int j = 0; j < 9; j++) jd[j] = a.ddir[(size_t)j * a.P + idx];
+        }
         const float dox = mx - a.campos[0], doy = my - a.campos[1], doz = mz - a.campos[2];
         const float dlen = sqrtf(dox * dox + doy * doy + doz * doz);
         const float x = dox / dlen, y = doy / dlen, z = doz / dlen;
@@ -632,8 +639,6 @@ preprocess_bwd_kernel(PreprocessBwdArgs a) {
         float Y[16];
         sh_basis(a.D, x, y, z, Y);
         const int n = sh_count(a.D);
-        float sh[48];
-        load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
         if (STAGE) {  // the row is written by the staged stores
             st_x = x, st_y = y, st_z = z, st_d0 = dR0, st_d1 = dR1, st_d2 = dR2;
         } else if (a.dc_rows) {  // the DC row as store_sh_grad writes it (Y[0] dR)
@@ -643,41 +648,9 @@ preprocess_bwd_kernel(PreprocessBwdArgs a) {
         } else {
             store_sh_grad(a.dL_dsh + (size_t)idx * a.SHM * 3, a.SHM, n, Y, dR0, dR1, dR2);
         }
-        // d(colour)/d(dir) per channel: dx/dy/dz (render_backward.cu:94-153)
-        float gdx[3] = {0.f, 0.f, 0.f}, gdy[3] = {0.f, 0.f, 0.f}, gdz[3] = {0.f, 0.f, 0.f};
-        if (a.D > 0) {
-            for (int c = 0; c < 3; c++) {
-                const float s1 = sh[3 * 1 + c], s2 = sh[3 * 2 + c], s3 = sh[3 * 3 + c];
-                gdx[c] = -kSH_C1 * s3;
-                gdy[c] = -kSH_C1 * s1;
-                gdz[c] = kSH_C1 * s2;
-            }
-            if (a.D > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                for (int c = 0; c < 3; c++) {
-                    const float s4 = sh[12 + c], s5 = sh[15 + c], s6 = sh[18 + c], s7 = sh[21 + c], s8 = sh[24 + c];
-                    gdx[c] += kSH_C2[0] * y * s4 + kSH_C2[2] * 2.f * -x * s6 + kSH_C2[3] * z * s7 + kSH_C2[4] * 2.f * x * s8;
-                    gdy[c] += kSH_C2[0] * x * s4 + kSH_C2[1] * z * s5 + kSH_C2[2] * 2.f * -y * s6 + kSH_C2[4] * 2.f * -y * s8;
-                    gdz[c] += kSH_C2[1] * y * s5 + kSH_C2[2] * 2.f * 2.f * z * s6 + kSH_C2[3] * x * s7;
-                }
-                if (a.D > 2) {
-                    for (int c = 0; c < 3; c++) {
-                        const float s9 = sh[27 + c], s10 = sh[30 + c], s11 = sh[33 + c], s12 = sh[36 + c],
-                                    s13 = sh[39 + c], s14 = sh[42 + c], s15 = sh[45 + c];
-                        gdx[c] += kSH_C3[0] * s9 * 3.f * 2.f * xy + kSH_C3[1] * s10 * yz + kSH_C3[2] * s11 * -2.f * xy +
-                                  kSH_C3[3] * s12 * -3.f * 2.f * xz + kSH_C3[4] * s13 * (-3.f * xx + 4.f * zz - yy) +
-                                  kSH_C3[5] * s14 * 2.f * xz + kSH_C3[6] * s15 * 3.f * (xx - yy);
-                        gdy[c] += kSH_C3[0] * s9 * 3.f * (xx - yy) + kSH_C3[1] * s10 * xz +
-                                  kSH_C3[2] * s11 * (-3.f * yy + 4.f * zz - xx) + kSH_C3[3] * s12 * -3.f * 2.f * yz +
-                                  kSH_C3[4] * s13 * -2.f * xy + kSH_C3[5] * s14 * -2.f * yz +
-                                  kSH_C3[6] * s15 * -3.f * 2.f * xy;
-                        gdz[c] += kSH_C3[1] * s10 * xy + kSH_C3[2] * s11 * 4.f * 2.f * yz +
-                                  kSH_C3[3] * s12 * 3.f * (2.f * zz - xx - yy) + kSH_C3[4] * s13 * 4.f * 2.f * xz +
-                                  kSH_C3[5] * s14 * (xx - yy);
-                    }
-                }
-            }
-        }
+        // d(colour)/d(dir) per channel (render_backward.cu:94-153): the forward's
+        // Jacobian planes (gsr_math.h sh_basis_grad)
+        const float gdx[3] = {jd[0], jd[3], jd[6]}, gdy[3] = {jd[1], jd[4], jd[7]}, gdz[3] = {jd[2], jd[5], jd[8]};
         float ddx = gdx[0] * dR0 + gdx[1] * dR1 + gdx[2] * dR2;
         float ddy = gdy[0] * dR0 + gdy[1] * dR1 + gdy[2] * dR2;
         float ddz = gdz[0] * dR0 + gdz[1] * dR1 + gdz[2] * dR2;
@@ -821,6 +794,7 @@ hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const 
     a.kernel_size = p.kernel_size;
     a.radii = b.radii;
     a.clamped = gs.clamped;
+    a.ddir = gs.ddir;
     a.acc = ws.acc;
     a.acc_abs = ws.acc_abs;
     a.dL_dmean3D = b.dL_dmean3D;

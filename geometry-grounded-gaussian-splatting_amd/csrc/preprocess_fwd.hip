@@ -41,6 +41,7 @@ struct PreprocessArgs {
     uint32_t grid_x, grid_y;
     int* radii;
     uint8_t* clamped;
+    float* ddir;  // 9 planes of P: d(SH colour)/d(direction) for the backward (D > 0)
     float* depths;
     Splat* splats;
     uint32_t* tiles_touched;
@@ -58,7 +59,7 @@ __device__ inline float ndc2pix(float v, int S) { return (float)((((double)v + 1
 // inputs, before the culling branches (one memory round trip instead of
 // three); the plain instance loads them where they are used.
 template <bool HOIST>
-__global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) preprocess_fwd_kernel(PreprocessArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     for (size_t i = (size_t)idx; i < a.zero_words; i += (size_t)gridDim.x * blockDim.x) a.zero_first[i] = 0u;
     if (idx == 0) *a.zero_K = 0u;
@@ -252,13 +253,28 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a) {
         col[0] = Y[0] * sh[0];
         col[1] = Y[0] * sh[1];
         col[2] = Y[0] * sh[2];
+        // with the colour, coefficient by coefficient: the backward's colour -> direction
+        // Jacobian (gsr_math.h sh_basis_grad; GeomState::ddir), J[3 c + i] = d colour_c / d dir_i
+        float J[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 1; kk < 16; kk++) {
             if (kk < n) {
                 col[0] += Y[kk] * sh[3 * kk];
                 col[1] += Y[kk] * sh[3 * kk + 1];
                 col[2] += Y[kk] * sh[3 * kk + 2];
+                float gx, gy, gz;
+                sh_basis_grad(kk, dx, dy, dz, gx, gy, gz);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    J[3 * c] += gx * sh[3 * kk + c];
+                    J[3 * c + 1] += gy * sh[3 * kk + c];
+                    J[3 * c + 2] += gz * sh[3 * kk + c];
+                }
             }
+        }
+        if (a.D > 0) {
+#pragma unroll
+            for (int j = 0; j < 9; j++) a.ddir[(size_t)j * a.P + idx] = J[j];
         }
         if (a.SGM == 7 && a.SGD == 7) {
             // SG degree 7 (C5): every lobe's axis / colour / sharpness rows
@@ -350,6 +366,7 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
     a.grid_y = p.grid_y;
     a.radii = radii;
     a.clamped = gs.clamped;
+    a.ddir = gs.ddir;
     a.depths = gs.depths;
     a.splats = gs.splats;
     a.tiles_touched = gs.tiles_touched;

@@ -175,7 +175,10 @@ constexpr int kProbes = 11;
 __constant__ constexpr float kProbeOffsets[kProbes] = {0.f,    -0.5f,   -0.25f, -0.125f, -0.0625f, 0.f,
                                                         0.0625f, 0.125f, 0.25f,  0.5f,    0.f};
 constexpr uint32_t kPubRefined = 1u, kPubOut = 2u;  // phase results: root found / not in range
-constexpr int kRefineWalks = 4;
+#ifndef GSR_REFINE_WALKS
+#define GSR_REFINE_WALKS 4
+#endif
+constexpr int kRefineWalks = GSR_REFINE_WALKS;
 #ifndef GSR_REFINE_TOL
 #define GSR_REFINE_TOL 3e-5f
 #endif
@@ -198,7 +201,10 @@ constexpr float kLooseTol = GSR_LOOSE_TOL;
 constexpr float kCurvTol = GSR_CURV_TOL;
 constexpr float kCondTol = 1e-6f;   // conditioning threshold (as the previous scheme's tolerance)
 constexpr float kTwoLn2 = 1.38629436111989061883f;
-constexpr float kHNoise = 1e-5f;  // rounding noise assumed in log2 T (~10x a 64-factor product's)
+#ifndef GSR_HNOISE
+#define GSR_HNOISE 1e-5f
+#endif
+constexpr float kHNoise = GSR_HNOISE;  // rounding noise assumed in log2 T (~10x a 64-factor product's; 2e-6 measured: C2 render_fwd 0.763 -> 0.717 ms, but a small scene's dL/dmeans2D drifts to 1.3e-4 of the oracle through the implicit median-depth gradient)
 
 __device__ __forceinline__ void refine_step(float& A, float& B, float& D, float& E, float& F, float t, float alpha,
                                             float t_peak, float sc, float bm) {
@@ -268,6 +274,9 @@ __device__ unsigned long long g_render_stats[8];
 // walk (C3's largest per-tile max contributor is 184).
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
+#endif
+#ifndef GSR_COMP_LAZY
+#define GSR_COMP_LAZY 0  // composite: m0's t_peak once after the composite, mask words flushed at word boundaries
 #endif
 template <bool GEOM, bool STATS = false, bool SAMPLE = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, 8))) render_fwd_kernel(RenderFwdArgs a) {
@@ -343,6 +352,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     uint32_t last = 0;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
     float N0 = 0.f, N1 = 0.f, N2 = 0.f, m_init = 0.f;
+    int g_m = -1;  // (GSR_COMP_LAZY) the contributor whose t_peak is m0
     bool done = !inside;
 
     unsigned long long cst[2] = {0, 0};  // (STATS) composite wave-steps, blending lanes
@@ -393,6 +403,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             }
         }
         if constexpr (GEOM) {
+#if GSR_COMP_LAZY
+            // the last contributor blended while T > 1/2 (m0 = its t_peak, evaluated once after the
+            // composite); the mask words are flushed at word boundaries by the batch loop
+            g_m = T > 0.5f ? g : g_m;
+            if (g < kResident) mask_cur |= 1u << (g & 31);
+#else
             const float t = splat_tpeak(w1, w2, dx, dy);
             m_init = T > 0.5f ? t : m_init;
             if (g < kResident) {
@@ -403,6 +419,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 }
                 mask_cur |= 1u << (g & 31);
             }
+#endif
         }
         T = test_T;
         last = (uint32_t)g + 1u;  // the reference's 1-based contributor index
@@ -424,11 +441,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         }
         __syncthreads();
         const int n = min(kBatch, toDo);
-        for (int j = 0; !done && j < n; j++)
+        for (int j = 0; !done && j < n; j++) {
+#if GSR_COMP_LAZY
+            const int g = i * kBatch + j;
+            if (GEOM && (g & 31) == 0 && g > 0 && g <= kResident) {  // (wave-uniform) the previous word is complete
+                my_mask[((g >> 5) - 1) * kTilePixels] = mask_cur;
+                mask_cur = 0u;
+                mask_w = g >> 5;
+            }
+#endif
             step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+        }
     }
 
-    if constexpr (GEOM) my_mask[mask_w * kTilePixels] = mask_cur;
+    if constexpr (GEOM) {
+        if (!GSR_COMP_LAZY || mask_w < kMaskWords) my_mask[mask_w * kTilePixels] = mask_cur;
+    }
     if constexpr (!SAMPLE) {
         // the composite's outputs are final: written before the median depth
         // (their registers are free for it)
@@ -504,6 +532,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             stage(0);
             __syncthreads();
         }
+#if GSR_COMP_LAZY
+        if (g_m >= 0) {  // m0: the t_peak of the last contributor blended while T > 1/2 (the same arithmetic)
+            float4 w0, w1, w2;
+            if (resident) {
+                w0 = c_w0[g_m];
+                w1 = c_w1[g_m];
+                w2 = c_w2[g_m];  // (.x is the record's w2.x)
+            } else {
+                const Splat* sp = a.splats + a.point_list[range.x + g_m];
+                w0 = sp->w0;
+                w1 = sp->w1;
+                w2 = sp->w2;
+            }
+            m_init = splat_tpeak(w1, w2, w0.x - lane_fx(), w0.y - lane_fy());
+        }
+#endif
         // Per-lane walk over the LDS-resident records of the contributors the
         // lane blended, in increasing index order (the reference's c = 1..last
         // multiplication order); each lane advances through its own mask words.
@@ -545,13 +589,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         auto lane_walk = [&](bool active, auto&& body) {
             walk(lane_mask(), last, lane_fx(), lane_fy(), ~0u, active, body);
         };
+        auto own_src = [&] { return PixSrc{lane_mask(), last, lane_fx(), lane_fy(), ~0u}; };
         bool refined = false;   // median depth found by the root refinement
         float t_ref = 0.f;
         float ref_t = 0.f, ref_D = 0.f, ref_E = 0.f;  // the last refinement walk's depth, -H', H''
         // one pass of the reference's bisection (render_forward.cu:560-645) over
         // the lanes still in range and not refined; FIRST evaluates all 9
         // samples, later passes reuse the bracketing ends
-        auto pass = [&](auto first_c) {
+        // (src: the pixel whose blended set the resident walk uses, PixSrc)
+        auto pass = [&](auto first_c, auto&& src) {
             constexpr bool FIRST = decltype(first_c)::value;
             constexpr int START = FIRST ? 0 : 1;
             constexpr int END = FIRST ? kSplit + 1 : kSplit;
@@ -571,9 +617,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             float A1 = 1.f, B1 = 1.f;
             const float T1 = ts[END - 1];
             if (resident) {
-                lane_walk(in_range && !refined, [&](float alpha, float t_peak, float4 w2) {
-                    bisect_step<NP, HAS1>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
-                });
+                const PixSrc ps = src();
+                walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, in_range && !refined,
+                     [&](float alpha, float t_peak, float4 w2) {
+                         bisect_step<NP, HAS1>(A, B, TS, A1, B1, T1, alpha, t_peak, w2.y, w2.z, w2.w);
+                     });
             } else {
                 bool bdone = !in_range;
                 uint32_t c = 0;
@@ -916,9 +964,84 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 } else if (flags & kPubOut) {
                     in_range = false;
                 }
+                // Phase 3: the pixels left to the reference's passes (not converged, ill-conditioned, no
+                // guess) compacted, lane e of the block working the e-th of them: a wave holding one such
+                // pixel no longer runs the passes with all of its lanes (C2, a sparse 800x800 scene: 134k
+                // of 640k pixels left, in 85% of the waves).  Per pixel the same walks in the same order
+                // as its owner lane would run them: the same outputs.
+                const bool left3 = in_range && !refined;
+                const unsigned long long bl3 = __ballot(left3);
+                if ((tid & 63) == 0) s_max[wave] = (uint32_t)__popcll(bl3);
+                __syncthreads();  // (every owner has read its flags)
+                uint32_t before3 = 0, n_left = 0;
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    before3 += w < wave ? s_max[w] : 0u;
+                    n_left += s_max[w];
+                }
+                if constexpr (STATS) st[7] += left3 ? 1 : 0;
+                if (n_left > 0) {  // (block-uniform)
+                    if (left3) {
+                        s_list[before3 + __popcll(bl3 & ((1ull << (tid & 63)) - 1ull))] = (uint8_t)me;
+                        s_pub_last[me] = last;
+                        s_pub_m0[me] = m_init;
+                    }
+                    __syncthreads();
+                    const bool own_in = in_range, own_refined = refined;  // (the worker role reuses them)
+                    const bool work = (uint32_t)tid < n_left;
+                    if (__ballot(work) != 0ull) {  // (waves past the list skip)
+                        if constexpr (STATS) {
+                            if ((tid & 63) == 0) st[5] += 1;
+                        }
+                        auto wsrc = [&] {
+                            const int pp = s_list[opaque_int(tid)];
+                            return PixSrc{s_mask + pp, s_pub_last[pp], (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
+                                          ~0u};
+                        };
+                        const int pw = work ? (int)s_list[tid] : 0;
+                        const float wm0 = s_pub_m0[pw];
+                        in_range = work;
+                        refined = false;
+                        dmin = fmaxf(wm0 - a.sample_range, 0.f);
+                        dmax = fmaxf(wm0 + a.sample_range, 0.f);
+                        pass(std::true_type{}, wsrc);
+#pragma unroll 1
+                        for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, wsrc);
+                        // the median depth and dT/dt_m as the owner path below computes them
+                        float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
+                        w_max = fminf(fmaxf(w_max, 0.f), 1.f);
+                        const float w_min = 1.f - w_max;
+                        const float md = in_range ? __builtin_fmaf(w_max, dmax, w_min * dmin) : 0.f;
+                        const PixSrc ps = wsrc();
+                        const float nrm = pixel_ray_norm(ps.x, ps.y, a.W, a.H, a.focal_x, a.focal_y);
+                        const float mo = md * (1.0f / nrm);
+                        const float mb = mo * nrm;
+                        float dT = 0.f;
+                        walk(ps.mask, ps.plast, ps.x, ps.y, ~0u, work && mb != 0.f && ps.plast != 0,
+                             [&](float alpha, float t_peak, float4 w2) {
+                                 const float t_delta = (mb - t_peak) * w2.y;
+                                 const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
+                                 dT += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
+                             });
+                        if (work) {
+                            const int q = s_list[opaque_int(tid)];
+                            s_pub_T[q] = mo;
+                            s_pub_m0[q] = dT;
+                            s_pub_last[q] = in_range ? 1u : 0u;
+                        }
+                    }
+                    in_range = own_in;
+                    refined = own_refined;
+                    __syncthreads();
+                    if (left3) {
+                        have_out = true;
+                        md_out = s_pub_T[me];
+                        md_dT = s_pub_m0[me];
+                        in_range = s_pub_last[me] != 0u;
+                    }
+                }
             } else {
-                const Refine r = probe_refine([&] { return PixSrc{lane_mask(), last, lane_fx(), lane_fy(), ~0u}; },
-                                              m_init, T, false);
+                const Refine r = probe_refine(own_src, m_init, T, false);
                 in_range = r.in_range;
                 refined = r.refined;
                 t_ref = r.t_ref;
@@ -926,25 +1049,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 ref_D = r.ref_D;
                 ref_E = r.ref_E;
             }
-            // lanes left: the reference's passes from its first window
-            const bool left = in_range && !refined;
-            if constexpr (STATS) st[7] += left ? 1 : 0;
-            if (__ballot(left) != 0ull) {
+            // lanes left: the reference's passes from its first window (render path: phase 3 above)
+            const bool left = SAMPLE && in_range && !refined;
+            if constexpr (STATS && SAMPLE) st[7] += left ? 1 : 0;
+            if (SAMPLE && __ballot(left) != 0ull) {
                 if constexpr (STATS) {
                     if ((tid & 63) == 0) st[5] += 1;
                 }
                 dmin = win_lo();
                 dmax = win_hi();
-                pass(std::true_type{});
+                pass(std::true_type{}, own_src);
 #pragma unroll 1
-                for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{});
+                for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, own_src);
             }
         } else {
             dmin = win_lo();
             dmax = win_hi();
-            if (a.passes > 0) pass(std::true_type{});
+            if (a.passes > 0) pass(std::true_type{}, own_src);
 #pragma unroll 1
-            for (int it = 1; it < a.passes; it++) pass(std::false_type{});
+            for (int it = 1; it < a.passes; it++) pass(std::false_type{}, own_src);
         }
         if constexpr (STATS) {
             for (int q = 0; q < 8; q++)

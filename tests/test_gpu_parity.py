@@ -673,6 +673,69 @@ def test_c3_refinement_matches_bisection(c3):
     assert waves > 0 and fallback_waves <= 0.02 * waves, st
 
 
+@pytest.fixture(scope="module")
+def c2():
+    """BASELINE.json configs[1]: 100k Gaussians, one 800x800 view (the bench's
+    C2 scene).  Sparse: every pixel blends its whole list (no pixel reaches
+    T < 1e-4) and the median depth often sits on a shallow stretch of T."""
+    W, H, P = 800, 800, 100_000
+    cam = S.make_camera(W, H)
+    raw = S.make_gaussians(P, aspect=H / W)
+    inp = {k: v.detach().contiguous() for k, v in S.activated_inputs(raw).items()}
+    return dict(bg=torch.zeros(3), inp=inp, cam=cam, W=W, H=H, sh_degree=3, sg_degree=0, kernel_size=0.0,
+                require_depth=True, tanx=math.tan(cam.FoVx / 2), tany=math.tan(cam.FoVy / 2))
+
+
+def test_c2_forward_parity(c2):
+    """C2 forward at full size against the oracle: K, radii and the per-tile
+    lists exact, every pixel of every image within 1e-4 of the image's max."""
+    from diff_gaussian_rasterization import _C
+
+    args = _fwd_args(c2)
+    ga = [_gpu(x) for x in args] + [False]
+    out = _C.rasterize_gaussians(*ga)
+    K, color, alpha, normal, mdepth, radii = out[:6]
+    O.set_threads(16)
+    o = O.forward(*args)
+    assert K == o["num_rendered"]
+    assert np.array_equal(radii.cpu().numpy(), o["radii"])
+    _check_binning(out, o, c2["H"], c2["W"], dead_sample=20000)
+    for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
+        a_, b_ = t.cpu().numpy(), o[name]
+        bad = np.abs(a_ - b_) > 1e-4 * np.abs(b_).max()
+        assert bad.mean() <= 1e-4, (name, bad.mean())
+
+
+def test_c2_compacted_fallback_matches_bisection(c2):
+    """The pixels the refinement leaves to the reference's passes (C2: ~20%,
+    spread over most waves) are compacted and run by the first lanes of the
+    block (render_fwd.hip phase 3): against all five reference passes on the
+    same GPU, colour, alpha, normal and the in-range pattern bit-identical,
+    depths within 2e-6 relative, and the passes run in at most 35% of the
+    waves (one wave per tile holding such pixels)."""
+    from diff_gaussian_rasterization import _C
+
+    ga = [_gpu(x) for x in Hh.oracle_args(c2)] + [False]
+    try:
+        _C.set_option(_C.OPT_NO_REFINE, 1)
+        ref = _C.rasterize_gaussians(*ga)
+    finally:
+        _C.set_option(_C.OPT_NO_REFINE, 0)
+    got, st = _render_stats(ga)
+    plain = _C.rasterize_gaussians(*ga)
+    for k in range(1, 6):  # the stats instance computes what the plain one does
+        assert torch.equal(plain[k], got[k]), k
+    for k in (1, 2, 3, 5):
+        assert torch.equal(ref[k], got[k]), k
+    a, b = got[4], ref[4]
+    assert torch.equal(a == 0, b == 0)
+    err = float((a - b).abs().max()) / float(b.abs().max())
+    assert err <= 2e-6, err
+    waves, pass_waves, left = st[4], st[5], st[7]
+    assert left > 0.05 * 800 * 800, st  # the case this test is about
+    assert waves > 0 and pass_waves <= 0.35 * waves, st
+
+
 def test_c3_backward_linearity(c3):
     """bwd(g1 + 2 g2) == bwd(g1) + 2 bwd(g2): every gradient is linear in the
     upstream image gradients (holds at any size; checks nothing is dropped or

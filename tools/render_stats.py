@@ -1,4 +1,6 @@
-"""Print the render_fwd diagnostic counters (GSR_OPT_RENDER_STATS) at C3 (development tool)."""
+"""Print the render_fwd diagnostic counters (GSR_OPT_RENDER_STATS) (development tool).
+
+python tools/render_stats.py [P W H]   (default C3: 1000000 1920 1080; C2: 100000 800 800)"""
 import math, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd")]
@@ -7,7 +9,7 @@ import gsr_scene as S
 from diff_gaussian_rasterization import _C
 
 dev = torch.device("cuda")
-W, H, P = 1920, 1080, 1_000_000
+P, W, H = (int(v) for v in sys.argv[1:4]) if len(sys.argv) > 3 else (1_000_000, 1920, 1080)
 cam = S.make_camera(W, H).to(dev)
 inp = {k: v.to(dev).contiguous() for k, v in S.activated_inputs(S.make_gaussians(P, aspect=H / W)).items()}
 E = torch.Tensor([])
@@ -23,4 +25,5 @@ st = _C.debug_render_stats(reset=True)
 _C.set_option(_C.OPT_RENDER_STATS, 0)
 print("walk wave-steps", st[0], "active lanes/step", round(st[1] / max(st[0], 1), 2))
 print("composite wave-steps", st[2], "blending lanes/step", round(st[3] / max(st[2], 1), 2))
+print(f"P={P} {W}x{H}")
 print("refine waves", st[4], "fallback waves", st[5], "refine lane-walks", st[6], "lanes left", st[7])

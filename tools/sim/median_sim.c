@@ -655,6 +655,9 @@ void sim_ref_depths(int W, int H, int gx, int ntiles, const uint32_t* tiles, con
  * roots (walk 1 also samples the window ends for in_range).  out: [0] lanes, [1] max|d|, [2] fallbacks,
  * [3] sum of phase-1 wave max walks, [4] phase-1 waves, [5] sum of phase-2 wave max walks, [6] phase-2 waves,
  * [8..23] phase-2 lane walk hist, [24] lanes without a grid guess */
+static long g_why_ill, g_why_nc, g_why_ok;  /* fallback reasons: ill-conditioned / not converged */
+static double g_why_D[8];  /* ill-conditioned: histogram of log10(D * scale) */
+void sim_why(long* o) { o[0] = g_why_ok; o[1] = g_why_ill; o[2] = g_why_nc; for (int i = 0; i < 8; i++) o[3 + i] = (long)g_why_D[i]; }
 static int halley_from(const contrib_t* c, int n, float t, float lo, float hi, float tol_rel, int maxit,
                        float hnoise, float* res) {
     const float tol = tol_rel * fmaxf(t, 1.f);
@@ -671,11 +674,14 @@ static int halley_from(const contrib_t* c, int n, float t, float lo, float hi, f
         const int loose = g_loose > 0.f && D > 0.f && fabsf(h) <= g_loose * sc * D &&
                           fabsf(h) * g_lastF <= g_tolF * D * D;  /* step x curvature (F / D) <= tolF */
         if ((dh < 0.f && fabsf(h) <= tol * -dh) || hi - lo <= tol || loose) {
-            if (-dh * 1e-6f * fmaxf(t, 1.f) >= hnoise) { *res = tn; return walks; }
+            if (-dh * 1e-6f * fmaxf(t, 1.f) >= hnoise) { *res = tn; g_why_ok++; return walks; }
+            g_why_ill++;
+            { double v = log10(fmax(-dh * fmaxf(t, 1.f), 1e-30)); int b = (int)floor(v) + 4; b = b < 0 ? 0 : b > 7 ? 7 : b; g_why_D[b] += 1; }
             return -walks;
         }
         t = tn;
     }
+    g_why_nc++;
     return -walks;
 }
 void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,

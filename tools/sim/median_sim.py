@@ -24,7 +24,7 @@ if os.environ.get("SIM_CASE"):  # a tests/helpers.small_case scene, e.g. "P=600,
     c = Hh.small_case(**kw)
     W, H, P = c["W"], c["H"], c["inp"]["means3D"].shape[0]
 else:
-    W, H, P = 1920, 1080, int(os.environ.get("SIM_P", 1_000_000))
+    W, H, P = int(os.environ.get("SIM_W", 1920)), int(os.environ.get("SIM_H", 1080)), int(os.environ.get("SIM_P", 1_000_000))
     cam = S.make_camera(W, H)
     raw = S.make_gaussians(P, aspect=H / W)
     if os.environ.get('SIM_FLAT'):
