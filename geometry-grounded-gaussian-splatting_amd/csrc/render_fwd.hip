@@ -275,9 +275,6 @@ __device__ unsigned long long g_render_stats[8];
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
-#ifndef GSR_COMP_LAZY
-#define GSR_COMP_LAZY 0  // composite: m0's t_peak once after the composite, mask words flushed at word boundaries
-#endif
 template <bool GEOM, bool STATS = false, bool SAMPLE = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, 8))) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 128 x 16 B = 8 KB) aliased with the
@@ -352,7 +349,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     uint32_t last = 0;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
     float N0 = 0.f, N1 = 0.f, N2 = 0.f, m_init = 0.f;
-    int g_m = -1;  // (GSR_COMP_LAZY) the contributor whose t_peak is m0
     bool done = !inside;
 
     unsigned long long cst[2] = {0, 0};  // (STATS) composite wave-steps, blending lanes
@@ -403,12 +399,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             }
         }
         if constexpr (GEOM) {
-#if GSR_COMP_LAZY
-            // the last contributor blended while T > 1/2 (m0 = its t_peak, evaluated once after the
-            // composite); the mask words are flushed at word boundaries by the batch loop
-            g_m = T > 0.5f ? g : g_m;
-            if (g < kResident) mask_cur |= 1u << (g & 31);
-#else
             const float t = splat_tpeak(w1, w2, dx, dy);
             m_init = T > 0.5f ? t : m_init;
             if (g < kResident) {
@@ -419,7 +409,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 }
                 mask_cur |= 1u << (g & 31);
             }
-#endif
         }
         T = test_T;
         last = (uint32_t)g + 1u;  // the reference's 1-based contributor index
@@ -441,22 +430,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         }
         __syncthreads();
         const int n = min(kBatch, toDo);
-        for (int j = 0; !done && j < n; j++) {
-#if GSR_COMP_LAZY
-            const int g = i * kBatch + j;
-            if (GEOM && (g & 31) == 0 && g > 0 && g <= kResident) {  // (wave-uniform) the previous word is complete
-                my_mask[((g >> 5) - 1) * kTilePixels] = mask_cur;
-                mask_cur = 0u;
-                mask_w = g >> 5;
-            }
-#endif
+        for (int j = 0; !done && j < n; j++)
             step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
-        }
     }
 
-    if constexpr (GEOM) {
-        if (!GSR_COMP_LAZY || mask_w < kMaskWords) my_mask[mask_w * kTilePixels] = mask_cur;
-    }
+    if constexpr (GEOM) my_mask[mask_w * kTilePixels] = mask_cur;
     if constexpr (!SAMPLE) {
         // the composite's outputs are final: written before the median depth
         // (their registers are free for it)
@@ -532,22 +510,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             stage(0);
             __syncthreads();
         }
-#if GSR_COMP_LAZY
-        if (g_m >= 0) {  // m0: the t_peak of the last contributor blended while T > 1/2 (the same arithmetic)
-            float4 w0, w1, w2;
-            if (resident) {
-                w0 = c_w0[g_m];
-                w1 = c_w1[g_m];
-                w2 = c_w2[g_m];  // (.x is the record's w2.x)
-            } else {
-                const Splat* sp = a.splats + a.point_list[range.x + g_m];
-                w0 = sp->w0;
-                w1 = sp->w1;
-                w2 = sp->w2;
-            }
-            m_init = splat_tpeak(w1, w2, w0.x - lane_fx(), w0.y - lane_fy());
-        }
-#endif
         // Per-lane walk over the LDS-resident records of the contributors the
         // lane blended, in increasing index order (the reference's c = 1..last
         // multiplication order); each lane advances through its own mask words.
