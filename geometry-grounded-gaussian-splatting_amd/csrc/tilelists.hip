@@ -449,7 +449,10 @@ __device__ __forceinline__ TileSeg find_seg(uint32_t b, uint32_t gy, const uint3
 // moment are one or two, and their point-list region (~1 MB at C3) stays in
 // that XCD's L2 while the partial lines written by successive segments fill
 // up (write-back of whole lines instead of ~16-B pieces).
-constexpr int kTileBlocks = 8 * 1024;
+#ifndef GSR_TILE_BLOCKS
+#define GSR_TILE_BLOCKS (8 * 1024)
+#endif
+constexpr int kTileBlocks = GSR_TILE_BLOCKS;
 
 template <typename F>
 __device__ __forceinline__ void for_xcd_segments(uint32_t n, F&& f) {

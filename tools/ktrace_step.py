@@ -1,11 +1,12 @@
 """Print one step's kernel timeline from a rocprofv3 kernel trace (development tool).
-python tools/ktrace_step.py TRACE_CSV [anchor_kernel_substring]"""
+python tools/ktrace_step.py TRACE_CSV [anchor_kernel_substring] [call index from the end, default -3]"""
 import csv, re, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 anchor = sys.argv[2] if len(sys.argv) > 2 else "preprocess_fwd"
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
-i0, i1 = idx[-3], idx[-2]
+k = int(sys.argv[3]) if len(sys.argv) > 3 else -3  # which call (from the end)
+i0, i1 = idx[k], idx[k + 1]
 t0 = int(rows[i0]["Start_Timestamp"])
 prev = t0
 for r in rows[i0:i1]:

@@ -86,6 +86,45 @@ def launches(path: str, counter: str) -> dict:
     return out
 
 
+def short_name(name: str) -> str:
+    n = name.split("(")[0].replace("void ", "").replace("gsr::", "")
+    return n[:60]
+
+
+def per_kernel(path: str, counter: str) -> dict:
+    """Per kernel (short name): the counter's average per dispatch."""
+    tot, seen = defaultdict(float), defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter or not stage_of(r["Kernel_Name"]):
+            continue
+        k = short_name(r["Kernel_Name"])
+        tot[k] += float(r["Counter_Value"])
+        seen[k].add(r["Dispatch_Id"])
+    return {k: v / max(1, len(seen[k])) for k, v in tot.items()}
+
+
+def kernel_table(src: str) -> dict:
+    """Per-kernel average duration (trace; each kernel's first dispatch skipped) and HBM bytes per
+    dispatch (separate FETCH / WRITE passes, gfx950 correction), VALU instructions per dispatch."""
+    durs = defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
+        if stage_of(r["Kernel_Name"]):
+            durs[short_name(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    f = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    w = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    sq_csv = os.path.join(src, "sq", "run_counter_collection.csv")
+    valu = per_kernel(sq_csv, "SQ_INSTS_VALU") if os.path.exists(sq_csv) else {}
+    out = {}
+    for k, lst in durs.items():
+        lst = sorted(lst[1:] or lst)
+        out[k] = {"dispatches": len(lst), "median_us": round(lst[len(lst) // 2] / 1e3, 2),
+                  "fetch_kib": None if k not in f else round(f[k], 1),
+                  "write_kib": None if k not in w else round(w[k], 1),
+                  "hbm_bytes": None if k not in f or k not in w else round((2.0 * f[k] + w[k]) * 1024.0),
+                  "valu_insts": None if k not in valu else round(valu[k])}
+    return out
+
+
 def main():
     src, dst, tag = sys.argv[1], sys.argv[2], sys.argv[3]
     key = sys.argv[4] if len(sys.argv) > 4 else "C3"
@@ -158,7 +197,8 @@ def main():
                 simd_cycles = 256 * 4 * c["GRBM_GUI_ACTIVE"] / 8.0
                 stages[st]["valu_busy"] = round(4.0 * c.get("SQ_INSTS_VALU", 0.0) / simd_cycles, 4)
     out = {"tag": tag, "workload_key": key, "source": src,
-           "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950)", "stages": stages}
+           "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950)", "stages": stages,
+           "kernels": kernel_table(src)}
     for name in (f"{tag}_stages.json", f"pmc_{key}.json"):
         with open(os.path.join(dst, name), "w") as fh:
             json.dump(out, fh, indent=1)
