@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(64)
 // slots, same values; chunks with more than kEmitCap instances write
 // directly.
 #ifndef GSR_TILES_EMIT_SORTED
-#define GSR_TILES_EMIT_SORTED 2  // 2: tiles_emit_wide_kernel (default), 1: 64-entry chunks, 0: direct
+#define GSR_TILES_EMIT_SORTED 3  // 3: tiles_emit_coop_kernel (default, grids <= 256 tiles wide), 2: tiles_emit_wide_kernel, 1: 64-entry chunks, 0: direct
 #endif
 constexpr int kEmitCap = 512;  // instances staged per 64-entry chunk (C3 averages ~3 tiles per row entry)
 
@@ -702,6 +702,136 @@ __global__ void __launch_bounds__(64)
     });
 }
 
+// tiles_emit with whole-workgroup segments (round 3).  The single-wave
+// emission runs ~1000 blocks per XCD, so every segment of the XCD's share is
+// in flight at once and the point-list region being written (~6.5 MB per XCD
+// at C3) exceeds its 4 MB L2: partial lines leave the L2 before they are
+// complete (WRITE_SIZE 158 MB per C3 launch against 52 MB of point list;
+// with 128 single-wave blocks per XCD the writes fall to 53 MB, but then the
+// launch is latency-bound).  Here NW waves work one segment together, its
+// 64 NW NPL entries ranked at once (entry c0 + 64 (NPL w + h) + lane is wave
+// w's plane h; a tile's rank counts the planes before, then the lower
+// lanes), staged in LDS by (tile, rank) and written by consecutive lanes; and
+// kCoopBlocks / 8 blocks per XCD walk its segments in lockstep strides, so
+// the region in flight is a row or two.  Same slots, same values.
+#ifndef GSR_COOP_BLOCKS
+#define GSR_COOP_BLOCKS (8 * 128)
+#endif
+#ifndef GSR_COOP_CAP
+#define GSR_COOP_CAP 2048
+#endif
+constexpr int kCoopBlocks = GSR_COOP_BLOCKS;
+constexpr int kCoopWaves = 4, kCoopPlanes = 2;  // 512 entries per round: one kTileSeg segment
+constexpr uint32_t kCoopCap = GSR_COOP_CAP;     // instances staged per round (more: direct writes)
+constexpr int kCoopMaxGx = 256;                 // wider grids keep tiles_emit_wide_kernel (LDS)
+size_t coop_lds_bytes(uint32_t gx) {
+    constexpr int kPl = kCoopWaves * kCoopPlanes;
+    return (size_t)8 * kPl * gx + (size_t)4 * (3 + kPl) * gx + (size_t)6 * kCoopCap;
+}
+
+template <int NW, int NPL>
+__global__ void __launch_bounds__(64 * NW)
+    tiles_emit_coop_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
+                           const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
+                           const uint2* __restrict__ rows, const uint32_t* __restrict__ O,
+                           uint32_t* __restrict__ point_list) {
+    constexpr int kPl = NW * NPL;
+    constexpr int kThreads = 64 * NW;
+    // LDS: kPl x [gx] masks; [gx] running slots, chunk offsets, write bases; kPl x [gx] plane prefixes;
+    // kCoopCap ids and tiles
+    extern __shared__ unsigned long long s_dyn[];
+    unsigned long long* s_cov = s_dyn;
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + kPl * gx);
+    uint32_t* s_off = s_run + gx;
+    uint32_t* s_base = s_off + gx;
+    uint32_t* s_pl = s_base + gx;
+    uint32_t* s_id = s_pl + kPl * gx;
+    uint16_t* s_x = reinterpret_cast<uint16_t*>(s_id + kCoopCap);
+    __shared__ uint32_t s_carry;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
+    const unsigned long long bit = 1ull << lane, below = bit - 1ull;
+    for_xcd_segments(segbase[gy], [&](uint32_t l) {
+        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
+        const size_t base = (size_t)gx * segbase[S.y];
+        __syncthreads();  // previous segment done with the LDS
+        for (uint32_t x = tid; x < gx; x += kThreads) s_run[x] = O[base + (size_t)x * S.nk + S.k];
+        for (uint32_t x = tid; x < kPl * gx; x += kThreads) s_cov[x] = 0ull;
+        __syncthreads();
+        for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64 * kPl) {
+            bool on[NPL];
+            uint32_t id[NPL], lo[NPL], hi[NPL];
+#pragma unroll
+            for (int h = 0; h < NPL; h++) {
+                const uint32_t e = c0 + 64 * (NPL * wave + h) + lane;
+                on[h] = e < S.e1;
+                const uint2 ent = on[h] ? rows[e] : make_uint2(0u, 1u);  // empty span when off
+                id[h] = ent.x;
+                lo[h] = ent.y & 0xffffu;
+                hi[h] = on[h] ? (ent.y >> 16) : 0u;
+            }
+#pragma unroll
+            for (int h = 0; h < NPL; h++) {
+                unsigned long long* cov = s_cov + (NPL * wave + h) * gx;
+                for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++) atomicOr(&cov[x], bit);
+            }
+            __syncthreads();
+            // per tile (wave 0): plane prefixes, count, base among the round's instances, write base
+            if (wave == 0) {
+                uint32_t carry = 0;
+                for (uint32_t b0 = 0; b0 < gx; b0 += 64) {
+                    const uint32_t b = b0 + lane;
+                    uint32_t cnt = 0;
+                    if (b < gx) {
+#pragma unroll
+                        for (int p = 0; p < kPl; p++) {
+                            s_pl[p * gx + b] = cnt;
+                            cnt += (uint32_t)__popcll(s_cov[p * gx + b]);
+                        }
+                    }
+                    const uint32_t incl = wave_incl_scan(cnt);
+                    if (b < gx) {
+                        const uint32_t o = carry + incl - cnt;
+                        const uint32_t r = s_run[b];
+                        s_off[b] = o;
+                        s_base[b] = r - o;
+                        s_run[b] = r + cnt;
+                    }
+                    carry += __shfl(incl, 63, 64);
+                }
+                if (lane == 0) s_carry = carry;
+            }
+            __syncthreads();
+            const uint32_t carry = s_carry;
+            auto slot = [&](int p, uint32_t x) {
+                return s_off[x] + s_pl[p * gx + x] + (uint32_t)__popcll(s_cov[p * gx + x] & below);
+            };
+            if (carry <= kCoopCap) {
+#pragma unroll
+                for (int h = 0; h < NPL; h++) {
+                    const int p = NPL * wave + h;
+                    for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++) {
+                        const uint32_t q = slot(p, x);
+                        s_id[q] = id[h];
+                        s_x[q] = (uint16_t)x;
+                    }
+                }
+                __syncthreads();
+                for (uint32_t q = tid; q < carry; q += kThreads) point_list[s_base[s_x[q]] + q] = s_id[q];
+            } else {
+#pragma unroll
+                for (int h = 0; h < NPL; h++) {
+                    const int p = NPL * wave + h;
+                    for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++) point_list[s_base[x] + slot(p, x)] = id[h];
+                }
+            }
+            __syncthreads();
+            for (uint32_t x = tid; x < kPl * gx; x += kThreads) s_cov[x] = 0ull;
+            __syncthreads();
+        }
+    });
+}
+
 __global__ void __launch_bounds__(256)
     list_ranges_kernel(uint32_t gx, uint32_t gy, const uint32_t* __restrict__ segbase, const uint32_t* __restrict__ O,
                        uint2* __restrict__ ranges) {
@@ -749,7 +879,11 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     if ((e = launch_scan_excl(bs.tiles_count, bs.tiles_off, (size_t)gx * L.nseg_tiles_max, 0u, bs.segbase + gy, gx,
                               sums, stream)) != hipSuccess)
         return e;
-    if (GSR_TILES_EMIT_SORTED == 2)
+    if (GSR_TILES_EMIT_SORTED == 3 && gx <= (uint32_t)kCoopMaxGx)
+        hipLaunchKernelGGL((tiles_emit_coop_kernel<kCoopWaves, kCoopPlanes>), dim3(kCoopBlocks), dim3(64 * kCoopWaves),
+                           coop_lds_bytes(gx), stream, gx, gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows,
+                           bs.tiles_off, bs.point_list);
+    else if (GSR_TILES_EMIT_SORTED >= 2)
         hipLaunchKernelGGL(tiles_emit_wide_kernel<kEmitPlanes>, dim3(kTileBlocks), dim3(64),
                            (8 * kEmitPlanes + 12) * gx + 6 * kEmitCapW, stream, gx,
                            gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
