@@ -145,6 +145,7 @@ size_t carve_geom(void* base, int P, uint32_t gx, uint32_t gy, GeomState& g, Car
     g.scan_tmp = t.take<char>(g.scan_tmp_bytes);
     g.dsort_tmp_bytes = depth_sort_temp_bytes(P);
     g.dsort_tmp = t.take<char>(g.dsort_tmp_bytes);
+    g.foot = t.take<uint4>((size_t)2 * P);
     return c.off + 256;
 }
 

@@ -79,6 +79,7 @@ struct GeomState {
     size_t scan_tmp_bytes;
     void* dsort_tmp;
     size_t dsort_tmp_bytes;
+    uint4* foot;  // forward-only: [P][2] tile footprint (x, y, conic.a, conic.b), (conic.c, opacity coef, rect) (tilelists.hip)
 };
 // ---- per-instance state (replaces BinningState) ----
 // tile ids as 16-bit sort keys when the grid allows (<= 65536 tiles)
@@ -87,7 +88,7 @@ inline int tile_key_bytes(int tile_bits) { return tile_bits <= 16 ? 2 : 4; }
 constexpr int kMaxGrid = 1024;
 enum BinPath : int { kBinInstanceSort = 0, kBinLists = 1 };
 struct ListLayout {
-    int nseg_rows = 0, nseg_tiles_max = 0;
+    int nseg_rows = 0, nseg_tiles_max = 0, rowseg = 64;
     size_t tmp_bytes = 0;
 };
 struct BinningState {

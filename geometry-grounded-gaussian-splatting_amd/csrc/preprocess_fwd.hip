@@ -45,6 +45,7 @@ struct PreprocessArgs {
     float* depths;
     Splat* splats;
     uint32_t* tiles_touched;
+    uint4* foot;  // [P][2] tile footprint for the rows pass (GeomState::foot); its rect is empty when culled
     bool no_color;
     uint32_t* zero_first;  // words zeroed for the next kernels (dsort state; dsort_zero_region)
     size_t zero_words;
@@ -53,6 +54,16 @@ struct PreprocessArgs {
 
 // ndc2Pix in double, as the reference (auxiliary.h:38-40)
 __device__ inline float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+// The rows pass of the tile lists (tilelists.hip) gathers, per Gaussian in
+// depth order, exactly the footprint written here: the splat's centre,
+// conic and opacity coefficient (bit for bit the Splat record's) and the
+// tile rect packed as x0 | y0 << 16, x1 | y1 << 16 — one 32-B piece instead
+// of the splat's first half plus the radius (two sectors and two dependent
+// round trips).  A culled Gaussian gets an empty rect.
+__device__ __forceinline__ void cull_foot(const PreprocessArgs& a, int idx) {
+    a.foot[2 * (size_t)idx + 1] = make_uint4(0u, 0u, 0u, 0u);
+}
 
 // HOIST (the SH 3 + SG 7 colour model, BASELINE C5): the colour rows (192-B
 // SH row, 196-B SG lobe rows) are requested at the top with the geometry
@@ -91,7 +102,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     }
     const float* V = a.view;
     const ViewGeom g = view_geom(V, px, py, pz, a.tan_fovx, a.tan_fovy);
-    if (g.t[2] <= kNearPlane) return;  // in_frustum (auxiliary.h:133-153)
+    if (g.t[2] <= kNearPlane) {  // in_frustum (auxiliary.h:133-153)
+        cull_foot(a, idx);
+        return;
+    }
 
     const float* Pm = a.proj;
     const float hx = Pm[0] * px + Pm[4] * py + Pm[8] * pz + Pm[12];
@@ -221,7 +235,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
 
     // conic, radius, rect (render_forward.cu:347-368)
     const float det = ca * cc - cb * cb;
-    if (det == 0.0f) return;
+    if (det == 0.0f) {
+        cull_foot(a, idx);
+        return;
+    }
     const float det_inv = 1.f / det;
     const float mid = 0.5f * (ca + cc);
     const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -233,7 +250,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     const uint32_t rmaxx = min(a.grid_x, (uint32_t)max(0, (int)((xpix + r + kTile - 1) / kTile)));
     const uint32_t rmaxy = min(a.grid_y, (uint32_t)max(0, (int)((ypix + r + kTile - 1) / kTile)));
     const uint32_t area = (rmaxx - rminx) * (rmaxy - rminy);
-    if (area == 0) return;
+    if (area == 0) {
+        cull_foot(a, idx);
+        return;
+    }
 
     // colour (render_forward.cu:22-78)
     float col[3];
@@ -327,6 +347,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     sp.w2 = make_float4(g.tc, rsig, col[0], col[1]);
     sp.w3 = make_float4(col[2], cnx * inn, cny * inn, cnz * inn);
     a.splats[idx] = sp;
+    a.foot[2 * (size_t)idx] = make_uint4(__float_as_uint(sp.w0.x), __float_as_uint(sp.w0.y), __float_as_uint(sp.w0.z),
+                                         __float_as_uint(sp.w0.w));
+    a.foot[2 * (size_t)idx + 1] = make_uint4(__float_as_uint(sp.w1.x), __float_as_uint(sp.w1.y), rminx | (rminy << 16),
+                                             rmaxx | (rmaxy << 16));
     a.depths[idx] = g.tc;
     a.radii[idx] = r;
     a.tiles_touched[idx] = area;
@@ -370,6 +394,7 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
     a.depths = gs.depths;
     a.splats = gs.splats;
     a.tiles_touched = gs.tiles_touched;
+    a.foot = gs.foot;
     dsort_zero_region(gs.dsort_tmp, p.P, &a.zero_first, &a.zero_words);
     a.zero_K = gs.offsets_K;
     // (the hoisted instance needs every colour row: SH + 7 SG lobes, scales / rotations, no precomputed colours)

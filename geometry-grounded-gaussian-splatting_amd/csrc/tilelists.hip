@@ -35,10 +35,16 @@ namespace gsr {
 #ifndef GSR_ROW_SEG
 #define GSR_ROW_SEG 64  // measured at C3: tile_lists 0.248 ms vs 0.256 (128), 0.277 (96), 0.31 (256), 0.39 (512)
 #endif
+#ifndef GSR_ROW_SEG_BIG
+#define GSR_ROW_SEG_BIG GSR_ROW_SEG  // row-pass segment for P > kRowSegBigP (multiple of 64)
+#endif
 #ifndef GSR_TILE_SEG
 #define GSR_TILE_SEG 512
 #endif
 constexpr int kRowSeg = GSR_ROW_SEG;    // Gaussians per row-pass segment
+constexpr int kRowSegBig = GSR_ROW_SEG_BIG;
+constexpr int kRowSegBigP = 2000000;
+static_assert(kRowSeg % 64 == 0 && kRowSegBig % 64 == 0, "row-pass segments are whole 64-entry chunks");
 constexpr int kTileSeg = GSR_TILE_SEG;  // row entries per tile-pass segment
 
 // ------------------------------------------- exclusive scan, device-sized
@@ -189,7 +195,8 @@ bool list_binning(uint32_t gx, uint32_t gy) { return gx <= (uint32_t)kMaxGrid &&
 
 ListLayout list_layout(int P, int K, uint32_t gx, uint32_t gy) {
     ListLayout L;
-    L.nseg_rows = (P + kRowSeg - 1) / kRowSeg;
+    L.rowseg = P > kRowSegBigP ? kRowSegBig : kRowSeg;
+    L.nseg_rows = (P + L.rowseg - 1) / L.rowseg;
     L.nseg_tiles_max = (K + kTileSeg - 1) / kTileSeg + (int)gy;
     size_t a = 0, b = 0, c = 0;
     (void)rocprim::exclusive_scan(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
@@ -221,17 +228,24 @@ struct QGauss {  // one Gaussian in q order, as the row kernels need it
     Ellipse E;
     TileRect R;
 };
-__device__ __forceinline__ QGauss load_q(int q, int q1, const uint32_t* order, const Splat* splats,
-                                         const int* radii, uint32_t gx, uint32_t gy, float pad) {
+// the Gaussian at q: its footprint (GeomState::foot, written by the
+// preprocess: the Splat record's centre, conic and opacity coefficient bit
+// for bit, and the tile_rect of its radius; an empty rect when culled)
+__device__ __forceinline__ QGauss load_q(int q, int q1, const uint32_t* order, const uint4* foot, float pad) {
     QGauss G{};
     if (q >= q1) return G;
     G.g = order[q];
-    const int r = radii[G.g];
-    if (r <= 0) return G;
-    const float4 w0 = splats[G.g].w0, w1 = splats[G.g].w1;
+    const uint4 f0 = foot[2 * (size_t)G.g], f1 = foot[2 * (size_t)G.g + 1];
+    G.R.x0 = f1.z & 0xffffu;
+    G.R.y0 = f1.z >> 16;
+    G.R.x1 = f1.w & 0xffffu;
+    G.R.y1 = f1.w >> 16;
+    if (!(G.R.x1 > G.R.x0 && G.R.y1 > G.R.y0)) return G;
+    const float4 w0 = make_float4(__uint_as_float(f0.x), __uint_as_float(f0.y), __uint_as_float(f0.z),
+                                  __uint_as_float(f0.w));
+    const float4 w1 = make_float4(__uint_as_float(f1.x), __uint_as_float(f1.y), 0.f, 0.f);
     G.E = make_ellipse(w0, w1, pad);
-    G.R = tile_rect(w0.x, w0.y, r, gx, gy);
-    G.on = G.E.mode != 2 && G.R.x1 > G.R.x0 && G.R.y1 > G.R.y0;
+    G.on = G.E.mode != 2;
     return G;
 }
 
@@ -245,17 +259,16 @@ constexpr int kRecSpans = 6;
 constexpr uint32_t kNoSpan = 0xffffffffu;  // (spans are lo | hi << 16 with hi < 1024)
 
 __global__ void __launch_bounds__(64)
-    rows_count_kernel(int P, int nseg, uint32_t gx, uint32_t gy, float pad, const uint32_t* __restrict__ order,
-                      const Splat* __restrict__ splats, const int* __restrict__ radii, uint32_t* __restrict__ M,
-                      uint4* __restrict__ qrec) {
+    rows_count_kernel(int P, int nseg, int rowseg, uint32_t gy, float pad, const uint32_t* __restrict__ order,
+                      const uint4* __restrict__ foot, uint32_t* __restrict__ M, uint4* __restrict__ qrec) {
     extern __shared__ unsigned long long s_dyn[];
     uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
     const int seg = (int)xcd_remap(blockIdx.x, gridDim.x), lane = threadIdx.x;  // XCD-contiguous segments
     for (uint32_t y = lane; y < gy; y += 64) s_cnt[y] = 0u;
     __syncthreads();
-    const int q0 = seg * kRowSeg, q1 = min(P, q0 + kRowSeg);
+    const int q0 = seg * rowseg, q1 = min(P, q0 + rowseg);
     for (int q = q0 + lane; q < q1; q += 64) {
-        const QGauss G = load_q(q, q1, order, splats, radii, gx, gy, pad);
+        const QGauss G = load_q(q, q1, order, foot, pad);
         uint32_t lo, hi;
         // the record rows_emit reads instead of re-gathering and re-spanning
         uint32_t sp[kRecSpans];
@@ -286,34 +299,43 @@ __global__ void __launch_bounds__(64)
 // entries does rank, write and advance.  The row-wide prologue of each chunk
 // carries the untouched running slots over and clears the next chunk's masks.
 __global__ void __launch_bounds__(64)
-    rows_emit_kernel(int P, int nseg, uint32_t gx, uint32_t gy, float pad, const uint32_t* __restrict__ order,
-                     const Splat* __restrict__ splats, const int* __restrict__ radii, const uint32_t* __restrict__ O,
-                     const uint4* __restrict__ qrec, uint2* __restrict__ rows) {
+    rows_emit_kernel(int P, int nseg, int rowseg, uint32_t gy, float pad, const uint32_t* __restrict__ order,
+                     const uint4* __restrict__ foot, const uint32_t* __restrict__ O, const uint4* __restrict__ qrec,
+                     uint2* __restrict__ rows) {
     extern __shared__ unsigned long long s_dyn[];  // 2 x [gy] masks, then 2 x [gy] running slots
     unsigned long long* s_cov = s_dyn;
     uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * gy);
     const int seg = (int)xcd_remap(blockIdx.x, gridDim.x), lane = threadIdx.x;  // XCD-contiguous segments
+    const int q0 = seg * rowseg, q1 = min(P, q0 + rowseg);
+    // the first chunk's records are requested before the strided running-slot
+    // loads, so the two round trips overlap; later chunks' one chunk ahead
+    uint4 n0 = make_uint4(kNoSpan, 0u, kNoSpan, kNoSpan), n1 = make_uint4(kNoSpan, kNoSpan, kNoSpan, kNoSpan);
+    if (q0 + lane < q1) {
+        n0 = qrec[2 * (size_t)(q0 + lane)];
+        n1 = qrec[2 * (size_t)(q0 + lane) + 1];
+    }
     for (uint32_t y = lane; y < gy; y += 64) {
         s_run[y] = O[(size_t)y * nseg + seg];
         s_cov[y] = 0ull;
     }
     __syncthreads();
     const unsigned long long bit = 1ull << lane, below = bit - 1ull;
-    const int q0 = seg * kRowSeg, q1 = min(P, q0 + kRowSeg);
     uint32_t cur = 0;
     for (int c0 = q0; c0 < q1; c0 += 64, cur ^= 1u) {
         unsigned long long* cov = s_cov + cur * gy;
         const uint32_t* run = s_run + cur * gy;
         uint32_t* run_next = s_run + (cur ^ 1u) * gy;
+        const int q = c0 + lane;
+        const uint4 r0 = n0, r1 = n1;
+        n0 = make_uint4(kNoSpan, 0u, kNoSpan, kNoSpan);
+        n1 = make_uint4(kNoSpan, kNoSpan, kNoSpan, kNoSpan);
+        if (q + 64 < q1) {
+            n0 = qrec[2 * (size_t)(q + 64)];
+            n1 = qrec[2 * (size_t)(q + 64) + 1];
+        }
         for (uint32_t y = lane; y < gy; y += 64) {
             run_next[y] = run[y];
             s_cov[(cur ^ 1u) * gy + y] = 0ull;
-        }
-        const int q = c0 + lane;
-        uint4 r0 = make_uint4(kNoSpan, 0u, kNoSpan, kNoSpan), r1 = make_uint4(kNoSpan, kNoSpan, kNoSpan, kNoSpan);
-        if (q < q1) {
-            r0 = qrec[2 * (size_t)q];
-            r1 = qrec[2 * (size_t)q + 1];
         }
         const bool on = r0.x != kNoSpan;
         const uint32_t y0 = r0.y & 0xffffu, y1 = r0.y >> 16;
@@ -321,7 +343,7 @@ __global__ void __launch_bounds__(64)
         // rows past the record: the splat's ellipse, as rows_count had it
         const bool tall = on && y1 > y0 + kRecSpans;
         QGauss G{};
-        if (tall) G = load_q(q, q1, order, splats, radii, gx, gy, pad);
+        if (tall) G = load_q(q, q1, order, foot, pad);
         uint32_t lo, hi;
 #pragma unroll
         for (int k = 0; k < kRecSpans; k++)
@@ -346,8 +368,8 @@ __global__ void __launch_bounds__(64)
     }
 }
 
-// Coalesced emission helpers (tiles_emit_sorted_kernel below).  (The rows
-// pass with the same staging measured 0.234 -> 0.239 ms at C3, 1.018 -> 1.008
+// Coalesced emission helper (the tiles pass below).  (The rows
+// pass with the staged emission measured 0.234 -> 0.239 ms at C3, 1.018 -> 1.008
 // at C5: not adopted; its 8-B entries land in only ~5 rows per Gaussian.)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     const int lane = threadIdx.x & 63;
@@ -357,29 +379,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
         if (lane >= o) x += y;
     }
     return x;
-}
-
-// per bucket b < n: its count in the chunk (popcount of its mask), its base
-// among the chunk's entries, its write base; advances the running slots.
-// Returns the chunk's entry total (wave-uniform).
-__device__ __forceinline__ uint32_t chunk_bases(uint32_t n, const unsigned long long* cov, uint32_t* run,
-                                                uint32_t* off, uint32_t* wbase) {
-    const int lane = threadIdx.x & 63;
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
-        const uint32_t b = b0 + lane;
-        const uint32_t cnt = b < n ? (uint32_t)__popcll(cov[b]) : 0u;
-        const uint32_t incl = wave_incl_scan(cnt);
-        if (b < n) {
-            const uint32_t o = carry + incl - cnt;
-            const uint32_t r = run[b];
-            off[b] = o;
-            wbase[b] = r - o;
-            run[b] = r + cnt;
-        }
-        carry += __shfl(incl, 63, 64);
-    }
-    return carry;
 }
 
 // --------------------------------------------------------------- tiles pass
@@ -442,6 +441,37 @@ __device__ __forceinline__ TileSeg find_seg(uint32_t b, uint32_t gy, const uint3
     return S;
 }
 
+// The segment table in LDS: segbase[0..gy] and every row's first entry
+// (row_begin), so locating a segment is a binary search over LDS instead of
+// ~log2(gy) + 3 dependent global round trips per segment.
+__device__ __forceinline__ void stage_seg_table(uint32_t gy, int nseg_rows, const uint32_t* O_rows,
+                                                const uint32_t* M_rows_last, const uint32_t* segbase, uint32_t* s_sb,
+                                                uint32_t* s_rb) {
+    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
+    for (uint32_t y = threadIdx.x; y <= gy; y += blockDim.x) {
+        s_sb[y] = segbase[y];
+        s_rb[y] = row_begin(O_rows, nseg_rows, y, gy, total);
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ TileSeg find_seg_lds(uint32_t b, uint32_t gy, const uint32_t* s_sb, const uint32_t* s_rb) {
+    TileSeg S{};
+    if (b >= s_sb[gy]) return S;
+    uint32_t lo = 0, hi = gy;  // largest y with segbase[y] <= b
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_sb[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    S.on = true;
+    S.y = lo;
+    S.k = b - s_sb[lo];
+    S.nk = s_sb[lo + 1] - s_sb[lo];
+    S.e0 = s_rb[lo] + S.k * kTileSeg;
+    S.e1 = min(s_rb[lo + 1], S.e0 + kTileSeg);
+    return S;
+}
+
 // The tile-pass kernels run a fixed grid that walks the actual segments
 // (segbase[gy], known on the device only).  Blocks are dealt round-robin over
 // the 8 XCDs; XCD x takes the x-th eighth of the segments, and its blocks
@@ -466,12 +496,14 @@ __global__ void __launch_bounds__(64)
     tiles_count_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
                        const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
                        const uint2* __restrict__ rows, uint32_t* __restrict__ M) {
-    extern __shared__ unsigned long long s_dyn[];
+    extern __shared__ unsigned long long s_dyn[];  // [gx] counts, then the segment table (2 x [gy + 1])
     uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
+    uint32_t* s_sb = s_cnt + gx;
+    uint32_t* s_rb = s_sb + gy + 1;
     const int lane = threadIdx.x;
-    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
-    for_xcd_segments(segbase[gy], [&](uint32_t l) {
-        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
+    stage_seg_table(gy, nseg_rows, O_rows, M_rows_last, segbase, s_sb, s_rb);
+    for_xcd_segments(s_sb[gy], [&](uint32_t l) {
+        const TileSeg S = find_seg_lds(l, gy, s_sb, s_rb);
         __syncthreads();  // previous segment's counts read out
         for (uint32_t x = lane; x < gx; x += 64) s_cnt[x] = 0u;
         __syncthreads();
@@ -480,122 +512,14 @@ __global__ void __launch_bounds__(64)
             for (uint32_t x = sp & 0xffffu; x <= (sp >> 16); x++) atomicAdd(&s_cnt[x], 1u);
         }
         __syncthreads();
-        const size_t base = (size_t)gx * segbase[S.y];
+        const size_t base = (size_t)gx * s_sb[S.y];
         for (uint32_t x = lane; x < gx; x += 64) M[base + (size_t)x * S.nk + S.k] = s_cnt[x];
     });
 }
 
-__global__ void __launch_bounds__(64)
-    tiles_emit_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
-                      const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
-                      const uint2* __restrict__ rows, const uint32_t* __restrict__ O, uint32_t* __restrict__ point_list) {
-    extern __shared__ unsigned long long s_dyn[];  // 2 x [gx] masks, then 2 x [gx] running slots (rows_emit_kernel)
-    unsigned long long* s_cov = s_dyn;
-    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * gx);
-    const int lane = threadIdx.x;
-    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
-    const unsigned long long bit = 1ull << lane, below = bit - 1ull;
-    for_xcd_segments(segbase[gy], [&](uint32_t l) {
-        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
-        const size_t base = (size_t)gx * segbase[S.y];
-        __syncthreads();  // previous segment done with the LDS
-        for (uint32_t x = lane; x < gx; x += 64) {
-            s_run[x] = O[base + (size_t)x * S.nk + S.k];
-            s_cov[x] = 0ull;
-        }
-        __syncthreads();
-        uint32_t cur = 0;
-        for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64, cur ^= 1u) {
-            unsigned long long* cov = s_cov + cur * gx;
-            const uint32_t* run = s_run + cur * gx;
-            uint32_t* run_next = s_run + (cur ^ 1u) * gx;
-            for (uint32_t x = lane; x < gx; x += 64) {
-                run_next[x] = run[x];
-                s_cov[(cur ^ 1u) * gx + x] = 0ull;
-            }
-            const uint32_t e = c0 + lane;
-            const bool on = e < S.e1;
-            const uint2 ent = on ? rows[e] : make_uint2(0u, 1u);  // empty span when off
-            const uint32_t lo = ent.y & 0xffffu, hi = on ? (ent.y >> 16) : 0u;
-            for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&cov[x], bit);
-            __syncthreads();
-            for (uint32_t x = lo; on && x <= hi; x++) {
-                const unsigned long long m = cov[x];
-                const uint32_t r0 = run[x];
-                point_list[r0 + (uint32_t)__popcll(m & below)] = ent.x;
-                if ((m & below) == 0ull) run_next[x] = r0 + (uint32_t)__popcll(m);
-            }
-            __syncthreads();
-        }
-    });
-}
-
-// tiles_emit with the writes coalesced: the direct emission above writes one
-// 4-B id per lane to ~64 different tiles per store instruction (one L2
-// request per lane).  Here a chunk's instances are first placed in LDS
-// ordered by (tile, rank) — a tile's base in the chunk is the exclusive
-// scan of the tiles' counts, popcount(cov[x]) — and then written out by
-// consecutive lanes to consecutive slots of the same tile's run.  Same
-// slots, same values; chunks with more than kEmitCap instances write
-// directly.
 #ifndef GSR_TILES_EMIT_SORTED
-#define GSR_TILES_EMIT_SORTED 3  // 3: tiles_emit_coop_kernel (default, grids <= 256 tiles wide), 2: tiles_emit_wide_kernel, 1: 64-entry chunks, 0: direct
+#define GSR_TILES_EMIT_SORTED 3  // 3: tiles_emit_coop_kernel (default, grids <= 256 tiles wide), 2: tiles_emit_wide_kernel
 #endif
-constexpr int kEmitCap = 512;  // instances staged per 64-entry chunk (C3 averages ~3 tiles per row entry)
-
-__global__ void __launch_bounds__(64)
-    tiles_emit_sorted_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
-                             const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
-                             const uint2* __restrict__ rows, const uint32_t* __restrict__ O,
-                             uint32_t* __restrict__ point_list) {
-    // LDS: [gx] masks, [gx] running slots, [gx] chunk offsets, [gx] write bases, kEmitCap ids and tiles
-    extern __shared__ unsigned long long s_dyn[];
-    unsigned long long* s_cov = s_dyn;
-    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + gx);
-    uint32_t* s_off = s_run + gx;
-    uint32_t* s_base = s_off + gx;
-    uint32_t* s_id = s_base + gx;
-    uint16_t* s_x = reinterpret_cast<uint16_t*>(s_id + kEmitCap);
-    const int lane = threadIdx.x;
-    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
-    const unsigned long long bit = 1ull << lane, below = bit - 1ull;
-    for_xcd_segments(segbase[gy], [&](uint32_t l) {
-        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
-        const size_t base = (size_t)gx * segbase[S.y];
-        __syncthreads();  // previous segment done with the LDS
-        for (uint32_t x = lane; x < gx; x += 64) {
-            s_run[x] = O[base + (size_t)x * S.nk + S.k];
-            s_cov[x] = 0ull;
-        }
-        __syncthreads();
-        for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64) {
-            const uint32_t e = c0 + lane;
-            const bool on = e < S.e1;
-            const uint2 ent = on ? rows[e] : make_uint2(0u, 1u);  // empty span when off
-            const uint32_t lo = ent.y & 0xffffu, hi = on ? (ent.y >> 16) : 0u;
-            for (uint32_t x = lo; on && x <= hi; x++) atomicOr(&s_cov[x], bit);
-            __syncthreads();
-            // per tile: its count in the chunk, its base among the chunk's instances, its write base
-            const uint32_t carry = chunk_bases(gx, s_cov, s_run, s_off, s_base);
-            __syncthreads();
-            if (carry <= (uint32_t)kEmitCap) {
-                for (uint32_t x = lo; on && x <= hi; x++) {
-                    const uint32_t p = s_off[x] + (uint32_t)__popcll(s_cov[x] & below);
-                    s_id[p] = ent.x;
-                    s_x[p] = (uint16_t)x;
-                }
-                __syncthreads();
-                for (uint32_t p = lane; p < carry; p += 64) point_list[s_base[s_x[p]] + p] = s_id[p];
-            } else {
-                for (uint32_t x = lo; on && x <= hi; x++)
-                    point_list[s_base[x] + s_off[x] + (uint32_t)__popcll(s_cov[x] & below)] = ent.x;
-            }
-            __syncthreads();
-            for (uint32_t x = lane; x < gx; x += 64) s_cov[x] = 0ull;
-            __syncthreads();
-        }
-    });
-}
 
 // tiles_emit_sorted with chunks of 64 NPL entries (NPL per lane: entries
 // c0 + 64 h + lane, h < NPL, with a mask plane each), so the per-chunk work —
@@ -721,14 +645,58 @@ __global__ void __launch_bounds__(64)
 #define GSR_COOP_CAP 2048
 #endif
 constexpr int kCoopBlocks = GSR_COOP_BLOCKS;
-constexpr int kCoopWaves = 4, kCoopPlanes = 2;  // 512 entries per round: one kTileSeg segment
+constexpr int kCoopWaves = 4, kCoopPlanes = 2;  // 512 entries per segment: one round
+static_assert(64 * kCoopWaves * kCoopPlanes == kTileSeg, "a tile-pass segment is one coop round");
 constexpr uint32_t kCoopCap = GSR_COOP_CAP;     // instances staged per round (more: direct writes)
-constexpr int kCoopMaxGx = 256;                 // wider grids keep tiles_emit_wide_kernel (LDS)
-size_t coop_lds_bytes(uint32_t gx) {
+constexpr int kCoopMaxGx = 64 * kCoopWaves;     // one running slot per thread; wider grids keep tiles_emit_wide_kernel
+size_t coop_lds_bytes(uint32_t gx, uint32_t gy) {
     constexpr int kPl = kCoopWaves * kCoopPlanes;
-    return (size_t)8 * kPl * gx + (size_t)4 * (3 + kPl) * gx + (size_t)6 * kCoopCap;
+    return (size_t)2 * 8 * kPl * gx + (size_t)4 * (3 + kPl) * gx + (size_t)6 * kCoopCap + (size_t)8 * (gy + 1);
 }
 
+// One segment's inputs, requested a segment ahead: its entries (NPL per lane)
+// and its running slots (one tile per thread).
+template <int NW, int NPL>
+struct CoopSeg {
+    TileSeg S;
+    uint32_t run;
+    uint2 ent[NPL];
+};
+template <int NW, int NPL>
+__device__ __forceinline__ CoopSeg<NW, NPL> coop_fetch(uint32_t l, uint32_t hi, uint32_t gx, uint32_t gy,
+                                                       const uint32_t* s_sb, const uint32_t* s_rb, const uint2* rows,
+                                                       const uint32_t* O) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    CoopSeg<NW, NPL> c;
+    c.S = l < hi ? find_seg_lds(l, gy, s_sb, s_rb) : TileSeg{};
+    c.run = 0u;
+    if (c.S.on && (uint32_t)tid < gx) c.run = O[(size_t)gx * s_sb[c.S.y] + (size_t)tid * c.S.nk + c.S.k];
+#pragma unroll
+    for (int h = 0; h < NPL; h++) {
+        const uint32_t e = c.S.e0 + 64 * (NPL * wave + h) + lane;
+        c.ent[h] = c.S.on && e < c.S.e1 ? rows[e] : make_uint2(0u, 1u);  // (lo 1 > hi 0: empty span)
+    }
+    return c;
+}
+
+// tiles_emit with whole-workgroup segments (round 3).  The single-wave
+// emission runs ~1000 blocks per XCD, so every segment of the XCD's share is
+// in flight at once and the point-list region being written (~6.5 MB per XCD
+// at C3) exceeds its 4 MB L2: partial lines leave the L2 before they are
+// complete (WRITE_SIZE 158 MB per C3 launch against 52 MB of point list;
+// with 128 single-wave blocks per XCD the writes fall to 53 MB, but then the
+// launch is latency-bound).  Here NW waves work one segment (one round of
+// 64 NW NPL entries) together: entry e0 + 64 (NPL w + h) + lane is wave w's
+// plane h, and a tile's rank counts the planes before, then the lower lanes;
+// the round's instances are staged in LDS by (tile, rank) and written by
+// consecutive lanes; kCoopBlocks / 8 blocks per XCD walk its segments in
+// lockstep strides, so the region in flight is a row or two.  Same slots,
+// same values.  Per segment the block is a chain of dependent steps, so:
+// the segment table sits in LDS (find_seg_lds); the next segment's entries
+// and running slots are requested before this one is worked; and the mask
+// planes are double-buffered (a buffer is cleared while the round's ids are
+// written out, and reused two segments later), which leaves three barriers
+// per segment.
 template <int NW, int NPL>
 __global__ void __launch_bounds__(64 * NW)
     tiles_emit_coop_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
@@ -737,99 +705,101 @@ __global__ void __launch_bounds__(64 * NW)
                            uint32_t* __restrict__ point_list) {
     constexpr int kPl = NW * NPL;
     constexpr int kThreads = 64 * NW;
-    // LDS: kPl x [gx] masks; [gx] running slots, chunk offsets, write bases; kPl x [gx] plane prefixes;
-    // kCoopCap ids and tiles
+    // LDS: 2 x kPl x [gx] masks; [gx] running slots, chunk offsets, write bases; kPl x [gx] plane prefixes;
+    // kCoopCap ids and tiles; the segment table
     extern __shared__ unsigned long long s_dyn[];
-    unsigned long long* s_cov = s_dyn;
-    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + kPl * gx);
+    unsigned long long* s_cov2 = s_dyn;
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * kPl * gx);
     uint32_t* s_off = s_run + gx;
     uint32_t* s_base = s_off + gx;
     uint32_t* s_pl = s_base + gx;
     uint32_t* s_id = s_pl + kPl * gx;
     uint16_t* s_x = reinterpret_cast<uint16_t*>(s_id + kCoopCap);
+    uint32_t* s_sb = reinterpret_cast<uint32_t*>(s_x + kCoopCap);
+    uint32_t* s_rb = s_sb + gy + 1;
     __shared__ uint32_t s_carry;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
     const unsigned long long bit = 1ull << lane, below = bit - 1ull;
-    for_xcd_segments(segbase[gy], [&](uint32_t l) {
-        const TileSeg S = find_seg(l, gy, segbase, O_rows, nseg_rows, total);
-        const size_t base = (size_t)gx * segbase[S.y];
-        __syncthreads();  // previous segment done with the LDS
-        for (uint32_t x = tid; x < gx; x += kThreads) s_run[x] = O[base + (size_t)x * S.nk + S.k];
-        for (uint32_t x = tid; x < kPl * gx; x += kThreads) s_cov[x] = 0ull;
+    for (uint32_t x = tid; x < 2 * kPl * gx; x += kThreads) s_cov2[x] = 0ull;
+    stage_seg_table(gy, nseg_rows, O_rows, M_rows_last, segbase, s_sb, s_rb);  // (ends with a barrier)
+    const uint32_t n = s_sb[gy];
+    const uint32_t xcd = blockIdx.x % 8u, slot0 = blockIdx.x / 8u, nslots = gridDim.x / 8u;
+    const uint32_t lo_l = (uint32_t)(((unsigned long long)n * xcd) / 8u);
+    const uint32_t hi_l = (uint32_t)(((unsigned long long)n * (xcd + 1u)) / 8u);
+    uint32_t l = lo_l + slot0, buf = 0;
+    CoopSeg<NW, NPL> cur = coop_fetch<NW, NPL>(l, hi_l, gx, gy, s_sb, s_rb, rows, O);
+    while (cur.S.on) {
+        const CoopSeg<NW, NPL> nxt = coop_fetch<NW, NPL>(l + nslots, hi_l, gx, gy, s_sb, s_rb, rows, O);
+        unsigned long long* s_cov = s_cov2 + buf * kPl * gx;
+        // (s_run is read only by wave 0's scan below, after the barrier that ends the previous segment's writes)
+        if ((uint32_t)tid < gx) s_run[tid] = cur.run;
+        uint32_t id[NPL], lo[NPL], hi[NPL];
+#pragma unroll
+        for (int h = 0; h < NPL; h++) {
+            id[h] = cur.ent[h].x;
+            lo[h] = cur.ent[h].y & 0xffffu;
+            hi[h] = cur.ent[h].y >> 16;
+            unsigned long long* cov = s_cov + (NPL * wave + h) * gx;
+            for (uint32_t x = lo[h]; x <= hi[h]; x++) atomicOr(&cov[x], bit);
+        }
         __syncthreads();
-        for (uint32_t c0 = S.e0; c0 < S.e1; c0 += 64 * kPl) {
-            bool on[NPL];
-            uint32_t id[NPL], lo[NPL], hi[NPL];
+        // per tile (wave 0): plane prefixes, count, base among the round's instances, write base
+        if (wave == 0) {
+            uint32_t carry = 0;
+            for (uint32_t b0 = 0; b0 < gx; b0 += 64) {
+                const uint32_t b = b0 + lane;
+                uint32_t cnt = 0;
+                if (b < gx) {
 #pragma unroll
-            for (int h = 0; h < NPL; h++) {
-                const uint32_t e = c0 + 64 * (NPL * wave + h) + lane;
-                on[h] = e < S.e1;
-                const uint2 ent = on[h] ? rows[e] : make_uint2(0u, 1u);  // empty span when off
-                id[h] = ent.x;
-                lo[h] = ent.y & 0xffffu;
-                hi[h] = on[h] ? (ent.y >> 16) : 0u;
-            }
-#pragma unroll
-            for (int h = 0; h < NPL; h++) {
-                unsigned long long* cov = s_cov + (NPL * wave + h) * gx;
-                for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++) atomicOr(&cov[x], bit);
-            }
-            __syncthreads();
-            // per tile (wave 0): plane prefixes, count, base among the round's instances, write base
-            if (wave == 0) {
-                uint32_t carry = 0;
-                for (uint32_t b0 = 0; b0 < gx; b0 += 64) {
-                    const uint32_t b = b0 + lane;
-                    uint32_t cnt = 0;
-                    if (b < gx) {
-#pragma unroll
-                        for (int p = 0; p < kPl; p++) {
-                            s_pl[p * gx + b] = cnt;
-                            cnt += (uint32_t)__popcll(s_cov[p * gx + b]);
-                        }
-                    }
-                    const uint32_t incl = wave_incl_scan(cnt);
-                    if (b < gx) {
-                        const uint32_t o = carry + incl - cnt;
-                        const uint32_t r = s_run[b];
-                        s_off[b] = o;
-                        s_base[b] = r - o;
-                        s_run[b] = r + cnt;
-                    }
-                    carry += __shfl(incl, 63, 64);
-                }
-                if (lane == 0) s_carry = carry;
-            }
-            __syncthreads();
-            const uint32_t carry = s_carry;
-            auto slot = [&](int p, uint32_t x) {
-                return s_off[x] + s_pl[p * gx + x] + (uint32_t)__popcll(s_cov[p * gx + x] & below);
-            };
-            if (carry <= kCoopCap) {
-#pragma unroll
-                for (int h = 0; h < NPL; h++) {
-                    const int p = NPL * wave + h;
-                    for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++) {
-                        const uint32_t q = slot(p, x);
-                        s_id[q] = id[h];
-                        s_x[q] = (uint16_t)x;
+                    for (int p = 0; p < kPl; p++) {
+                        s_pl[p * gx + b] = cnt;
+                        cnt += (uint32_t)__popcll(s_cov[p * gx + b]);
                     }
                 }
-                __syncthreads();
-                for (uint32_t q = tid; q < carry; q += kThreads) point_list[s_base[s_x[q]] + q] = s_id[q];
-            } else {
+                const uint32_t incl = wave_incl_scan(cnt);
+                if (b < gx) {
+                    const uint32_t o = carry + incl - cnt;
+                    s_off[b] = o;
+                    s_base[b] = s_run[b] - o;
+                }
+                carry += __shfl(incl, 63, 64);
+            }
+            if (lane == 0) s_carry = carry;
+        }
+        __syncthreads();
+        const uint32_t carry = s_carry;
+        auto slot = [&](int p, uint32_t x) {
+            return s_off[x] + s_pl[p * gx + x] + (uint32_t)__popcll(s_cov[p * gx + x] & below);
+        };
+        if (carry <= kCoopCap) {
 #pragma unroll
-                for (int h = 0; h < NPL; h++) {
-                    const int p = NPL * wave + h;
-                    for (uint32_t x = lo[h]; on[h] && x <= hi[h]; x++) point_list[s_base[x] + slot(p, x)] = id[h];
+            for (int h = 0; h < NPL; h++) {
+                const int p = NPL * wave + h;
+                for (uint32_t x = lo[h]; x <= hi[h]; x++) {
+                    const uint32_t q = slot(p, x);
+                    s_id[q] = id[h];
+                    s_x[q] = (uint16_t)x;
                 }
             }
             __syncthreads();
             for (uint32_t x = tid; x < kPl * gx; x += kThreads) s_cov[x] = 0ull;
+            for (uint32_t q = tid; q < carry; q += kThreads) point_list[s_base[s_x[q]] + q] = s_id[q];
+        } else {
+#pragma unroll
+            for (int h = 0; h < NPL; h++) {
+                const int p = NPL * wave + h;
+                for (uint32_t x = lo[h]; x <= hi[h]; x++) point_list[s_base[x] + slot(p, x)] = id[h];
+            }
             __syncthreads();
+            for (uint32_t x = tid; x < kPl * gx; x += kThreads) s_cov[x] = 0ull;
         }
-    });
+        // The next segment's mask atomics use the other buffer (cleared one segment ago, before this
+        // segment's first barrier); its scan rewrites s_off / s_base / s_pl / s_carry only after its
+        // first barrier, which every wave reaches after finishing the writes above.
+        cur = nxt;
+        l += nslots;
+        buf ^= 1u;
+    }
 }
 
 __global__ void __launch_bounds__(256)
@@ -854,9 +824,8 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     const ListLayout& L = bs.lists;
     hipError_t e;
     // rows pass
-    hipLaunchKernelGGL(rows_count_kernel, dim3(L.nseg_rows), dim3(64), 4 * gy, stream, p.P, L.nseg_rows, gx, gy,
-                       p.cull_pad, gs.order,
-                       gs.splats, radii, bs.rows_count, bs.qrec);
+    hipLaunchKernelGGL(rows_count_kernel, dim3(L.nseg_rows), dim3(64), 4 * gy, stream, p.P, L.nseg_rows, L.rowseg, gy,
+                       p.cull_pad, gs.order, (const uint4*)gs.foot, bs.rows_count, bs.qrec);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     uint32_t* sums = reinterpret_cast<uint32_t*>(bs.list_tmp);
     const size_t nrows = (size_t)gy * L.nseg_rows;
@@ -864,35 +833,29 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     if ((e = launch_scan_excl(bs.rows_count, bs.rows_off, nrows - 1, (uint32_t)(nrows - 1), nullptr, 1u, sums,
                               stream)) != hipSuccess)
         return e;
-    hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, gx, gy,
-                       p.cull_pad, gs.order, gs.splats, radii, bs.rows_off, bs.qrec, bs.rows);
+    hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, L.rowseg, gy,
+                       p.cull_pad, gs.order, (const uint4*)gs.foot, bs.rows_off, bs.qrec, bs.rows);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // tiles pass
     const uint32_t* last = bs.rows_count + (size_t)gy * L.nseg_rows - 1;
     hipLaunchKernelGGL(tiles_setup_kernel, dim3(1), dim3(1024), 0, stream, gy, L.nseg_rows, bs.rows_off, last,
                        bs.segbase);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(tiles_count_kernel, dim3(kTileBlocks), dim3(64), 4 * gx, stream, gx, gy, L.nseg_rows,
+    hipLaunchKernelGGL(tiles_count_kernel, dim3(kTileBlocks), dim3(64), 4 * gx + 8 * (gy + 1), stream, gx, gy, L.nseg_rows,
                        bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // counts of the live segments only: gx * segbase[gy] of them (tiles_count_kernel writes every one)
     if ((e = launch_scan_excl(bs.tiles_count, bs.tiles_off, (size_t)gx * L.nseg_tiles_max, 0u, bs.segbase + gy, gx,
                               sums, stream)) != hipSuccess)
         return e;
-    if (GSR_TILES_EMIT_SORTED == 3 && gx <= (uint32_t)kCoopMaxGx)
+    if (GSR_TILES_EMIT_SORTED == 3 && gx <= (uint32_t)kCoopMaxGx && coop_lds_bytes(gx, gy) <= 65536)
         hipLaunchKernelGGL((tiles_emit_coop_kernel<kCoopWaves, kCoopPlanes>), dim3(kCoopBlocks), dim3(64 * kCoopWaves),
-                           coop_lds_bytes(gx), stream, gx, gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows,
+                           coop_lds_bytes(gx, gy), stream, gx, gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows,
                            bs.tiles_off, bs.point_list);
-    else if (GSR_TILES_EMIT_SORTED >= 2)
+    else
         hipLaunchKernelGGL(tiles_emit_wide_kernel<kEmitPlanes>, dim3(kTileBlocks), dim3(64),
                            (8 * kEmitPlanes + 12) * gx + 6 * kEmitCapW, stream, gx,
                            gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
-    else if (GSR_TILES_EMIT_SORTED)
-        hipLaunchKernelGGL(tiles_emit_sorted_kernel, dim3(kTileBlocks), dim3(64), 20 * gx + 6 * kEmitCap, stream, gx,
-                           gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
-    else
-        hipLaunchKernelGGL(tiles_emit_kernel, dim3(kTileBlocks), dim3(64), 24 * gx, stream, gx, gy, L.nseg_rows,
-                           bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(list_ranges_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, stream, gx, gy, bs.segbase,
                        bs.tiles_off, ts.ranges);
