@@ -81,6 +81,9 @@ def parse():
                     help="N > 1: gradient exchange: gsr_dist.OverlappedViewGrads (inside the backward, range by "
                          "range), FactoredViewGrads (after it), or an all-reduce of every row")
     ap.add_argument("--chunks", type=int, default=4, help="--exchange overlap: Gaussian ranges per backward")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1: nccl (= RCCL over xGMI, the measured path); gloo only to rehearse the N > 1 "
+                         "protocol with several ranks on one GPU (RCCL refuses two ranks on one device)")
     ap.add_argument("--cpu-tile-stride", type=int, default=0, help="0 = auto")
     ap.add_argument("--stage-steps", type=int, default=5,
                     help="untimed steps with every stage bracketed by hipEvents (the per-stage table)")
@@ -218,10 +221,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # (a rehearsal with more ranks than GPUs shares the devices; device_count() does not initialise the GPU)
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     import gsr_scene as S
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer

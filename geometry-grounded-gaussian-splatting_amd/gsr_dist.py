@@ -26,6 +26,17 @@ import torch
 import torch.distributed as dist
 
 
+def _coalescing(group, tensors):
+    """torch's coalescing manager (one allreduce_coalesced for several
+    tensors) where the backend has it for these tensors: RCCL does; gloo
+    only for host tensors (gloo with device tensors is the one-GPU
+    rehearsal of the N > 1 path).  None: one all_reduce per tensor."""
+    cm_fn = getattr(dist, "_coalescing_manager", None)
+    if cm_fn is not None and dist.get_backend(group) == "gloo" and any(t.is_cuda for t in tensors):
+        return None
+    return cm_fn
+
+
 class ViewParallelGrads:
     def __init__(self, params: Iterable[torch.Tensor], bucket_mb: float = 256.0,
                  group: Optional[dist.ProcessGroup] = None, average: bool = False, inplace: bool = True):
@@ -67,6 +78,7 @@ class ViewParallelGrads:
 
     def all_reduce(self, async_op: bool = False):
         """Sum every parameter's .grad over the ranks of the group."""
+        cm_fn = _coalescing(self.group, self.params)
         self._work = []
         if self.inplace:
             grads = []
@@ -75,7 +87,6 @@ class ViewParallelGrads:
                     p.grad = torch.zeros_like(p)
                 if p.numel():
                     grads.append(p.grad)
-            cm_fn = getattr(dist, "_coalescing_manager", None)
             if cm_fn is None or len(grads) < 2:
                 for g in grads:
                     self._work.append((None, dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
@@ -353,7 +364,7 @@ class OverlappedViewGrads:
         rows += [dscales[b:e], drotations[b:e]] if self._scales else [dcov3D[b:e]]
         if not self._sh:
             rows.append(dcolors[b:e])
-        cm_fn = getattr(dist, "_coalescing_manager", None)
+        cm_fn = _coalescing(self.group, rows)
         if cm_fn is None:
             self._works += [dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True) for t in rows]
         else:

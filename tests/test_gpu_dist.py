@@ -245,3 +245,88 @@ def test_overlapped_exchange_one_rank_matches_plain_backward(tmp_path, sg_degree
         assert bool(torch.isfinite(got).all()), k
         err = float((got - want).norm() / want.norm().clamp_min(1e-30))
         assert err <= 1e-5, (k, err)
+
+
+# ---- two ranks through the real HIP backward (one GPU shared, gloo) ----
+def _two_rank_worker(rank, world, port, outdir, sg_degree):
+    import math
+    import socket  # noqa: F401  (spawned interpreter: nothing is imported yet)
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [root, os.path.join(root, "geometry-grounded-gaussian-splatting_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gsr_scene as S
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gsr_dist import FactoredViewGrads, OverlappedViewGrads
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    P, W, H = 20000, 320, 240
+    raw = S.make_gaussians(P, sg_degree=sg_degree, seed=7, aspect=H / W, z_range=(2.0, 6.0))
+    inp = {k: v.detach().contiguous().to(dev) for k, v in S.activated_inputs(raw).items()}
+    cam = S.orbit_cameras(2, W, H, center_z=4.0, max_deg=8.0)[rank].to(dev)
+    settings = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2),
+        kernel_size=0.0, bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam.world_view_transform,
+        projmatrix=cam.full_proj_transform, sh_degree=3, sg_degree=sg_degree, campos=cam.camera_center,
+        prefiltered=False, require_depth=True, debug=False)
+    g = {k: v.to(dev) for k, v in S.upstream_grads(H, W, seed=4 + rank).items()}
+
+    def step(ps=None):
+        ps = ps or {k: t.clone().requires_grad_(True) for k, t in inp.items()}
+        color, radii, mdepth, alpha, normal = GaussianRasterizer(settings)(
+            means3D=ps["means3D"], means2D=torch.zeros(P, 3, device=dev, requires_grad=True),
+            opacities=ps["opacities"], shs=ps["shs"], sg_axis=ps["sg_axis"], sg_sharpness=ps["sg_sharpness"],
+            sg_color=ps["sg_color"], scales=ps["scales"], rotations=ps["rotations"])
+        torch.autograd.backward([color, mdepth, normal], [g["color"], g["mdepth"], g["normal"]])
+        torch.cuda.synchronize()
+        return ps
+
+    plain = {k: t.grad.cpu() for k, t in step().items()}
+    with OverlappedViewGrads(chunks=3):
+        over = {k: t.grad.cpu() for k, t in step().items()}
+    ps = {k: t.clone().requires_grad_(True) for k, t in inp.items()}
+    ex = FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"], ps["sg_axis"],
+                           ps["sg_sharpness"], ps["sg_color"])  # (its guard counts the backwards from here)
+    step(ps)
+    ex.exchange(cam.camera_center, 3, sg_degree)
+    torch.cuda.synchronize()
+    fact = {k: t.grad.cpu() for k, t in ps.items()}
+    torch.save({"plain": plain, "over": over, "fact": fact}, os.path.join(outdir, f"g{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sg_degree", [0, 3])
+def test_two_ranks_exchange_sums_views_on_gpu(tmp_path, sg_degree):
+    """bench.py's N > 1 step with two ranks (two processes sharing cuda:0;
+    gloo, since RCCL refuses two ranks on one device): each rank renders its
+    own orbit view through the HIP forward and backward, and the overlapped
+    (inside the backward, range by range) and factored (after it) exchanges
+    give both ranks the same gradients, equal to the sum of the two views'
+    plain gradients (rel. L2 <= 1e-5: the geometry rows are sums in another
+    order, the colour rows are rebuilt from the gathered DC rows)."""
+    import socket
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_two_rank_worker, args=(2, port, str(tmp_path), sg_degree), nprocs=2, join=True,
+                       start_method="spawn")
+    r0 = torch.load(tmp_path / "g0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "g1.pt", weights_only=True)
+    for k, p0 in r0["plain"].items():
+        want = (p0.double() + r1["plain"][k].double())
+        if want.numel() == 0:
+            continue
+        for form in ("over", "fact"):
+            a, b = r0[form][k], r1[form][k]
+            assert torch.equal(a, b), (form, k)  # the replicas stay bit-identical
+            assert bool(torch.isfinite(a).all()), (form, k)
+            err = float((a.double() - want).norm() / want.norm().clamp_min(1e-30))
+            assert err <= 1e-5, (form, k, err)
