@@ -607,11 +607,24 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
         GSR_STAGE(GSR_STAGE_SORT, launch_sort(bs, (int)K_live, tile_bits, stream), "sort");
         GSR_STAGE(GSR_STAGE_TILE_RANGES, launch_tile_ranges(bs, (int)K_live, ts, tiles, stream), "tile ranges");
     }
-    // (heaviest-first order measured for the forward with the list length as
-    // the cost: -12 us of render_fwd for a 15 us ordering kernel; not used)
-    ts.order = nullptr;
-    GSR_STAGE(GSR_STAGE_RENDER_FWD,
-              launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream), "render");
+    // Heaviest tile first (LPT, cost = list length) when the grid fills the
+    // chip only a few times over: then the last round of long tiles sets the
+    // launch's length.  At C3 (8160 tiles, ~5 rounds of 6 blocks per CU) the
+    // order saved 8 us of render_fwd for a 12 us ordering launch, so larger
+    // grids keep the XCD-contiguous order.
+#ifndef GSR_FWD_LPT_MAX_TILES
+#define GSR_FWD_LPT_MAX_TILES 4096
+#endif
+    const bool lpt = tiles <= GSR_FWD_LPT_MAX_TILES;
+    if (!lpt) ts.order = nullptr;
+    // (one stage: the ordering launch is part of the forward raster's time)
+    GSR_STAGE(GSR_STAGE_RENDER_FWD, [&]() {
+        if (lpt) {
+            const hipError_t e = launch_tile_order((uint32_t)tiles, ts.ranges, nullptr, ts.order, stream);
+            if (e != hipSuccess) return e;
+        }
+        return launch_render_fwd(p, gs, bs, is, ts, out_color, out_alpha, out_normal, out_mdepth, stream);
+    }(), "render");
     if (num_rendered) *num_rendered = (int)K;
     return GSR_OK;
 }
