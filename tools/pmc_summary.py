@@ -35,14 +35,14 @@ def stage_of(name: str) -> str | None:
     if "tile_ranges_kernel" in n:
         return "tile_ranges"
     if any(k in n for k in ("rows_count_kernel", "rows_emit_kernel", "tiles_setup_kernel", "tiles_count_kernel",
-                            "tiles_emit_kernel", "tiles_emit_sorted_kernel", "tiles_emit_wide_kernel",
+                            "tiles_emit_kernel", "tiles_emit_sorted_kernel", "tiles_emit_wide_kernel", "tiles_emit_coop_kernel",
                             "list_ranges_kernel")):
         return "tile_lists"
-    if "render_fwd_kernel" in n:
+    if "render_fwd_kernel" in n or "tile_order_kernel" in n:  # (the forward's LPT order on small grids)
         return "render_fwd"
     if "render_bwd_kernel" in n:
         return "render_bwd"
-    if "tile_order_kernel" in n or "bwd_prepare_kernel" in n:
+    if "bwd_prepare_kernel" in n:
         return "bwd_clear"
     if "gather_counts_kernel" in n or "live_tiles_kernel" in n or "dsort_" in n:
         return "depth_order"
