@@ -1,11 +1,11 @@
 """Print one step's kernel timeline from a rocprofv3 kernel trace (development tool).
-python tools/ktrace_step.py TRACE_CSV [anchor_kernel_substring] [call index from the end, default -3]"""
+python tools/ktrace_step.py TRACE_CSV [anchor_kernel_substring] [call index from the end, default -8]"""
 import csv, re, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 anchor = sys.argv[2] if len(sys.argv) > 2 else "preprocess_fwd"
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
-k = int(sys.argv[3]) if len(sys.argv) > 3 else -3  # which call (from the end)
+k = int(sys.argv[3]) if len(sys.argv) > 3 else -8  # which call (from the end): -8 is inside bench.py's timed loop (the last two forwards are its K and K_live readouts)
 i0, i1 = idx[k], idx[k + 1]
 t0 = int(rows[i0]["Start_Timestamp"])
 prev = t0
