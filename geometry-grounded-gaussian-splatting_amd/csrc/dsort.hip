@@ -11,10 +11,11 @@
 // and one kernel per 8-bit digit, and the look-back state of all four passes
 // is zeroed once.
 //
-// Pass kernel (one 1024-lane workgroup per 4096-key tile — 16 waves per CU
+// Pass kernel (one 1024-lane workgroup per tile of 8192 keys, 12288 above 2M
+// keys — 16 waves per CU
 // for latency; tiles numbered in the order workgroups start, by an atomic
 // counter, so every look-back target is running or done):
-//  1. each wave ranks its 256 keys (4 per lane, position i*64 + lane) by
+//  1. each wave ranks its 512 / 768 keys (8 / 12 per lane, position i*64 + lane) by
 //     digit with 8 ballots per item (peer lanes), a per-wave digit counter in
 //     LDS giving the stable rank among the wave's earlier items;
 //  2. per digit (lanes 0-255): the wave counts combined into the tile's
@@ -29,14 +30,28 @@
 // Stability: within a digit, tile order, then wave, item and lane order,
 // which is position order; so the result is the (key, index) order of the
 // reference's stable sort.
+#include <type_traits>
+
 #include "gsr_kernels.h"
 
 namespace gsr {
 
-constexpr int kDsThreads = 1024;
+#ifndef GSR_DS_THREADS
+#define GSR_DS_THREADS 1024
+#endif
+#ifndef GSR_DS_ITEMS
+#define GSR_DS_ITEMS 8  // keys per lane up to kDsBigP keys (round 3; was 4: C5 depth order 0.294 -> 0.222 ms)
+#endif
+#ifndef GSR_DS_ITEMS_BIG
+#define GSR_DS_ITEMS_BIG 12  // above kDsBigP (C5: 0.221 -> 0.188 ms; 12 at C3: 0.080 -> 0.088, 16: 0.207 / 0.098)
+#endif
+constexpr int kDsThreads = GSR_DS_THREADS;
 constexpr int kDsWaves = kDsThreads / 64;
-constexpr int kDsItems = 4;
-constexpr int kDsTile = kDsThreads * kDsItems;  // 4096 keys
+constexpr int kDsItems = GSR_DS_ITEMS, kDsItemsBig = GSR_DS_ITEMS_BIG;
+constexpr int kDsBigP = 2000000;
+// keys per lane for P keys: fewer, larger tiles for large P (fewer look-back steps; one block per CU)
+static int dsort_items(int P) { return P > kDsBigP ? kDsItemsBig : kDsItems; }
+static_assert(kDsThreads >= 256 && kDsThreads % 64 == 0, "a digit per lane of the first 256 lanes");
 constexpr int kDsLook = 32;                     // status words read per look-back round
 constexpr uint32_t kDsAgg = 1u << 30, kDsInc = 2u << 30, kDsVal = (1u << 30) - 1u;
 
@@ -49,7 +64,10 @@ struct DsortState {
     int tiles;
 };
 
-static int dsort_tiles(int P) { return (P + kDsTile - 1) / kDsTile; }
+static int dsort_tiles(int P) {
+    const int tile = kDsThreads * dsort_items(P);
+    return (P + tile - 1) / tile;
+}
 
 static DsortState carve_dsort(void* base, int P) {
     Carver c(base);
@@ -146,7 +164,10 @@ __global__ void __launch_bounds__(256) count_k_hist_kernel(int P, const uint32_t
 hipError_t launch_count_k_hist(const GeomState& gs, int P, bool hist, hipStream_t stream) {
     if (P == 0) return hipMemsetAsync(gs.offsets_K, 0, sizeof(uint32_t), stream);
     DsortState s = carve_dsort(gs.dsort_tmp, P);
-    hipLaunchKernelGGL(count_k_hist_kernel, dim3(min(256, (P + 4095) / 4096)), dim3(256), 0, stream, P,
+#ifndef GSR_KHIST_BLOCKS
+#define GSR_KHIST_BLOCKS 512  // round 3: 256 -> 512 blocks, C5 count + histograms 47 -> 36 us (1024: 39)
+#endif
+    hipLaunchKernelGGL(count_k_hist_kernel, dim3(min(GSR_KHIST_BLOCKS, (P + 4095) / 4096)), dim3(256), 0, stream, P,
                        gs.tiles_touched, reinterpret_cast<const uint32_t*>(gs.depths), gs.offsets_K, hist ? 1 : 0, s);
     return hipGetLastError();
 }
@@ -176,17 +197,18 @@ __device__ __forceinline__ uint32_t ds_digit_excl(uint32_t v, uint32_t* s_w) {
     return before + x - v;
 }
 
-template <int PASS>
+template <int PASS, int ITEMS>
 __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* __restrict__ keys_in,
                                                                 const uint32_t* __restrict__ vals_in, int P,
                                                                 DsortState s, uint32_t* __restrict__ keys_out,
                                                                 uint32_t* __restrict__ vals_out) {
     constexpr int kShift = 8 * PASS;
+    constexpr int kItems = ITEMS, kTile = kDsThreads * ITEMS;
     __shared__ uint32_t s_wcnt[kDsWaves][256];  // per-wave digit counters, then the waves' exclusive offsets
     __shared__ uint32_t s_goff[256];     // digit start in the output: global prefix + preceding tiles
     __shared__ uint32_t s_pre[256];      // in-tile exclusive digit prefix
     __shared__ uint32_t s_cnt[256], s_excl[256];  // the tile's digit counts; the preceding tiles' sums
-    __shared__ uint32_t s_keys[kDsTile], s_vals[kDsTile];
+    __shared__ uint32_t s_keys[kTile], s_vals[kTile];
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_tile;
 
@@ -195,11 +217,11 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
     for (int i = tid; i < kDsWaves * 256; i += kDsThreads) (&s_wcnt[0][0])[i] = 0u;
     __syncthreads();
     const int tile = (int)s_tile;
-    const int base = tile * kDsTile + wave * (kDsTile / kDsWaves);
+    const int base = tile * kTile + wave * (kTile / kDsWaves);
 
-    uint32_t k[kDsItems], v[kDsItems], r[kDsItems];
+    uint32_t k[kItems], v[kItems], r[kItems];
 #pragma unroll
-    for (int i = 0; i < kDsItems; i++) {
+    for (int i = 0; i < kItems; i++) {
         const int p = base + i * 64 + lane;
         const bool ok = p < P;
         k[i] = ok ? keys_in[p] : 0xffffffffu;  // padding: digit 255, after every real key of the tile
@@ -208,7 +230,7 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
     // 1. stable rank of each item among the wave's keys of its digit
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int i = 0; i < kDsItems; i++) {
+    for (int i = 0; i < kItems; i++) {
         const uint32_t d = (k[i] >> kShift) & 255u;
         uint64_t peers = ~0ull;
 #pragma unroll
@@ -233,7 +255,7 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
             s_wcnt[w][d] = cnt;  // wave's exclusive offset within the digit
             cnt += c;
         }
-        if (tile == s.tiles - 1 && d == 255) cnt -= (uint32_t)(s.tiles * kDsTile - P);  // not the padding keys
+        if (tile == s.tiles - 1 && d == 255) cnt -= (uint32_t)(s.tiles * kTile - P);  // not the padding keys
         ds_store(st + (size_t)tile * 256, (tile == 0 ? kDsInc : kDsAgg) | cnt);
     }
     // (digit 255's count, with or without the padding, enters no prefix)
@@ -242,7 +264,7 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
     __syncthreads();
     // 3. keys and values to LDS in tile-sorted order (while the preceding tiles publish)
 #pragma unroll
-    for (int i = 0; i < kDsItems; i++) {
+    for (int i = 0; i < kItems; i++) {
         const uint32_t dd = (k[i] >> kShift) & 255u;
         const uint32_t rank = s_pre[dd] + s_wcnt[wave][dd] + r[i];
         s_keys[rank] = k[i];
@@ -254,8 +276,8 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
     //    not-ready word
     if (dl) s_cnt[d] = cnt;
     __syncthreads();
-    {
-        const int dq = tid >> 2, part = tid & 3, quad = lane & ~3;
+    for (int dq0 = 0; dq0 < 256; dq0 += kDsThreads / 4) {  // (one round with 1024 lanes)
+        const int dq = dq0 + (tid >> 2), part = tid & 3, quad = lane & ~3;
         const uint32_t* sq = s.status + ((size_t)PASS * s.tiles) * 256 + dq;
         uint32_t excl = 0;
         int j = tile - 1;
@@ -303,9 +325,9 @@ __global__ void __launch_bounds__(kDsThreads) dsort_pass_kernel(const uint32_t* 
     const uint32_t gpre = ds_digit_excl(dl ? s.hist[PASS * 256 + d] : 0u, s_w);
     if (dl) s_goff[d] = gpre + s_excl[d];
     __syncthreads();
-    const int nvalid = min(kDsTile, P - tile * kDsTile);
+    const int nvalid = min(kTile, P - tile * kTile);
 #pragma unroll
-    for (int i = 0; i < kDsItems; i++) {
+    for (int i = 0; i < kItems; i++) {
         const int rank = i * kDsThreads + tid;
         if (rank < nvalid) {
             const uint32_t key = s_keys[rank];
@@ -327,13 +349,19 @@ hipError_t launch_dsort(const GeomState& gs, int P, bool prepared, hipStream_t s
         hipLaunchKernelGGL(dsort_hist_kernel, dim3(min(256, (P + 4095) / 4096)), dim3(256), 0, stream, keys, P, s);
     }
     const dim3 grid(s.tiles), block(kDsThreads);
-    hipLaunchKernelGGL(dsort_pass_kernel<0>, grid, block, 0, stream, keys, nullptr, P, s, s.keys_alt, s.vals_alt);
-    hipLaunchKernelGGL(dsort_pass_kernel<1>, grid, block, 0, stream, s.keys_alt, s.vals_alt, P, s,
-                       gs.depth_keys_sorted, gs.order);
-    hipLaunchKernelGGL(dsort_pass_kernel<2>, grid, block, 0, stream, gs.depth_keys_sorted, gs.order, P, s,
-                       s.keys_alt, s.vals_alt);
-    hipLaunchKernelGGL(dsort_pass_kernel<3>, grid, block, 0, stream, s.keys_alt, s.vals_alt, P, s,
-                       gs.depth_keys_sorted, gs.order);
+    auto passes = [&](auto items_c) {
+        constexpr int I = decltype(items_c)::value;
+        hipLaunchKernelGGL((dsort_pass_kernel<0, I>), grid, block, 0, stream, keys, nullptr, P, s, s.keys_alt,
+                           s.vals_alt);
+        hipLaunchKernelGGL((dsort_pass_kernel<1, I>), grid, block, 0, stream, s.keys_alt, s.vals_alt, P, s,
+                           gs.depth_keys_sorted, gs.order);
+        hipLaunchKernelGGL((dsort_pass_kernel<2, I>), grid, block, 0, stream, gs.depth_keys_sorted, gs.order, P, s,
+                           s.keys_alt, s.vals_alt);
+        hipLaunchKernelGGL((dsort_pass_kernel<3, I>), grid, block, 0, stream, s.keys_alt, s.vals_alt, P, s,
+                           gs.depth_keys_sorted, gs.order);
+    };
+    if (dsort_items(P) == kDsItems) passes(std::integral_constant<int, kDsItems>{});
+    else passes(std::integral_constant<int, kDsItemsBig>{});
     return hipGetLastError();
 }
 

@@ -70,7 +70,10 @@ __device__ __forceinline__ void cull_foot(const PreprocessArgs& a, int idx) {
 // inputs, before the culling branches (one memory round trip instead of
 // three); the plain instance loads them where they are used.
 template <bool HOIST>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) preprocess_fwd_kernel(PreprocessArgs a) {
+#ifndef GSR_PRE_WAVES
+#define GSR_PRE_WAVES 1
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_PRE_WAVES, 8))) preprocess_fwd_kernel(PreprocessArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     for (size_t i = (size_t)idx; i < a.zero_words; i += (size_t)gridDim.x * blockDim.x) a.zero_first[i] = 0u;
     if (idx == 0) *a.zero_K = 0u;
