@@ -248,3 +248,23 @@ def test_overlapped_exchange_sums_views(tmp_path):
         want = (g0[name].grad + g1[name].grad).float()
         assert torch.equal(o0[name], o1[name]), name
         torch.testing.assert_close(o0[name], want, rtol=1e-5, atol=1e-7)
+
+
+def test_coalescing_choice_by_backend_and_device(tmp_path):
+    """gsr_dist._coalescing: the coalesced all-reduce where the backend has it
+    for the tensors (gloo on host tensors; RCCL always), one all-reduce per
+    tensor for gloo with device tensors (the one-GPU rehearsal of the N > 1
+    path: gloo has no allreduce_coalesced for them)."""
+    sys.path[:0] = [os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd")]
+    from gsr_dist import _coalescing
+
+    class Dev:  # a stand-in device tensor: only .is_cuda is read
+        is_cuda = True
+
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("gloo", store=store, rank=0, world_size=1)
+    try:
+        assert _coalescing(None, [torch.zeros(3), torch.zeros(2)]) is getattr(dist, "_coalescing_manager", None)
+        assert _coalescing(None, [torch.zeros(3), Dev()]) is None
+    finally:
+        dist.destroy_process_group()
