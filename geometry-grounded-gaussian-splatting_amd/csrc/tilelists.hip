@@ -392,31 +392,6 @@ __device__ __forceinline__ uint32_t row_begin(const uint32_t* O_rows, int nseg_r
     return y < gy ? O_rows[(size_t)y * nseg_rows] : total;
 }
 
-__global__ void __launch_bounds__(1024)
-    tiles_setup_kernel(uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
-                       const uint32_t* __restrict__ M_rows_last, uint32_t* __restrict__ segbase) {
-    __shared__ uint32_t s[kMaxGrid];
-    const uint32_t y = threadIdx.x;
-    // total row entries = last exclusive offset + last count
-    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
-    uint32_t nk = 0;
-    if (y < gy) {
-        const uint32_t len = row_begin(O_rows, nseg_rows, y + 1, gy, total) - row_begin(O_rows, nseg_rows, y, gy, total);
-        nk = (len + kTileSeg - 1) / kTileSeg;
-    }
-    s[y] = nk;
-    __syncthreads();
-    // inclusive Hillis-Steele scan over <= 1024 rows
-    for (uint32_t o = 1; o < blockDim.x; o <<= 1) {
-        const uint32_t v = y >= o ? s[y - o] : 0u;
-        __syncthreads();
-        s[y] += v;
-        __syncthreads();
-    }
-    if (y < gy) segbase[y + 1] = s[y];
-    if (y == 0) segbase[0] = 0u;
-}
-
 struct TileSeg {
     bool on;
     uint32_t y, k, nk, e0, e1;
@@ -454,6 +429,32 @@ __device__ __forceinline__ void stage_seg_table(uint32_t gy, int nseg_rows, cons
     }
     __syncthreads();
 }
+// The segment table built from the rows pass's scan by one wave (the work a
+// separate one-workgroup launch did before): every row's first entry, its
+// segment count ceil(len / kTileSeg), their exclusive scan in s_sb; `out`
+// (one block) gets segbase for the kernels after.  One 64-lane block.
+__device__ __forceinline__ void build_seg_table(uint32_t gy, int nseg_rows, const uint32_t* O_rows,
+                                                const uint32_t* M_rows_last, uint32_t* s_sb, uint32_t* s_rb,
+                                                uint32_t* out) {
+    const uint32_t lane = threadIdx.x;
+    // total row entries = last exclusive offset + last count
+    const uint32_t total = O_rows[(size_t)gy * nseg_rows - 1] + M_rows_last[0];
+    for (uint32_t y = lane; y <= gy; y += 64) s_rb[y] = row_begin(O_rows, nseg_rows, y, gy, total);
+    __syncthreads();
+    uint32_t carry = 0;
+    for (uint32_t y0 = 0; y0 < gy; y0 += 64) {
+        const uint32_t y = y0 + lane;
+        const uint32_t nk = y < gy ? (s_rb[y + 1] - s_rb[y] + kTileSeg - 1) / kTileSeg : 0u;
+        const uint32_t incl = wave_incl_scan(nk);
+        if (y < gy) s_sb[y + 1] = carry + incl;
+        carry += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) s_sb[0] = 0u;
+    __syncthreads();
+    if (out)
+        for (uint32_t y = lane; y <= gy; y += 64) out[y] = s_sb[y];
+}
+
 __device__ __forceinline__ TileSeg find_seg_lds(uint32_t b, uint32_t gy, const uint32_t* s_sb, const uint32_t* s_rb) {
     TileSeg S{};
     if (b >= s_sb[gy]) return S;
@@ -494,14 +495,15 @@ __device__ __forceinline__ void for_xcd_segments(uint32_t n, F&& f) {
 
 __global__ void __launch_bounds__(64)
     tiles_count_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
-                       const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
+                       const uint32_t* __restrict__ M_rows_last, uint32_t* __restrict__ segbase,
                        const uint2* __restrict__ rows, uint32_t* __restrict__ M) {
+    // (segbase: written here by block 0 for the kernels after; every block builds its own copy in LDS)
     extern __shared__ unsigned long long s_dyn[];  // [gx] counts, then the segment table (2 x [gy + 1])
     uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
     uint32_t* s_sb = s_cnt + gx;
     uint32_t* s_rb = s_sb + gy + 1;
     const int lane = threadIdx.x;
-    stage_seg_table(gy, nseg_rows, O_rows, M_rows_last, segbase, s_sb, s_rb);
+    build_seg_table(gy, nseg_rows, O_rows, M_rows_last, s_sb, s_rb, blockIdx.x == 0 ? segbase : nullptr);
     for_xcd_segments(s_sb[gy], [&](uint32_t l) {
         const TileSeg S = find_seg_lds(l, gy, s_sb, s_rb);
         __syncthreads();  // previous segment's counts read out
@@ -702,7 +704,7 @@ __global__ void __launch_bounds__(64 * NW)
     tiles_emit_coop_kernel(uint32_t gx, uint32_t gy, int nseg_rows, const uint32_t* __restrict__ O_rows,
                            const uint32_t* __restrict__ M_rows_last, const uint32_t* __restrict__ segbase,
                            const uint2* __restrict__ rows, const uint32_t* __restrict__ O,
-                           uint32_t* __restrict__ point_list) {
+                           uint32_t* __restrict__ point_list, uint2* __restrict__ ranges) {
     constexpr int kPl = NW * NPL;
     constexpr int kThreads = 64 * NW;
     // LDS: 2 x kPl x [gx] masks; [gx] running slots, chunk offsets, write bases; kPl x [gx] plane prefixes;
@@ -723,6 +725,19 @@ __global__ void __launch_bounds__(64 * NW)
     for (uint32_t x = tid; x < 2 * kPl * gx; x += kThreads) s_cov2[x] = 0ull;
     stage_seg_table(gy, nseg_rows, O_rows, M_rows_last, segbase, s_sb, s_rb);  // (ends with a barrier)
     const uint32_t n = s_sb[gy];
+    // the tile ranges (list_ranges_kernel's work) depend only on the scan this kernel starts from: every
+    // block writes a share of them first, so they need no launch of their own
+    for (uint32_t t = blockIdx.x * kThreads + tid; t < gx * gy; t += gridDim.x * kThreads) {
+        const uint32_t y = t / gx, x = t - y * gx;
+        const uint32_t nk = s_sb[y + 1] - s_sb[y];
+        uint2 r = make_uint2(0u, 0u);
+        if (nk) {
+            const size_t base = (size_t)gx * s_sb[y];
+            const uint32_t b = O[base + (size_t)x * nk], e = O[base + (size_t)(x + 1) * nk];
+            if (e > b) r = make_uint2(b, e);  // empty tiles stay (0, 0) as in the reference
+        }
+        ranges[t] = r;
+    }
     const uint32_t xcd = blockIdx.x % 8u, slot0 = blockIdx.x / 8u, nslots = gridDim.x / 8u;
     const uint32_t lo_l = (uint32_t)(((unsigned long long)n * xcd) / 8u);
     const uint32_t hi_l = (uint32_t)(((unsigned long long)n * (xcd + 1u)) / 8u);
@@ -838,9 +853,6 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // tiles pass
     const uint32_t* last = bs.rows_count + (size_t)gy * L.nseg_rows - 1;
-    hipLaunchKernelGGL(tiles_setup_kernel, dim3(1), dim3(1024), 0, stream, gy, L.nseg_rows, bs.rows_off, last,
-                       bs.segbase);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(tiles_count_kernel, dim3(kTileBlocks), dim3(64), 4 * gx + 8 * (gy + 1), stream, gx, gy, L.nseg_rows,
                        bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -848,17 +860,19 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     if ((e = launch_scan_excl(bs.tiles_count, bs.tiles_off, (size_t)gx * L.nseg_tiles_max, 0u, bs.segbase + gy, gx,
                               sums, stream)) != hipSuccess)
         return e;
-    if (GSR_TILES_EMIT_SORTED == 3 && gx <= (uint32_t)kCoopMaxGx && coop_lds_bytes(gx, gy) <= 65536)
+    if (GSR_TILES_EMIT_SORTED == 3 && gx <= (uint32_t)kCoopMaxGx && coop_lds_bytes(gx, gy) <= 65536) {
+        // (the coop kernel writes the tile ranges too)
         hipLaunchKernelGGL((tiles_emit_coop_kernel<kCoopWaves, kCoopPlanes>), dim3(kCoopBlocks), dim3(64 * kCoopWaves),
                            coop_lds_bytes(gx, gy), stream, gx, gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows,
-                           bs.tiles_off, bs.point_list);
-    else
+                           bs.tiles_off, bs.point_list, ts.ranges);
+    } else {
         hipLaunchKernelGGL(tiles_emit_wide_kernel<kEmitPlanes>, dim3(kTileBlocks), dim3(64),
                            (8 * kEmitPlanes + 12) * gx + 6 * kEmitCapW, stream, gx,
                            gy, L.nseg_rows, bs.rows_off, last, bs.segbase, bs.rows, bs.tiles_off, bs.point_list);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(list_ranges_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, stream, gx, gy, bs.segbase,
-                       bs.tiles_off, ts.ranges);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(list_ranges_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, stream, gx, gy, bs.segbase,
+                           bs.tiles_off, ts.ranges);
+    }
     (void)K;
     return hipGetLastError();
 }
