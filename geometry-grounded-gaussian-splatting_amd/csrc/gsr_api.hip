@@ -78,16 +78,26 @@ class ReadbackPool {
 };
 ReadbackPool g_readback_pool;
 
-// a slot leased for one forward's readback, returned on every exit path
+// a slot leased for one forward's readback, returned on every exit path.  Copies into the
+// slot are queued on `stream` (arm() before the first); the slot's event is recorded after
+// the last one (recorded()).  An exit between the two has no event covering the copies, so
+// the stream is drained instead; a slot whose copies cannot be proven finished is never
+// returned to the pool (another forward could otherwise lease it while a late copy lands).
 struct ReadbackLease {
     HostReadback* rb = nullptr;
+    hipStream_t stream = nullptr;
+    bool armed = false, has_event = false;
     ReadbackLease() = default;
     ReadbackLease(const ReadbackLease&) = delete;
     ReadbackLease& operator=(const ReadbackLease&) = delete;
+    void arm(hipStream_t s) { stream = s; armed = true; }
+    void recorded() { has_event = true; }
     ~ReadbackLease() {
         if (!rb) return;
-        (void)hipEventSynchronize(rb->ev);  // an error path may leave the copy in flight: drain it first
-        g_readback_pool.release(rb);
+        hipError_t e = hipSuccess;
+        if (has_event) e = hipEventSynchronize(rb->ev);
+        else if (armed) e = hipStreamSynchronize(stream);
+        if (e == hipSuccess) g_readback_pool.release(rb);  // (else the slot is leaked, not reused)
     }
 };
 
@@ -443,7 +453,13 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 14; }
+int gsr_abi_version(void) { return 15; }
+
+int gsr_backward_chunk_size(int P, int chunks) {
+    if (P < 0 || chunks < 1) return -1;
+    const long long per = ((long long)P + chunks - 1) / chunks;
+    return (int)((per + 255) / 256 * 256);
+}
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_tmu);
@@ -565,11 +581,13 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
         GSR_TRY(g_readback_pool.acquire(lease.rb), "pinned readback buffer");
         HostReadback* rb = lease.rb;
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_k_hist(gs, P, path == kBinLists, stream), "count K");
+        lease.arm(stream);
         GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
         if (prefiltered)
             GSR_TRY(hipMemcpyAsync(rb->pinned + 1, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
                     "memcpy prefiltered flag");
         GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
+        lease.recorded();
         // the GPU counts the tile lists (or sorts by depth) while the host waits
         if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, true, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");
@@ -736,8 +754,9 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
     // the per-Gaussian backward over `chunks` consecutive Gaussian ranges; after each range's launch
     // the host callback may post work on other streams that waits for it (gsr_dist.OverlappedViewGrads:
     // the range's gradient exchange runs while the next range computes)
-    // (ranges of whole 256-Gaussian workgroups; gsr_dist.OverlappedViewGrads.chunk_size mirrors this)
-    const int cs = ((P + chunks - 1) / chunks + 255) / 256 * 256;
+    // (ranges of whole 256-Gaussian workgroups; gsr_dist.OverlappedViewGrads reads the size from
+    // gsr_backward_chunk_size and checks the ranges it is called with against it)
+    const int cs = gsr_backward_chunk_size(P, chunks);
     for (int b0 = 0; b0 < P; b0 += cs) {
         const int b1 = min(P, b0 + cs);
         GSR_STAGE(GSR_STAGE_PREPROCESS_BWD, launch_preprocess_bwd(b, gs, ws, stream, b0, b1, dc_rows),
@@ -850,6 +869,7 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
         GSR_STAGE(GSR_STAGE_SCAN, launch_count_k_hist(gs, P, path == kBinLists, stream), "count K");
         GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_points(p, PN, points3D, ps, pb, st, stream), "sample points");
         GSR_STAGE(GSR_STAGE_SAMPLE_POINTS, launch_sample_setup(PN, tiles, pb, st, stream), "sample setup");
+        lease.arm(stream);
         GSR_TRY(hipMemcpyAsync(rb->pinned, gs.offsets_K, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "memcpy K");
         GSR_TRY(hipMemcpyAsync(rb->pinned + 4, st.totals, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
                 "memcpy totals");
@@ -857,6 +877,7 @@ static int point_query_forward(int query, gsr_alloc_fn geom_alloc, void* geom_ct
             GSR_TRY(hipMemcpyAsync(rb->pinned + 1, gs.near_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream),
                     "memcpy prefiltered flag");
         GSR_TRY(hipEventRecord(rb->ev, stream), "event record");
+        lease.recorded();
         // the GPU counts the tile lists (or sorts by depth) while the host waits
         if (path == kBinLists) GSR_STAGE(GSR_STAGE_DEPTH_ORDER, launch_depth_sort(gs, P, true, stream), "depth order");
         GSR_TRY(hipEventSynchronize(rb->ev), "event sync");

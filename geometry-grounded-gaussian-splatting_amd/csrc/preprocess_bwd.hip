@@ -211,10 +211,10 @@ __device__ __forceinline__ void wave_store_rows(float* __restrict__ g, const flo
 #define GSR_PBWD_STAGE_DEFAULT 1  // staged row stores: C5 preprocess_bwd 1.18-1.22 -> 0.91-0.93 ms, C3 0.151 -> 0.122
 #endif
 // STAGE (SH rows of 16 coefficients, launch ranges in whole workgroups): the
-// SH and SG-7 gradient rows go out through LDS as whole-wave stores.  Every
-// lane of a wave then takes part in the stores, so a lane past the range
-// computes Gaussian `begin` again (same values to the same addresses) and
-// only its staged rows are left out.
+// SH and SG-7 gradient rows go out through LDS as whole-wave stores (and the
+// SG-7 input rows come in by 16-B LDS-DMA).  Every lane of a wave then takes
+// part, so a lane past the range computes the wave's first Gaussian (`wbase`)
+// again (same values to the same addresses) and only its staged rows are left out.
 template <bool STAGE>
 #if GSR_PBWD_WAVES
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_PBWD_WAVES, 8)))
@@ -812,12 +812,15 @@ hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const 
     a.end = end;
     a.dc_rows = dc_rows;
     // staged row stores: the 16-coefficient SH layout, 16-B aligned rows, SG degree 0 or 7 (the
-    // configurations with wide rows), whole-workgroup ranges; GSR_OPT_PBWD_STAGE 1 forces it, 2 turns it off
+    // configurations with wide rows), whole-workgroup ranges; GSR_OPT_PBWD_STAGE 1 forces it, 2 turns it off.
+    // Alignment of every row base the stage touches: the gradient rows it stores and, at SG 7, the lobe
+    // input rows it loads by 16-B LDS-DMA (a tensor that is a view at a 4-B offset takes the per-lane path)
     const int so = option(kOptPbwdStage);
     auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     const bool stage_ok = p.shs && !dc_rows && p.SHM == 16 && (begin & 255) == 0 && al16(b.dL_dsh) &&
                           (p.SGM == 0 || (p.SGM == kSG7 && p.SGD == kSG7 && al16(b.dL_dsg_color) &&
-                                          al16(b.dL_dsg_sharpness) && al16(b.dL_dsg_axis)));
+                                          al16(b.dL_dsg_sharpness) && al16(b.dL_dsg_axis) &&
+                                          al16(p.sg_color) && al16(p.sg_sharpness) && al16(p.sg_axis)));
     const bool stage = stage_ok && (so == 1 || (so == 0 && GSR_PBWD_STAGE_DEFAULT));
     if (stage)
         hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((end - begin + 255) / 256), dim3(256), 0, stream, a);

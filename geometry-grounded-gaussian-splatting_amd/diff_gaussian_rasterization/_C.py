@@ -44,7 +44,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 
 def _load():
@@ -93,6 +93,8 @@ def _load():
     L.gsr_view_color_grads.argtypes = [i] * 6 + [vp] * 10
     L.gsr_view_color_grads_chunked.restype = i
     L.gsr_view_color_grads_chunked.argtypes = [i] * 7 + [vp] * 11
+    L.gsr_backward_chunk_size.restype = i
+    L.gsr_backward_chunk_size.argtypes = [i, i]
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     L.gsr_set_option.argtypes = [i, i]
@@ -129,6 +131,15 @@ OPT_NO_REFINE = 5
 OPT_BWD_NO_CACHE = 6
 OPT_ROCPRIM_DSORT = 9
 OPT_PBWD_STAGE = 10
+
+
+def backward_chunk_size(P: int, chunks: int) -> int:
+    """The Gaussian range size of a backward run in `chunks` ranges
+    (gsr_backward_chunk_size; host only, no GPU needed)."""
+    n = _load().gsr_backward_chunk_size(int(P), int(chunks))
+    if n < 0:
+        raise RuntimeError(f"gsr: backward_chunk_size({P}, {chunks}): P must be >= 0 and chunks >= 1")
+    return n
 
 
 def debug_render_stats(reset: bool = True) -> list:
@@ -363,20 +374,13 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
         scratch = _ByteBuffer(dev)
         grads = (outs["dmeans2D"], outs["dcolors"], outs["dopacity"], outs["dmeans3D"], outs["dcov3D"], outs["dsh"],
                  outs["dsg_axis"], outs["dsg_sharpness"], outs["dsg_color"], outs["dscales"], outs["drotations"])
-        chunks, dc, errors = 1, None, []
+        chunks, dc = 1, None
         hook = _CHUNK()  # NULL
         if exchange is not None:
             chunks = max(1, int(exchange.chunks))
             dc = exchange.dc_rows(P, dev) if SHM else None
-
-            def on_chunk(_ctx, b, e):
-                try:
-                    if not errors:
-                        exchange.on_chunk(b, e, grads)
-                except BaseException as ex:  # noqa: BLE001 - re-raised after the C call returns
-                    errors.append(ex)
-
-            hook = _CHUNK(on_chunk)
+            cb = exchange.hook(grads)  # (errors held by the exchange, raised by settle below)
+            hook = _CHUNK(lambda _ctx, b, e: cb(b, e))
         with torch.cuda.device(dev):
             rc = L.gsr_rasterize_backward_ex(
                 scratch.cb, None, P, int(sh_degree), SHM, int(sg_degree), SGM, int(R), _ptr(a["background"]), W, H,
@@ -391,9 +395,9 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
                 _ptr(outs["dcov3D"]), _ptr(outs["dsh"]), _ptr(outs["dsg_axis"]), _ptr(outs["dsg_sharpness"]),
                 _ptr(outs["dsg_color"]), int(bool(require_depth)), int(bool(debug)), chunks, hook, None,
                 None if dc is None else _ptr(dc), _stream(dev))
+        if exchange is not None:  # a failed backward still posts every range's collectives (no peer blocks)
+            exchange.settle(rc == 0)
         _check(rc)
-        if errors:
-            raise errors[0]
         if KEEP_BWD_SCRATCH:
             global last_bwd_scratch
             last_bwd_scratch = scratch.tensor

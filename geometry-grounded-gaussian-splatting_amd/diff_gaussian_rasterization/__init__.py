@@ -101,16 +101,21 @@ class _RasterizeGaussians(torch.autograd.Function):
         if ex is not None:  # gsr_dist.OverlappedViewGrads: the exchange rides on the backward's Gaussian ranges
             ex.begin(s.campos, means3D.shape[0], scales.numel() > 0, sh.numel() > 0)
             kw["exchange"] = ex
-        if s.debug:
-            cpu_args = cpu_deep_copy_tuple(args)
-            try:
+        try:
+            if s.debug:
+                cpu_args = cpu_deep_copy_tuple(args)
+                try:
+                    g = _C.rasterize_gaussians_backward(*args, **kw)
+                except Exception as ex_:
+                    torch.save(cpu_args, "snapshot_bw.dump")
+                    print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
+                    raise ex_
+            else:
                 g = _C.rasterize_gaussians_backward(*args, **kw)
-            except Exception as ex_:
-                torch.save(cpu_args, "snapshot_bw.dump")
-                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
-                raise ex_
-        else:
-            g = _C.rasterize_gaussians_backward(*args, **kw)
+        except BaseException:
+            if ex is not None:  # the exchange's remaining collectives are posted, its works settled
+                ex.abort()
+            raise
         if ex is not None:
             ex.finish(g, means3D, sg_axis, sg_sharpness, sg_color, s.sh_degree, s.sg_degree)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,

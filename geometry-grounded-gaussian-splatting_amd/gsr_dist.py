@@ -314,7 +314,10 @@ class OverlappedViewGrads:
         self._campos_local = self._campos_all = None
         self._works = []
         self._scales = self._sh = True
-        self._P = 0
+        self._P = self._cs = self._next = 0
+        self._ar_done = False  # the current range's all-reduce is posted, its all-gather not yet
+        self._active = False
+        self._error = None
 
     # ---- installation -------------------------------------------------
     def install(self) -> "OverlappedViewGrads":
@@ -343,41 +346,120 @@ class OverlappedViewGrads:
         return self._dc
 
     def chunk_size(self, P: int) -> int:
-        return ((P + self.chunks - 1) // self.chunks + 255) // 256 * 256  # as gsr_rasterize_backward_ex
+        """The backward's Gaussian range size, from the library that runs it
+        (gsr_backward_chunk_size): the gathered DC rows are laid out by it."""
+        from diff_gaussian_rasterization import _C
+        return _C.backward_chunk_size(P, self.chunks)
 
     def begin(self, campos: torch.Tensor, P: int, scales_path: bool, sh_path: bool) -> None:
+        if self._active:  # a backward that neither finished nor failed cleanly: settle its collectives first
+            self.abort()
         self._works = []
         self._P, self._scales, self._sh = P, scales_path, sh_path
+        self._cs = self.chunk_size(P) if P else 1
+        self._next, self._ar_done, self._error = 0, False, None
         dev = campos.device
         if self._campos_local is None or self._campos_local.device != dev:
             self._campos_local = torch.zeros(4, dtype=torch.float32, device=dev)
             self._campos_all = torch.empty(4 * self.world, dtype=torch.float32, device=dev)
         self._campos_local[:3].copy_(campos.reshape(3))
+        self._active = True
         if sh_path:
             self._works.append(dist.all_gather_into_tensor(self._campos_all, self._campos_local, group=self.group,
                                                            async_op=True))
 
+    def _post(self, b: int, e: int, rows, dc_in) -> None:
+        """One range's collectives, in the order every rank posts them."""
+        if not self._ar_done:
+            cm_fn = _coalescing(self.group, rows)
+            if cm_fn is None:
+                self._works += [dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                                for t in rows]
+            else:
+                with cm_fn(group=self.group, async_ops=True) as cm:
+                    for t in rows:
+                        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+                self._works.append(cm)
+            self._ar_done = True
+        if self._sh:
+            W = self.world
+            self._works.append(dist.all_gather_into_tensor(self._gathered[3 * W * b:3 * W * e], dc_in,
+                                                           group=self.group, async_op=True))
+        self._ar_done = False
+        self._next = e
+
     def on_chunk(self, b: int, e: int, grads) -> None:
+        if b != self._next or e != min(self._P, b + self._cs):
+            raise RuntimeError(f"OverlappedViewGrads: backward range [{b}, {e}) does not follow the range layout "
+                               f"(next {self._next}, size {self._cs}, P {self._P})")
         (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dsg_axis, dsg_sharpness, dsg_color, dscales,
          drotations) = grads
         rows = [dmeans3D[b:e], dopacity[b:e]]
         rows += [dscales[b:e], drotations[b:e]] if self._scales else [dcov3D[b:e]]
         if not self._sh:
             rows.append(dcolors[b:e])
-        cm_fn = _coalescing(self.group, rows)
-        if cm_fn is None:
-            self._works += [dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True) for t in rows]
-        else:
-            with cm_fn(group=self.group, async_ops=True) as cm:
-                for t in rows:
-                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-            self._works.append(cm)
-        if self._sh:
-            W = self.world
-            self._works.append(dist.all_gather_into_tensor(self._gathered[3 * W * b:3 * W * e], self._dc[3 * b:3 * e],
-                                                           group=self.group, async_op=True))
+        self._post(b, e, rows, self._dc[3 * b:3 * e] if self._sh else None)
+
+    def hook(self, grads):
+        """The per-range callback for the backward: errors are held (the C
+        backward keeps launching its ranges) until `settle`."""
+        def cb(b: int, e: int) -> None:
+            if self._error is None:
+                try:
+                    self.on_chunk(b, e, grads)
+                except BaseException as ex:  # noqa: BLE001 - re-raised by settle()
+                    self._error = ex
+        return cb
+
+    def settle(self, ok: bool) -> None:
+        """After the backward's launches: on a failed backward (`ok` False) or
+        a range whose exchange raised, keep the group in lockstep (`abort`)
+        and re-raise the range's error."""
+        if ok and self._error is None:
+            return
+        err = self._error
+        self.abort()
+        if err is not None:
+            raise err
+
+    def abort(self) -> None:
+        """The error path: post the collectives of every range not yet posted
+        — on NaN-filled rows, so the peers' summed gradients for those ranges
+        are NaN (visibly invalid) instead of silently missing this view —
+        then wait for every outstanding work and reset.  Every rank thus
+        posts the same collectives per backward, and no peer blocks."""
+        if not self._active:
+            return
+        self._active = False
+        try:
+            P, cs = self._P, self._cs
+            dev = self._campos_local.device
+            b = self._next
+            while b < P:
+                e = min(P, b + cs)
+                n = e - b
+                nan = lambda *shape: torch.full(shape, float("nan"), dtype=torch.float32, device=dev)  # noqa: E731
+                rows = [nan(n, 3), nan(n, 1)] + ([nan(n, 3), nan(n, 4)] if self._scales else [nan(n, 6)])
+                if not self._sh:
+                    rows.append(nan(n, 3))
+                if self._sh and (self._gathered is None or self._gathered.numel() < 3 * self.world * P):
+                    self._gathered = torch.empty(3 * self.world * P, dtype=torch.float32, device=dev)
+                self._post(b, e, rows, nan(3 * n) if self._sh else None)
+                b = e
+        finally:
+            works, self._works = self._works, []
+            for w in works:
+                try:
+                    w.wait()
+                except Exception:  # noqa: BLE001 - already failing; the original error is what is raised
+                    pass
 
     def finish(self, grads, means3D, sg_axis, sg_sharpness, sg_color, sh_degree: int, sg_degree: int) -> None:
+        if self._next != self._P:
+            msg = f"OverlappedViewGrads: the backward's ranges covered [0, {self._next}) of {self._P} Gaussians"
+            self.abort()
+            raise RuntimeError(msg)
+        self._active = False
         for w in self._works:
             w.wait()  # (RCCL: the backward's stream waits for the collective; no host synchronisation)
         self._works = []
@@ -386,9 +468,31 @@ class OverlappedViewGrads:
         (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dsg_axis, dsg_sharpness, dsg_color, dscales,
          drotations) = grads
         sg = [None if t is None or not t.numel() else t.detach() for t in (sg_axis, sg_sharpness, sg_color)]
-        self.expand(self._gathered, self._campos_all.view(self.world, 4), self.world, self.chunk_size(self._P),
+        self.expand(self._gathered, self._campos_all.view(self.world, 4), self.world, self._cs,
                     means3D.detach(), sh_degree, dsh, sg_degree, *sg,
                     *[None if t is None or not t.numel() else t for t in (dsg_axis, dsg_sharpness, dsg_color)])
+
+    def verify_replicas(self, params: Iterable[torch.Tensor]) -> None:
+        """Opt-in check after a training step's whole backward: every rank's
+        .grad must be identical (this exchange sums only the rasterizer's own
+        gradients; another loss term on the same parameters that was not
+        reduced makes the replicas drift).  One small all-reduce (MAX and
+        -MIN of float64 checksums) and a host synchronisation."""
+        sums = []
+        for p in params:
+            g = p.grad
+            sums += [0.0, 0.0] if g is None else [float(g.double().sum()), float(g.double().abs().sum())]
+        if not sums:
+            return
+        dev = self._campos_local.device if self._campos_local is not None else "cpu"
+        t = torch.tensor(sums + [-x for x in sums], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        n = len(sums)
+        hi, lo = t[:n], -t[n:]
+        if not bool(torch.equal(hi, lo)):
+            bad = int(torch.nonzero(hi != lo)[0]) // 2
+            raise RuntimeError(f"OverlappedViewGrads.verify_replicas: parameter {bad}'s gradients differ across "
+                               "ranks (a loss term outside the rasterizer was not reduced?)")
 
 
 def reduce_densification_stats(grad_norm_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,

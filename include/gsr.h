@@ -153,6 +153,13 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
                               float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
                               int chunks, gsr_chunk_fn on_chunk, void* chunk_ctx, float* dc_rows, void* stream);
 
+/* The Gaussian range size gsr_rasterize_backward_ex uses for `chunks` ranges
+ * of P Gaussians: ceil(ceil(P / chunks) / 256) * 256 (whole 256-Gaussian
+ * workgroups; the last range holds the rest).  The range-major layout of the
+ * gathered DC rows (gsr_view_color_grads_chunked) depends on it, so callers
+ * take it from here.  -1 for P < 0 or chunks < 1.  Host only. */
+int gsr_backward_chunk_size(int P, int chunks);
+
 /* Replaces CudaRasterizer::Rasterizer::markVisible (rasterizer.h:21-27,
  * rasterizer_impl.cu:186-197): present[i] = (view-space z > 0.2). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -86,6 +86,8 @@ def lib():
                                        + [ctypes.c_float] * 3 + [_f, _f, _u8, _i])
         L.gsro_knn_mean_dist.restype = ctypes.c_int
         L.gsro_knn_mean_dist.argtypes = [ctypes.c_int, _f, _f, _u32]
+        L.gsro_cov3d.argtypes = [ctypes.c_int, _f, ctypes.c_float, _f, _f]
+        L.gsro_cov3d_bwd.argtypes = [ctypes.c_int, _f, ctypes.c_float, _f, _f, _f, _f]
         L.gsro_sample_gaussians.restype = ctypes.c_void_p
         L.gsro_sample_gaussians.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -437,6 +439,28 @@ def warp_patch_ncc(depths, normals, uvs, R, T, image_r, image_n, fx_r, fy_r, cx_
                               _p(out["ncc"]), _p(out["grad_depths"]), _p(out["grad_normals"]), _p(out["valid"], _u8))
     out["valid"] = out["valid"].astype(bool)
     return out
+
+
+def cov3d(scales, scale_modifier, rotations):
+    """[P, 6] 3D covariance (xx, xy, xz, yy, yz, zz) of the scale/rotation
+    path, (S R)^T (S R) in the kernels' glm convention (gsro_cov3d)."""
+    s = np.ascontiguousarray(_np(scales), np.float32).reshape(-1, 3)
+    q = np.ascontiguousarray(_np(rotations), np.float32).reshape(-1, 4)
+    out = np.zeros((s.shape[0], 6), np.float32)
+    lib().gsro_cov3d(s.shape[0], _p(s), float(scale_modifier), _p(q), _p(out))
+    return out
+
+
+def cov3d_backward(scales, scale_modifier, rotations, dL_dcov3D):
+    """(dL/d(mod scale) [P, 3], dL/dq [P, 4]) of computeCov3D's backward
+    (render_backward.cu:193-244) alone (gsro_cov3d_bwd)."""
+    s = np.ascontiguousarray(_np(scales), np.float32).reshape(-1, 3)
+    q = np.ascontiguousarray(_np(rotations), np.float32).reshape(-1, 4)
+    g = np.ascontiguousarray(_np(dL_dcov3D), np.float32).reshape(-1, 6)
+    ds = np.zeros_like(s)
+    dq = np.zeros_like(q)
+    lib().gsro_cov3d_bwd(s.shape[0], _p(s), float(scale_modifier), _p(q), _p(g), _p(ds), _p(dq))
+    return ds, dq
 
 
 def knn_mean_dist(points):

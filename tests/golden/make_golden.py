@@ -27,6 +27,15 @@ reference's CUDA rasterizer, which cannot build in this image):
                    mode loss_utils.ssim asks fused_ssim for, :48-49) and
                    utils/graphics_utils.py:103-119 depth_to_normal, with the
                    reference's own fp32 torch autograd gradients (CPU).
+  cov3d.npz        scene/gaussian_model.py:46-50 build_covariance_from_scaling_rotation
+                   over utils/general_utils.py:77-113 (build_rotation,
+                   build_scaling_rotation, strip_symmetric): the 3D covariance
+                   of (scale, quaternion, scaling_modifier) — the glm
+                   column-major hazard of SURVEY §7 — and its fp32 autograd
+                   gradients w.r.t. scale and quaternion for random upstream
+                   gradients of the six covariance entries.
+
+    python tests/golden/make_golden.py [fixture ...]   (default: all)
 """
 from __future__ import annotations
 
@@ -367,14 +376,50 @@ def loss_fixture(rng):
     np.savez(os.path.join(OUT, "losses.npz"), **out)
 
 
+def cov3d_fixture(rng):
+    gm = importlib.import_module("scene.gaussian_model")
+    g = gm.GaussianModel(3, 0)  # setup_functions: covariance_activation (gaussian_model.py:46-55)
+    P = 96
+    scales = np.exp(rng.standard_normal((P, 3)) * 0.8 + math.log(0.05)).astype(np.float32)
+    rot = rng.standard_normal((P, 4)).astype(np.float32)
+    rot[:8] = np.eye(4, dtype=np.float32)[np.arange(8) % 4]  # axis-aligned: identity and half-turns
+    rot /= np.linalg.norm(rot, axis=1, keepdims=True)
+    up = rng.standard_normal((P, 6)).astype(np.float32)
+    zeros = torch.zeros  # build_rotation / build_scaling_rotation allocate with device="cuda"
+
+    def cpu_zeros(*a, **k):
+        k.pop("device", None)
+        return zeros(*a, **k)
+
+    out = dict(scales=scales, rotations=rot, upstream=up)
+    torch.zeros = cpu_zeros
+    try:
+        for tag, mod in (("m1", 1.0), ("m07", 0.7)):
+            s = torch.tensor(scales, requires_grad=True)
+            q = torch.tensor(rot, requires_grad=True)
+            cov = g.covariance_activation(s, mod, q)
+            (cov * torch.tensor(up)).sum().backward()
+            out.update({f"cov_{tag}": cov.detach().numpy(), f"dscales_{tag}": s.grad.numpy(),
+                        f"drotations_{tag}": q.grad.numpy()})
+    finally:
+        torch.zeros = zeros
+    np.savez(os.path.join(OUT, "cov3d.npz"), **out)
+
+
 def main():
     _install_stubs()
-    rng = np.random.default_rng(1234)
-    sh_fixture(rng)
-    camera_fixture(rng)
-    getters_fixture(rng)
-    boundary_fixture()
-    loss_fixture(np.random.default_rng(4321))
+    which = set(sys.argv[1:]) or {"sh", "boundary", "loss", "cov3d"}
+    if "sh" in which:  # sh_eval, cameras and getters share one random stream
+        rng = np.random.default_rng(1234)
+        sh_fixture(rng)
+        camera_fixture(rng)
+        getters_fixture(rng)
+    if "boundary" in which:
+        boundary_fixture()
+    if "loss" in which:
+        loss_fixture(np.random.default_rng(4321))
+    if "cov3d" in which:
+        cov3d_fixture(np.random.default_rng(2468))
     print("wrote", sorted(os.listdir(OUT)))
 
 

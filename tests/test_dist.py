@@ -268,3 +268,144 @@ def test_coalescing_choice_by_backend_and_device(tmp_path):
         assert _coalescing(None, [torch.zeros(3), Dev()]) is None
     finally:
         dist.destroy_process_group()
+
+
+# ---- OverlappedViewGrads on its error paths -------------------
+def _overlap_grads(P, seed):
+    g = torch.Generator().manual_seed(seed)
+    r = lambda *s: torch.randn(*s, generator=g)  # noqa: E731
+    return (torch.zeros(P, 3), torch.zeros(P, 3), r(P, 1), r(P, 3), torch.zeros(P, 6), torch.zeros(P, 16, 3),
+            torch.zeros(P, 0, 3), torch.zeros(P, 0), torch.zeros(P, 0, 3), r(P, 3), r(P, 4))
+
+
+def _error_worker(rank, world, port, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd"), HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gsr_dist import OverlappedViewGrads
+
+    P = 30
+
+    class Failing(OverlappedViewGrads):
+        def on_chunk(self, b, e, grads):
+            if rank == 0 and b == 8:
+                raise ValueError("injected failure in range [8, 16)")
+            super().on_chunk(b, e, grads)
+
+    ex = Failing(chunks=4, expand=_expand_chunked_ref)
+    ex.chunk_size = lambda P_: 8
+    grads = _overlap_grads(P, seed=rank)
+    mine = [t.clone() for t in grads]
+    ex.begin(torch.zeros(3), P, True, True)
+    ex.dc_rows(P, "cpu").copy_(torch.arange(3 * P, dtype=torch.float32) * (rank + 1))
+    cb = ex.hook(grads)
+    for b in range(0, P, 8):  # as gsr_rasterize_backward_ex calls its callback: every range, after a failure too
+        cb(b, min(P, b + 8))
+    raised = None
+    try:
+        ex.settle(True)
+        ex.finish(grads, torch.randn(P, 3), None, None, None, 3, 0)
+    except ValueError as e:
+        raised = str(e)
+    out = {"raised": raised, "works_left": len(ex._works), "active": ex._active,
+           "means3D": grads[3], "mine": mine[3]}
+    # the next backward runs normally after the failed one: the group is still in lockstep
+    ex2 = OverlappedViewGrads(chunks=4, expand=_expand_chunked_ref)
+    ex2.chunk_size = lambda P_: 8
+    g2 = _overlap_grads(P, seed=10 + rank)
+    ex2.begin(torch.zeros(3), P, True, False)
+    cb2 = ex2.hook(g2)
+    for b in range(0, P, 8):
+        cb2(b, min(P, b + 8))
+    ex2.settle(True)
+    ex2.finish(g2, None, None, None, None, 3, 0)
+    out["next_step"] = g2[3]
+    torch.save(out, os.path.join(outdir, f"e{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_exchange_failure_keeps_ranks_in_lockstep(tmp_path):
+    """A range whose exchange raises on one rank: that rank still
+    posts every remaining range's collectives — on NaN rows — waits for all of
+    its works and re-raises; the peer finishes its backward (no deadlock) with
+    the failed rank's ranges visibly NaN, and the next step runs normally."""
+    port = _free_port()
+    mp.start_processes(_error_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    e0 = torch.load(tmp_path / "e0.pt", weights_only=True)
+    e1 = torch.load(tmp_path / "e1.pt", weights_only=True)
+    assert e0["raised"] == "injected failure in range [8, 16)" and e1["raised"] is None
+    assert e0["works_left"] == 0 and not e0["active"] and not e1["active"]
+    m1 = e1["means3D"]
+    torch.testing.assert_close(m1[:8], e0["mine"][:8] + e1["mine"][:8])  # posted before the failure: summed
+    assert torch.isnan(m1[8:]).all()  # the failed rank's remaining ranges: NaN, not silently one view
+    want = _overlap_grads(30, 10)[3] + _overlap_grads(30, 11)[3]
+    torch.testing.assert_close(e0["next_step"], want)
+    torch.testing.assert_close(e1["next_step"], want)
+
+
+def _layout_worker(rank, world, port, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd"), HERE]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gsr_dist import OverlappedViewGrads
+    import pytest
+
+    P = 30
+    ex = OverlappedViewGrads(chunks=4, expand=_expand_chunked_ref)
+    ex.chunk_size = lambda P_: 8
+    g = _overlap_grads(P, seed=rank)
+    # a backward whose ranges do not follow the layout the gathered rows assume (a range size of 10, not 8)
+    ex.begin(torch.zeros(3), P, True, False)
+    cb = ex.hook(g)
+    for b in range(0, P, 10):
+        cb(b, min(P, b + 10))
+    with pytest.raises(RuntimeError, match="does not follow the range layout"):
+        ex.settle(True)
+    # a backward that stopped part-way (the C call failed after range 1) is settled by abort()
+    ex.begin(torch.zeros(3), P, True, False)
+    cb = ex.hook(g)
+    cb(0, 8)
+    cb(8, 16)
+    ex.settle(False)
+    assert not ex._works and not ex._active
+    # ranges that do not cover [0, P): finish refuses
+    ex.begin(torch.zeros(3), P, True, False)
+    cb = ex.hook(g)
+    cb(0, 8)
+    with pytest.raises(RuntimeError, match=r"covered \[0, 8\) of 30"):
+        ex.finish(g, None, None, None, None, 3, 0)
+    # verify_replicas: identical gradients pass, a rank-local extra term is caught
+    ps = [torch.ones(4, 3).requires_grad_(True), torch.ones(4, 1).requires_grad_(True)]
+    for p in ps:
+        p.grad = torch.full_like(p, 2.0)
+    ex.verify_replicas(ps)
+    if rank == 1:
+        ps[1].grad[0] += 1e-3
+    with pytest.raises(RuntimeError, match="parameter 1's gradients differ"):
+        ex.verify_replicas(ps)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_exchange_layout_and_replica_guards(tmp_path):
+    """Ranges that do not follow gsr_backward_chunk_size's layout are refused
+    (the DC rows would be rebuilt from the wrong views' rows); a backward that
+    failed part-way is settled with every range posted; ranges that stop
+    short are refused by finish; verify_replicas catches drifting replicas."""
+    port = _free_port()
+    mp.start_processes(_layout_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+
+
+def test_backward_chunk_size_is_the_library_s():
+    """One source for the range size: gsr_backward_chunk_size (host
+    only) and OverlappedViewGrads.chunk_size agree with the layout
+    view_color_grads_chunked reads."""
+    sys.path[:0] = [os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd")]
+    from diff_gaussian_rasterization import _C
+    import pytest
+
+    for P, c in [(0, 1), (1, 1), (255, 4), (256, 1), (1000, 4), (1_000_000, 4), (5_000_000, 7), (2**31 - 1, 3)]:
+        assert _C.backward_chunk_size(P, c) == ((P + c - 1) // c + 255) // 256 * 256
+    with pytest.raises(RuntimeError, match="chunks >= 1"):
+        _C.backward_chunk_size(10, 0)

@@ -100,23 +100,23 @@ def _check_binning(out, o, H, W, dead_sample=None):
         assert np.all((power > 0) | (alpha < 1.0 / 255.0)), (t, g)
 
 
-def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True):
+def _run(c, colors_precomp=None, cov3D=None, scale_modifier=1.0, check_bwd=True, gpu_views=None):
     from diff_gaussian_rasterization import _C
 
     a = _fwd_args(c, colors_precomp, cov3D, scale_modifier)
     o = O.forward(*a)
     ga = [_gpu(x) for x in a] + [False]
+    if gpu_views is not None:  # the device inputs as other layouts of the same values
+        ga = gpu_views(ga)
     out = _C.rasterize_gaussians(*ga)
     K, color, alpha, normal, mdepth, radii = out[:6]
     assert K == o["num_rendered"]
     assert np.array_equal(radii.cpu().numpy(), o["radii"])
     _check_binning(out, o, c["H"], c["W"])
     geom = c["require_depth"]
-    for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
-        if not geom and name in ("normal", "mdepth"):
-            assert float(t.abs().max()) == 0.0
-            continue
-        _check_image(name, t.cpu().numpy(), o[name])
+    if not geom:
+        assert float(normal.abs().max()) == 0.0 and float(mdepth.abs().max()) == 0.0
+    _audit_full_images(c, out, o)
     if not check_bwd:
         return
     g = S.upstream_grads(c["H"], c["W"])
@@ -211,7 +211,11 @@ def test_parity_small(case):
 
 YARDSTICK = [dict(P=300, W=64, H=48, seed=1), dict(P=400, W=64, H=48, seed=40, opacity_max_logit=6.0, opacity_std=3.0),
              dict(P=400, W=64, H=48, seed=42, sh_degree=1, sh_max_degree=3),
-             dict(P=300, W=64, H=48, seed=10, sgm=7, sg_degree=7)]
+             dict(P=300, W=64, H=48, seed=10, sgm=7, sg_degree=7),
+             # surfels (1000x flattened: what a trained Geometry-Grounded GS scene is made of): the fp32
+             # problem is ill-conditioned (the oracle itself is ~1e-3 from float64), so only the relative
+             # criterion applies: the GPU no further from float64 than 2x the oracle
+             dict(P=2000, W=96, H=64, seed=11, flat=1000.0, relative_only=True)]
 
 
 @pytest.mark.parametrize("case", YARDSTICK, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
@@ -225,6 +229,8 @@ def test_float64_yardstick(case):
     import torch_ref as R
     from diff_gaussian_rasterization import _C
 
+    case = dict(case)
+    relative_only = case.pop("relative_only", False)
     c = Hh.small_case(**case)
     a = _fwd_args(c)
     o = O.forward(*a)
@@ -265,7 +271,7 @@ def test_float64_yardstick(case):
         e_orc = Hh.rel_err(b[name], e)
         print(f"{name}: gpu-vs-f64 {e_gpu:.2e}  oracle-vs-f64 {e_orc:.2e}")
         assert e_gpu <= 2 * e_orc + 1e-6, (name, e_gpu, e_orc)
-        assert e_gpu <= 1e-4, (name, e_gpu)
+        assert relative_only or e_gpu <= 1e-4, (name, e_gpu)
 
 
 @pytest.mark.parametrize("stage", [1, 2], ids=["staged", "per-lane"])
@@ -284,6 +290,96 @@ def test_parity_row_store_paths(case, stage):
         _run(Hh.small_case(**case))
     finally:
         _C.set_option(_C.OPT_PBWD_STAGE, 0)
+
+
+def _offset_view(t):
+    """The same values as a contiguous device view 4 B into a larger buffer
+    (a slice of a bigger parameter tensor), so its base is not 16-B aligned."""
+    buf = torch.empty(t.numel() + 1, dtype=t.dtype, device=DEV)
+    v = buf[1:].view(t.shape)
+    v.copy_(t)
+    assert v.is_contiguous() and v.data_ptr() % 16 == 4
+    return v
+
+
+@pytest.mark.parametrize("stage", [0, 1], ids=["default", "staged-forced"])
+def test_parity_sg7_offset_views(stage):
+    """SG-7 lobe rows (and the SH rows, rotations) handed over as views at a
+    4-B offset: the staged per-Gaussian backward reads the lobe
+    rows by 16-B LDS-DMA, so misaligned rows must take the per-lane path —
+    even when the stage is forced — and every output stays at the oracle bar."""
+    from diff_gaussian_rasterization import _C
+
+    def views(ga):
+        for k in (5, 7, 8, 9, 10):  # rotations, shs, sg_axis, sg_sharpness, sg_color
+            ga[k] = _offset_view(ga[k])
+        return ga
+
+    _C.set_option(_C.OPT_PBWD_STAGE, stage)
+    try:
+        _run(Hh.small_case(P=3001, W=96, H=64, seed=54, sgm=7, sg_degree=7), gpu_views=views)
+    finally:
+        _C.set_option(_C.OPT_PBWD_STAGE, 0)
+
+
+@pytest.mark.parametrize("geom", [False, True], ids=["color", "depth"])
+def test_cov3d_precomp_path_pinned_to_reference_covariance(geom):
+    """The GPU's two covariance inputs against each other, with the
+    covariance computed by the reference's own Python (tests/golden/cov3d.npz,
+    scene/gaussian_model.py:46-50; the oracle's convention is pinned to it in
+    test_oracle.py): the scale/rotation path and cov3D_precomp = the
+    reference's covariance give the same K, radii and images (1e-4), and
+    without depth the backward agrees through the chain rule — dL/dscale and
+    dL/dq of the scale/rotation path equal computeCov3D's backward (the pinned
+    oracle restatement) applied to the cov3D_precomp path's dL/dcov3D."""
+    import os
+    from diff_gaussian_rasterization import _C
+
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "cov3d.npz"))
+    P = d["scales"].shape[0]
+    c = Hh.small_case(P=P, W=64, H=48, seed=60, require_depth=geom, z_range=(2.0, 4.0))
+    c["inp"]["scales"] = torch.from_numpy(d["scales"]).contiguous()
+    c["inp"]["rotations"] = torch.from_numpy(d["rotations"]).contiguous()
+    cov = torch.from_numpy(d["cov_m1"]).contiguous()
+    ga_sr = [_gpu(x) for x in _fwd_args(c)] + [False]
+    ga_cv = [_gpu(x) for x in _fwd_args(c, cov3D=cov)] + [False]
+    o_sr = _C.rasterize_gaussians(*ga_sr)
+    o_cv = _C.rasterize_gaussians(*ga_cv)
+    assert o_sr[0] == o_cv[0] and torch.equal(o_sr[5], o_cv[5])
+    assert int((o_sr[5] > 0).sum()) > P // 2
+    names = ["color", "alpha"] + (["normal", "mdepth"] if geom else [])
+    for k, name in zip((1, 2, 3, 4), names):
+        err = Hh.rel_err(o_cv[k].cpu().numpy(), o_sr[k].cpu().numpy())
+        assert err <= 1e-4, (name, err)
+    if geom:
+        return
+    g = {k: _gpu(v) for k, v in S.upstream_grads(c["H"], c["W"], seed=61).items()}
+
+    def bwd(ga, o):
+        return _C.rasterize_gaussians_backward(*ga[:19], g["color"], g["mdepth"], g["alpha"], g["normal"], o[2], o[3],
+                                               o[4], _gpu(c["cam"].camera_center), o[5], o[6], o[0], o[7], o[8], o[9],
+                                               False, False)
+
+    b_sr, b_cv = bwd(ga_sr, o_sr), bwd(ga_cv, o_cv)
+    ds, dq = O.cov3d_backward(d["scales"], 1.0, d["rotations"], b_cv[4].cpu().numpy())
+    # the same two fp32 paths through the oracle: how far apart two valid fp32 evaluations of the chain
+    # land on this scene (the rotation gradients of near-isotropic Gaussians cancel), the yardstick for the GPU's
+    gc = {k: v for k, v in S.upstream_grads(c["H"], c["W"], seed=61).items()}
+    a_sr, a_cv = _fwd_args(c), _fwd_args(c, cov3D=cov)
+    orc = {}
+    for tag, a_ in (("sr", a_sr), ("cv", a_cv)):
+        o_ = O.forward(*a_)
+        orc[tag] = O.backward(o_["state"], *a_[:19], gc["color"], gc["mdepth"], gc["alpha"], gc["normal"],
+                              torch.from_numpy(o_["alpha"]), torch.from_numpy(o_["normal"]),
+                              torch.from_numpy(o_["mdepth"]), c["cam"].camera_center, o_["radii"])
+    ods, odq = O.cov3d_backward(d["scales"], 1.0, d["rotations"], orc["cv"]["dcov3D"])
+    for name, mine, want, o_mine, o_want in (("dscales", b_sr[9], ds, orc["sr"]["dscales"], ods),
+                                             ("drotations", b_sr[10], dq, orc["sr"]["drotations"], odq)):
+        mine = mine.cpu().numpy().astype(np.float64)
+        l2 = np.linalg.norm(mine - want) / np.linalg.norm(want)
+        o_l2 = np.linalg.norm(o_mine - o_want) / np.linalg.norm(o_want)
+        print(f"{name}: gpu chain L2 {l2:.2e}, oracle chain L2 {o_l2:.2e}")
+        assert l2 <= 2 * o_l2 + 1e-5 and l2 <= 3e-4, (name, l2, o_l2)
 
 
 def _with_depth_ties(c, n_tied):
@@ -325,11 +421,12 @@ def test_parity_long_tile_lists():
 
 def test_parity_surfels_forward():
     """1000x-flattened Gaussians (vacancy T(t) made of near-steps): forward
-    parity at the 1e-4 bar.  The backward is not compared: there the fp32
-    problem itself is ill-conditioned (the oracle differs from a float64
-    restatement by 2e-3 in dmeans2D and 15% in dmeans3D on this scene; the
-    GPU differs from the oracle by 1.1e-4), so a 1e-4 gradient bar would test
-    rounding, not parity."""
+    parity at the 1e-4 bar.  The backward is not compared with the oracle at
+    1e-4: there the fp32 problem itself is ill-conditioned (the oracle differs
+    from a float64 restatement by 2e-3 in dmeans2D and 15% in dmeans3D on
+    this scene), so a 1e-4 gradient bar would test rounding, not parity; the
+    surfel backward is held to the float64 yardstick instead
+    (test_float64_yardstick, relative criterion)."""
     _run(Hh.small_case(P=2000, W=96, H=64, seed=11, flat=1000.0), check_bwd=False)
 
 
@@ -570,6 +667,52 @@ def c3():
     return c
 
 
+def _audit_full_images(c, out, o, report=None):
+    """Every pixel of every image against the oracle, with an exact account of
+    the pixels where the two fp32 forwards decide differently (tests/flip_audit.py):
+      * last contributor: equal to the oracle's everywhere except at flip
+        pixels (at most 1e-5 of the image, 2 on small images), each proven a near-tie — some
+        decision between the two last contributors is within 2e-4 (relative,
+        float64) of its threshold (T (1 - alpha) = 1e-4, alpha = 1/255);
+      * colour, alpha, normal: every other pixel within 1e-4 of the image max;
+      * median depth: every other pixel within 1e-4, except where the
+        bisection's own decisions are ill-conditioned — each such pixel is
+        proven so in float64 (T within 1e-4 of 1/2 at both depths and between
+        them, or at the in-range tests) and they number at most 1e-4 of the image (2 on small ones).
+    Must run before the oracle state takes the GPU's contributors."""
+    import flip_audit as FA
+
+    H, W = c["H"], c["W"]
+    K, color, alpha, normal, mdepth = out[:5]
+    nc_gpu = Hh.gpu_n_contrib_for_oracle(out, o, H, W).astype(np.int64)
+    nc_orc = o["state"].n_contrib().astype(np.int64)
+    flip = nc_gpu != nc_orc
+    ch = FA.PixelChains(o, W, H, c["tanx"], c["tany"])
+    nc_margins = [FA.ncontrib_flip_margin(ch, int(x), int(y), nc_gpu[y, x], nc_orc[y, x])
+                  for y, x in np.argwhere(flip)]
+    rep = {"pixels": H * W, "n_contrib_flips": int(flip.sum()),
+           "n_contrib_flip_max_margin": max(nc_margins, default=0.0)}
+    for name, t in (("color", color), ("alpha", alpha), ("normal", normal)):
+        a_, b_ = t.cpu().numpy().astype(np.float64), o[name].astype(np.float64)
+        bad = (np.abs(a_ - b_) > 1e-4 * np.abs(b_).max()).reshape(-1, H, W).any(0)
+        rep[name + "_bad_off_flip"] = int((bad & ~flip).sum())
+        rep[name + "_bad_at_flip"] = int((bad & flip).sum())
+    md_g, md_o = mdepth.cpu().numpy()[0].astype(np.float64), o["mdepth"][0].astype(np.float64)
+    md_bad = (np.abs(md_g - md_o) > 1e-4 * np.abs(md_o).max()) & ~flip
+    md_margins = [FA.mdepth_flip_margin(ch, int(x), int(y), ch.depth_of(int(x), int(y), md_g[y, x]),
+                                        ch.depth_of(int(x), int(y), md_o[y, x])) for y, x in np.argwhere(md_bad)]
+    rep.update(mdepth_bad_off_flip=int(md_bad.sum()), mdepth_max_margin=max(md_margins, default=0.0))
+    print("image audit:", rep)
+    if report is not None:
+        report.update(rep)
+    assert rep["n_contrib_flips"] <= max(2, 1e-5 * H * W), rep
+    assert rep["n_contrib_flip_max_margin"] <= 2e-4, rep
+    for name in ("color", "alpha", "normal"):
+        assert rep[name + "_bad_off_flip"] == 0, (name, rep)
+    assert rep["mdepth_bad_off_flip"] <= max(2, 1e-4 * H * W), rep
+    assert rep["mdepth_max_margin"] <= 1e-4, rep
+
+
 def _full_parity(c, dead_sample):
     """Every pixel and every per-Gaussian gradient of a full-size scene
     against the oracle (16 threads), the oracle backward on the GPU
@@ -590,10 +733,7 @@ def _full_parity(c, dead_sample):
     assert K == o["num_rendered"]
     assert np.array_equal(radii.cpu().numpy(), o["radii"])
     _check_binning(out, o, H, W, dead_sample=dead_sample)
-    for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
-        a_, b_ = t.cpu().numpy(), o[name]
-        bad = np.abs(a_ - b_) > 1e-4 * np.abs(b_).max()
-        assert bad.mean() <= 1e-4, (name, bad.mean())  # isolated float-decision flips only
+    _audit_full_images(c, out, o)
     # the clamp branch runs: visible Gaussians with o > 0.99 (alpha = min(0.99, o G) clamps at their centres)
     assert int(((c["inp"]["opacities"][:, 0] > 0.99) & (torch.from_numpy(o["radii"]) > 0)).sum()) > 0
     g = S.upstream_grads(H, W, seed=3)
@@ -700,10 +840,7 @@ def test_c2_forward_parity(c2):
     assert K == o["num_rendered"]
     assert np.array_equal(radii.cpu().numpy(), o["radii"])
     _check_binning(out, o, c2["H"], c2["W"], dead_sample=20000)
-    for name, t in (("color", color), ("alpha", alpha), ("normal", normal), ("mdepth", mdepth)):
-        a_, b_ = t.cpu().numpy(), o[name]
-        bad = np.abs(a_ - b_) > 1e-4 * np.abs(b_).max()
-        assert bad.mean() <= 1e-4, (name, bad.mean())
+    _audit_full_images(c2, out, o)
 
 
 def test_c2_compacted_fallback_matches_bisection(c2):
@@ -839,10 +976,7 @@ def test_c2_full_forward_parity():
     assert out[0] == o["num_rendered"]
     assert np.array_equal(out[5].cpu().numpy(), o["radii"])
     _check_binning(out, o, 800, 800, dead_sample=20000)
-    for name, t in (("color", out[1]), ("alpha", out[2]), ("normal", out[3]), ("mdepth", out[4])):
-        a, b = t.cpu().numpy(), o[name]
-        bad = np.abs(a - b) > 1e-4 * np.abs(b).max()
-        assert bad.mean() <= 1e-4, (name, bad.mean())  # isolated float-decision flips only
+    _audit_full_images(c, out, o)
 
 
 @pytest.mark.timeout(400)

@@ -109,6 +109,35 @@ CASES = [
 ]
 
 
+def test_cov3d_matches_reference_fixture():
+    """The covariance convention (the glm column-major hazard)
+    pinned to the reference's own Python: scene/gaussian_model.py:46-50
+    build_covariance_from_scaling_rotation over utils/general_utils.py:77-113
+    (tests/golden/cov3d.npz), forward and fp32 autograd gradients.  The
+    kernels' Sigma = (S R)^T (S R) (gsro_cov3d) equals the reference's
+    L L^T (L = R S); computeCov3D's backward (render_backward.cu:193-244)
+    gives dL/d(mod scale) (the Python gradient is mod times
+    it) and dL/dq of the unnormalised quaternion (App. B.3: the Python,
+    which normalises, sees its tangential part)."""
+    d = np.load(os.path.join(GOLD, "cov3d.npz"))
+    q = d["rotations"].astype(np.float64)
+    for tag, mod in (("m1", 1.0), ("m07", 0.7)):
+        cov = O.cov3d(d["scales"], mod, d["rotations"])
+        ref = d["cov_" + tag]
+        assert np.abs(cov - ref).max() <= 2e-6 * np.abs(ref).max(), tag
+        ds, dq = O.cov3d_backward(d["scales"], mod, d["rotations"], d["upstream"])
+        want_s = d["dscales_" + tag]
+        assert np.abs(mod * ds - want_s).max() <= 1e-5 * np.abs(want_s).max(), tag
+        dq = dq.astype(np.float64)
+        tang = dq - q * (q * dq).sum(1, keepdims=True)
+        want_q = d["drotations_" + tag]
+        assert np.abs(tang - want_q).max() <= 1e-5 * np.abs(want_q).max(), tag
+    # a transposed rotation (the classic mis-transpose) is caught by the fixture
+    qt = d["rotations"].copy()
+    qt[:, 1:] *= -1  # conjugate quaternion: R^T
+    assert np.abs(O.cov3d(d["scales"], 1.0, qt) - d["cov_m1"]).max() > 1e-3 * np.abs(d["cov_m1"]).max()
+
+
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_oracle_matches_float64_autograd(case):
     case = dict(case)
