@@ -144,6 +144,10 @@ def parse():
     ap.add_argument("--cpu-tile-stride", type=int, default=0, help="0 = auto")
     ap.add_argument("--stage-steps", type=int, default=5,
                     help="untimed steps with every stage bracketed by hipEvents (the per-stage table)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="time the whole training iteration after iteration 7000 (train.py:142-262: render, "
+                         "depth-normal, PatchMatch with sample_depth + NCC, SSIM, backward, densification "
+                         "statistics, Adam) instead of the raster alone; one line with a per-component breakdown")
     ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)  # tests: ranks report and exit
     ap.add_argument("--all-stage-events", action="store_true",
                     help="bracket every stage with hipEvents inside the timed region too (each event pair "
@@ -162,11 +166,16 @@ def parse():
     return a
 
 
-def stage_bytes(P, K, K_live, HW, shm, sgm, geom):
+def stage_bytes(P, K, K_live, HW, shm, sgm, geom, K_contrib=None):
     """Algorithmic (compulsory) HBM bytes per launch of each stage, from the
     per-unit figures of SURVEY.md §8(d).  K is the reference's instance count
-    (rect tiles); the stages after binning process the K_live instances that
-    survive tile culling, so their unit count is K_live."""
+    (rect tiles); the binning stages produce the K_live instances that survive
+    tile culling.  The raster kernels read each tile's list
+    only up to its max contributor (the last position any pixel blended: the
+    backward's loop bound, the forward's saturation point), so their gather
+    unit count is K_contrib = sum over tiles of max_contrib (None: K_live,
+    the upper bound of SURVEY §8(d)'s formula)."""
+    K_r = K_live if K_contrib is None else K_contrib
     Bp = 44 + 12 * shm + 28 * sgm
     G = 64 if geom else 36
     Opx = 36 if geom else 20
@@ -181,9 +190,9 @@ def stage_bytes(P, K, K_live, HW, shm, sgm, geom):
         "tile_ranges": K_live * 2,
         # q-ordered Gaussians (index + splat rect/conic + radius) in, per-tile lists out
         "tile_lists": P * 40 + K_live * 4,
-        "render_fwd": K_live * (4 + G) + HW * Opx,
+        "render_fwd": K_r * (4 + G) + HW * Opx,
         "bwd_clear": P * A,
-        "render_bwd": HW * Ipx + K_live * (4 + G),
+        "render_bwd": HW * Ipx + K_r * (4 + G),
         "preprocess_bwd": P * (A + Bp + 8 + Bp),
     }
 
@@ -323,6 +332,46 @@ def time_exchange(mode, P, shm, sgm, world, chunks, dev, reps=10):
             "bus_GBps": round(bus_bytes / (ms * 1e-3) / 1e9, 2)}
 
 
+def run_e2e(args, dev):
+    """bench.py --e2e: one training iteration (gsr_train.TrainStep) per step."""
+    import gsr_train
+
+    W, H, P = args.width, args.height, args.P
+    ts, view, nearest = gsr_train.synthetic_training_setup(P, W, H, args.sh_degree, args.sg_degree, device=dev)
+    for _ in range(args.warmup):
+        ts.step(view, nearest)
+    torch.cuda.synchronize(dev)
+    comps = {k: [] for k in ts.COMPONENTS}
+    ts.timing = True
+    for _ in range(max(1, args.stage_steps)):
+        ts.step(view, nearest)
+        for k, v in ts.component_ms().items():
+            comps[k].append(v)
+    ts.timing = False
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = ts.step(view, nearest)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / args.steps * 1e3
+    line = {
+        "metric": "train iters/sec (full training iteration after iteration 7000) at 1080p, 1M Gaussians",
+        "value": round(args.steps / elapsed, 3), "unit": "iters/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (ground truth: renders of perturbed Gaussians)",
+        "config": {"workload": (f"e2e {args.config}: {P} Gaussians (SH {args.sh_degree}, SG {args.sg_degree}), "
+                                f"{W}x{H}, train.py:142-262 after iteration 7000: getters, render(require_depth), "
+                                "L1 + fused SSIM, depth_to_normal loss, PatchMatch (sample_depth from the nearest "
+                                "view + geometric loss + warp_patch_ncc), backward, densification statistics, "
+                                "FusedAdam step"),
+                   "P": P, "width": W, "height": H, "loss": float(loss)},
+        "components_ms": {k: round(sorted(v)[len(v) // 2], 4) for k, v in comps.items()},
+        "roofline": None, "cpu_baseline": None,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     cmd = check_launch(args)
@@ -345,6 +394,10 @@ def main():
         return
     # (a rehearsal with more ranks than GPUs shares the devices; device_count() does not initialise the GPU)
     dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    if args.e2e:
+        if world > 1:
+            raise SystemExit("bench.py --e2e runs on one GPU")
+        return run_e2e(args, dev)
     if world > 1:
         torch.cuda.set_device(dev)
         if args.dist_backend == "nccl":
@@ -501,10 +554,12 @@ def main():
                                     args.sg_degree, 1.0, cam.world_view_transform, cam.full_proj_transform, tanx,
                                     tany, 0.0, H, W, cam.camera_center, False, geom, False)
         K_live = int(_C.debug_binning(fo[7], fo[9], fo[0], H, W, with_list=False)[1][:, 1].max())
+        K_contrib = int(_C.debug_max_contrib(fo[9], H, W).astype("int64").sum())
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.steps / elapsed
     shm = (args.sh_degree + 1) ** 2
-    algo = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom)
+    algo = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom, K_contrib)
+    algo_upper = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom)
     per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in stages.items()}
     if not args.all_stage_events:  # the other stages from the untimed table
         per_launch = {k: (per_launch[k] if k == dom else v) for k, v in table_ms.items()}
@@ -524,6 +579,11 @@ def main():
     roofline = {"bound": bound, "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(hbm_frac, 5),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(algo[dom]),
+                "algorithmic_units": ("instances read up to each tile's max contributor (sum of max_contrib: "
+                                      f"{K_contrib}) x (4 + {64 if geom else 36}) B + pixels x "
+                                      f"{(36 if geom else 20) if dom == 'render_fwd' else (56 if geom else 24)} B"
+                                      if dom in ("render_fwd", "render_bwd") else "SURVEY §8(d) per-unit bytes"),
+                "upper_bound_bytes_per_launch": int(algo_upper[dom]),
                 "avg_launch_ms": round(per_launch[dom], 4),
                 "valu": None if valu_frac is None else {
                     "frac": round(valu_frac, 4), "insts_per_launch": int(valu_insts),
@@ -547,6 +607,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": workload, "P": P, "width": W, "height": H, "sh_degree": args.sh_degree,
                        "sg_degree": args.sg_degree, "require_depth": geom, "num_rendered": int(K), "instances_after_tile_culling": K_live,
+                       "instances_to_max_contributor": K_contrib,
                        "parallelism": f"view-parallel dp{world}" if world > 1 else "single",
                        "step_algorithmic_GBps": round(total_algo / (ms_per_step * 1e-3) / 1e9, 2)},
             "roofline": roofline,

@@ -446,6 +446,18 @@ int gsr_debug_image(const void* image_buffer, int width, int height, uint32_t* n
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "debug image", e);
 }
 
+int gsr_debug_tile_stats(const void* tile_buffer, int width, int height, uint32_t* max_contrib_out, void* stream_ptr) {
+    if (!tile_buffer || width <= 0 || height <= 0 || !max_contrib_out) return fail(GSR_ERR_ARGS, "invalid arguments");
+    const int tiles = (int)(((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile));
+    TileState ts{};
+    carve_tiles(aligned_base(const_cast<void*>(tile_buffer)), tiles, ts);
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    hipError_t e = hipMemcpyAsync(max_contrib_out, ts.max_contrib, sizeof(uint32_t) * (size_t)tiles,
+                                  hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "debug tile stats", e);
+}
+
 int gsr_set_option(int opt, int value) {
     if (opt < 0 || opt >= gsr::kNumOptions || gsr::option_retired(opt)) return fail(GSR_ERR_ARGS, "unknown option");
     gsr::g_options[opt] = value;
@@ -739,7 +751,7 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
     if (!wbuf) return fail(GSR_ERR_ALLOC, "backward buffer allocation failed");
     void* wb = aligned_base(wbuf);
     carve_bwd(wb, P, ws, tiles);
-    if (!option(kOptNoTileOrder) && tiles > 0) {
+    if (tiles > 0) {
         // heaviest tiles first (cost: the forward's per-tile max contributor),
         // ordered by one workgroup while the others clear the accumulators
         const size_t zbytes = (size_t)(reinterpret_cast<char*>(ws.tile_order) - static_cast<char*>(wb));
@@ -1068,7 +1080,7 @@ int gsr_sample_depth_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
     void* wb = aligned_base(wbuf);
     carve_bwd(wb, P, ws, (int)bound);
     GSR_STAGE(GSR_STAGE_BWD_CLEAR, hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");
-    if (!option(kOptNoTileOrder) && bound)  // heaviest chunks first (cost: the forward's chunk max contributor)
+    if (bound)  // heaviest chunks first (cost: the forward's chunk max contributor)
         GSR_STAGE(GSR_STAGE_BWD_CLEAR, launch_chunk_order(bound, st.totals + 2, cs.chunk_max, ws.tile_order, stream),
                   "chunk order");
     else

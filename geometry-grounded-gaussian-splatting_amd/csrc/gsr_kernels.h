@@ -10,8 +10,8 @@ namespace gsr {
 // (gsr_set_option in include/gsr.h); defaults are the shipped paths.
 // ids 0, 7 and 8 belonged to retired A/B variants (bisection shortcut, per-tile
 // sort binning, two-wave backward); gsr_set_option rejects them
-enum Option : int { kOptRenderStats = 1, kOptBisectPasses = 2, kOptBwdNoPrepass = 3, kOptNoTileOrder = 4, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptRocprimDsort = 9, kOptPbwdStage = 10, kNumOptions = 11 };
-inline bool option_retired(int opt) { return opt == 0 || opt == 7 || opt == 8; }
+enum Option : int { kOptRenderStats = 1, kOptNoRefine = 5, kOptBwdNoCache = 6, kOptRocprimDsort = 9, kOptPbwdStage = 10, kNumOptions = 11 };
+inline bool option_retired(int opt) { return opt == 0 || (opt >= 2 && opt <= 4) || opt == 7 || opt == 8; }
 int option(int which);
 hipError_t read_render_stats(unsigned long long* out, bool reset);
 

@@ -39,12 +39,14 @@ struct RenderBwdArgs {
     const float* dL_dnormal;
     float* acc;      // [P][16]
     float* acc_abs;  // [P]
-    int skip_prepass;  // diagnostic (GSR_OPT_BWD_NO_PREPASS): time the kernel without the pre-pass
     int no_cache;      // GSR_OPT_BWD_NO_CACHE: recompute dT/dt_m everywhere
     const uint32_t* tile_order;  // [tiles] launch order (heaviest first) or null: XCD-contiguous
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+#ifndef GSR_BWD_WAVES
+#define GSR_BWD_WAVES 3
+#endif
 constexpr int kBwdBatch = 128;    // splat records staged per LDS batch (8.5 KB: 3 one-wave blocks per SIMD)
 
 __device__ __forceinline__ f2 sel2(bool ca, bool cb, f2 x, f2 y) { return f2{ca ? x.x : y.x, cb ? x.y : y.y}; }
@@ -142,7 +144,7 @@ __device__ __forceinline__ PixPair load_pair(const RenderBwdArgs& a, int px, int
 // 0.568 at 168, 0.619 with 2 spilled registers; 4 waves per SIMD spill 72;
 // NP = 1 0.565.
 template <bool GEOM, int NP>
-__global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(NP == 1 ? 4 : 3, 8)))
+__global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(NP == 1 ? 4 : GSR_BWD_WAVES, 8)))
     render_bwd_kernel(RenderBwdArgs a) {
     constexpr int kThreads = 128 / NP;
     __shared__ float4 s_w0[kBwdBatch], s_w1[kBwdBatch], s_w2[kBwdBatch], s_w3[kBwdBatch];
@@ -184,7 +186,7 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
     f2 kappa[NP];
 #pragma unroll
     for (int k = 0; k < NP; k++) kappa[k] = zero;
-    if (GEOM && !a.skip_prepass) {
+    if (GEOM) {
         f2 dT_dtm[NP];
         bool on_a[NP], on_b[NP];
         uint32_t mine = 0;
@@ -238,20 +240,24 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
     // ---- main back-to-front pass (render_backward.cu:882-1068)
     // The reference carries (last_alpha, last_colour) one step and folds them
     // into accum_rec at the NEXT valid contributor; here a contributor is
-    // folded in right after its own terms (same values; accum_rec's update is
-    // written as one fma, a few ulp from the reference's rounding).  A pixel
-    // for which the splat is not valid runs with alpha = 0, which leaves
-    // T (x rcp(1) = 1), accum_rec (+ 0 x d) and the plane terms unchanged
-    // exactly, so only G dL/dopacity needs a select.
+    // folded in right after its own terms.  accum_rec (and accum_normal) enter
+    // the gradient only through sum_ch (c_ch - accum_rec_ch) dL/dpixel_ch
+    // (render_backward.cu:946-957), so the pixel keeps the one running dot
+    // product S = sum_ch accum_rec_ch dL/dpixel_ch instead of the three
+    // channels: dL/dalpha = c.dL - S, then S += alpha (c.dL - S) — the same
+    // recurrence, dotted with the pixel's constant dL/dpixel (5 operations per
+    // pixel instead of 9, a few ulp of rounding apart).  A pixel for which the
+    // splat is not valid runs with alpha = 0, which leaves T (x rcp(1) = 1), S
+    // (+ 0 x d) and the plane terms unchanged exactly, so only G dL/dopacity
+    // needs a select.
     uint32_t contributor = (uint32_t)max_contrib;
-    f2 T[NP], tfd[NP], kh[NP], ar0[NP], ar1[NP], ar2[NP], an0[NP], an1[NP], an2[NP];
+    f2 T[NP], tfd[NP], kh[NP], sc[NP], sn[NP];
 #pragma unroll
     for (int k = 0; k < NP; k++) {
         T[k] = pp[k].T_final;
         tfd[k] = -pp[k].T_final * pp[k].dL_dfinalT;  // dL/dopacity term of the final transmittance, / (1 - alpha)
         kh[k] = 0.5f * kappa[k];
-        ar0[k] = ar1[k] = ar2[k] = zero;
-        an0[k] = an1[k] = an2[k] = zero;
+        sc[k] = sn[k] = zero;
     }
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
     int toDo = max_contrib;
@@ -325,23 +331,22 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
                 const f2 r1a = {fast_rcp(one_m_alpha.x), fast_rcp(one_m_alpha.y)};
                 T[k] = T[k] * r1a;
                 const f2 bw = alpha * T[k];
-                // accum_rec = alpha c + (1 - alpha) accum_rec as accum_rec + alpha (c - accum_rec)
-                const f2 d0 = splat2(w2.z) - ar0[k], d1 = splat2(w2.w) - ar1[k], d2 = splat2(w3.x) - ar2[k];
-                f2 dL_dopa = d0 * P.dLp0 + d1 * P.dLp1 + d2 * P.dLp2;
-                ar0[k] = __builtin_elementwise_fma(alpha, d0, ar0[k]);
-                ar1[k] = __builtin_elementwise_fma(alpha, d1, ar1[k]);
-                ar2[k] = __builtin_elementwise_fma(alpha, d2, ar2[k]);
+                // accum_rec . dL/dpixel as S + alpha (c . dL/dpixel - S)
+                const f2 cdl = __builtin_elementwise_fma(
+                    splat2(w3.x), P.dLp2, __builtin_elementwise_fma(splat2(w2.w), P.dLp1, splat2(w2.z) * P.dLp0));
+                f2 dL_dopa = cdl - sc[k];
+                sc[k] = __builtin_elementwise_fma(alpha, dL_dopa, sc[k]);
                 const f2 c0 = bw * P.dLp0, c1 = bw * P.dLp1, c2 = bw * P.dLp2;
                 Fc0 = k ? Fc0 + c0 : c0;
                 Fc1 = k ? Fc1 + c1 : c1;
                 Fc2 = k ? Fc2 + c2 : c2;
                 f2 dL_dt = zero;
                 if constexpr (GEOM) {
-                    const f2 e0 = splat2(w3.y) - an0[k], e1 = splat2(w3.z) - an1[k], e2 = splat2(w3.w) - an2[k];
-                    dL_dopa += e0 * P.dLn0 + e1 * P.dLn1 + e2 * P.dLn2;
-                    an0[k] = __builtin_elementwise_fma(alpha, e0, an0[k]);
-                    an1[k] = __builtin_elementwise_fma(alpha, e1, an1[k]);
-                    an2[k] = __builtin_elementwise_fma(alpha, e2, an2[k]);
+                    const f2 ndl = __builtin_elementwise_fma(
+                        splat2(w3.w), P.dLn2, __builtin_elementwise_fma(splat2(w3.z), P.dLn1, splat2(w3.y) * P.dLn0));
+                    const f2 e = ndl - sn[k];
+                    dL_dopa += e;
+                    sn[k] = __builtin_elementwise_fma(alpha, e, sn[k]);
                     const f2 n0 = bw * P.dLn0, n1 = bw * P.dLn1, n2 = bw * P.dLn2;
                     Fn0 = k ? Fn0 + n0 : n0;
                     Fn1 = k ? Fn1 + n1 : n1;
@@ -383,11 +388,14 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
                     dL_ddelx = __builtin_elementwise_fma(dL_dt, splat2(w1.z), dL_ddelx);
                     dL_ddely = __builtin_elementwise_fma(dL_dt, splat2(w1.w), dL_ddely);
                 }
-                const f2 mx = dL_ddelx * ddelx_dx, my = dL_ddely * ddely_dy;
-                fabs_sum += (fabsf(mx.x) + fabsf(my.x)) + (fabsf(mx.y) + fabsf(my.y));
+                // (the NDC scale W/2, H/2 of dL/dmean2D applied to the sums; |.| per pixel, scaled)
+                fabs_sum = __builtin_fmaf(fabsf(dL_ddelx.x), ddelx_dx, fabs_sum);
+                fabs_sum = __builtin_fmaf(fabsf(dL_ddely.x), ddely_dy, fabs_sum);
+                fabs_sum = __builtin_fmaf(fabsf(dL_ddelx.y), ddelx_dx, fabs_sum);
+                fabs_sum = __builtin_fmaf(fabsf(dL_ddely.y), ddely_dy, fabs_sum);
                 const f2 qdy = q * dy[k], qdy2 = qdy * dy[k];
-                Fmx = k ? Fmx + mx : mx;
-                Fmy = k ? Fmy + my : my;
+                Fmx = k ? Fmx + dL_ddelx : dL_ddelx;
+                Fmy = k ? Fmy + dL_ddely : dL_ddely;
                 Fq = k ? Fq + q : q;
                 Fqdy = k ? Fqdy + qdy : qdy;
                 Fqdy2 = k ? Fqdy2 + qdy2 : qdy2;
@@ -397,8 +405,8 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
             f[kAccColor + 0] = hsum(Fc0);
             f[kAccColor + 1] = hsum(Fc1);
             f[kAccColor + 2] = hsum(Fc2);
-            f[kAccMean2D + 0] = hsum(Fmx);
-            f[kAccMean2D + 1] = hsum(Fmy);
+            f[kAccMean2D + 0] = hsum(Fmx) * ddelx_dx;
+            f[kAccMean2D + 1] = hsum(Fmy) * ddely_dy;
             f[kAccConic + 0] = hsum(Fq) * (-0.5f * dx * dx);
             f[kAccConic + 1] = hsum(Fqdy) * (-0.5f * dx);
             f[kAccConic + 2] = -0.5f * hsum(Fqdy2);
@@ -457,7 +465,6 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.dL_dnormal = b.dL_dnormal;
     a.acc = ws.acc;
     a.acc_abs = ws.acc_abs;
-    a.skip_prepass = option(kOptBwdNoPrepass);
     a.no_cache = option(kOptBwdNoCache);
     a.tile_order = ws.tile_order;
     if (a.num_tiles == 0) return hipSuccess;

@@ -67,7 +67,7 @@ struct RenderFwdArgs {
     float* out_alpha;
     float* out_normal;
     float* out_mdepth;
-    int passes;  // bisection passes (kSplitIterations; fewer only for GSR_OPT_BISECT_PASSES timing runs)
+    int passes;  // bisection passes (kSplitIterations; evaluate_sdf: kSplitIterations + 1)
     int refine;  // root refinement after pass 2 (GSR_OPT_NO_REFINE = 0 for the reference's passes only)
     float sample_range;  // half-width of the first bisection window (kSampleRange; 2 kSampleRange for evaluate_sdf)
     // SAMPLE mode (sample_depth, sample.hip): a workgroup is one chunk of
@@ -1153,11 +1153,7 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.out_mdepth = out_mdepth;
     a.sample_range = kSampleRange;
     a.refine = option(kOptNoRefine) ? 0 : 1;
-    {
-        const int np = option(kOptBisectPasses);
-        a.passes = (np > 0 && np < kSplitIterations) ? np : kSplitIterations;
-        if (np < 0) a.passes = 0;
-    }
+    a.passes = kSplitIterations;
     if (a.num_tiles == 0) return hipSuccess;
     if (p.require_depth) {
         if (option(kOptRenderStats))

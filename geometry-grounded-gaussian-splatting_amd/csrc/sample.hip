@@ -200,7 +200,6 @@ struct SampleBwdArgs {
     uint32_t num_tiles;
     float focal_x, focal_y;
     float* acc;  // [P][16] (gsr_common.h AccField): mean2D, conic, ray-plane
-    int diag;    // diagnostic timing switches (GSR_OPT_BWD_NO_PREPASS: bit 0 no pre-pass, bit 1 no reduction)
     const uint32_t* chunk_order;  // launch order of the chunks (heaviest first) or null
 };
 
@@ -275,7 +274,7 @@ __global__ void __launch_bounds__(256) sample_bwd_kernel(SampleBwdArgs a) {
 
     // pre-pass dT/dt_m (sample_backward.cu:170-215) unless the forward cached it
     {
-        const bool need = on && !cached && !(a.diag & 1);
+        const bool need = on && !cached;
         const uint32_t wave_last = wave_max_u(need ? last : 0u);
         const bool block_needs = __syncthreads_or(wave_last != 0u);
         uint32_t c = 0;
@@ -358,10 +357,6 @@ __global__ void __launch_bounds__(256) sample_bwd_kernel(SampleBwdArgs a) {
                 f[kAccPlane + 2] = dL_dt;
                 f[kAccPlane + 3] = dL_drsig;
             }
-            if (a.diag & 2) {
-                if (f[kAccConic + 3] == 12345.f) a.acc[0] = 1.f;  // keep the math alive
-                continue;
-            }
             const float red = wave_transpose_reduce16(f);
             // lanes 4k hold field k; colour (0-2) and normal (9-11) are zero here
             const int field = lane >> 2;
@@ -422,7 +417,6 @@ hipError_t launch_sample_bwd(const SampleBwdParams& b, const GeomState& gs, cons
     a.focal_x = p.focal_x;
     a.focal_y = p.focal_y;
     a.acc = ws.acc;
-    a.diag = option(kOptBwdNoPrepass);
     a.chunk_order = ws.tile_order;
     const uint32_t bound = sample_chunk_bound(b.PN, tiles);
     hipLaunchKernelGGL(sample_bwd_kernel, dim3(bound), dim3(kTilePixels), 0, stream, a);

@@ -100,6 +100,7 @@ def _load():
     L.gsr_set_option.argtypes = [i, i]
     L.gsr_debug_binning.argtypes = [vp, vp, i, i, i, vp, vp, vp]
     L.gsr_debug_image.argtypes = [vp, i, i, vp, vp]
+    L.gsr_debug_tile_stats.argtypes = [vp, i, i, vp, vp]
     L.gsr_debug_sample_points.argtypes = [vp, i, vp, vp, vp]
     L.gsr_debug_render_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i]
     L.gsr_timing_enable.argtypes = [i]
@@ -122,11 +123,8 @@ NUM_STAGES = 14
 # carve_bwd layout: 256-B aligned base, float acc[P][16], then float acc_abs[P])
 KEEP_BWD_SCRATCH = False
 last_bwd_scratch = None
-# (ids 0, 7, 8: retired A/B variants, rejected by gsr_set_option)
+# (ids 0, 2-4, 7, 8: retired variants and diagnostics, rejected by gsr_set_option)
 OPT_RENDER_STATS = 1
-OPT_BISECT_PASSES = 2
-OPT_BWD_NO_PREPASS = 3
-OPT_NO_TILE_ORDER = 4
 OPT_NO_REFINE = 5
 OPT_BWD_NO_CACHE = 6
 OPT_ROCPRIM_DSORT = 9
@@ -177,6 +175,20 @@ def debug_n_contrib(imgBuffer, image_height: int, image_width: int):
     stream = torch.cuda.current_stream(imgBuffer.device).cuda_stream
     _check(_load().gsr_debug_image(ctypes.c_void_p(imgBuffer.data_ptr()), int(image_width), int(image_height),
                                    out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream)))
+    return out
+
+
+def debug_max_contrib(tileBuffer, image_height: int, image_width: int):
+    """Per-tile max contributor [tiles] uint32 of a forward's tile buffer
+    (gsr_debug_tile_stats): how far into each culled tile list the forward's
+    pixels blended, the range the backward walks."""
+    import numpy as np
+
+    tiles = ((image_width + 15) // 16) * ((image_height + 15) // 16)
+    out = np.zeros(tiles, np.uint32)
+    stream = torch.cuda.current_stream(tileBuffer.device).cuda_stream
+    _check(_load().gsr_debug_tile_stats(ctypes.c_void_p(tileBuffer.data_ptr()), int(image_width), int(image_height),
+                                        out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream)))
     return out
 
 

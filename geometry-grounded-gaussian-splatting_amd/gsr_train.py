@@ -1,0 +1,300 @@
+"""One training iteration of the reference after the regularisation kick-in
+(train.py:142-262, iteration >= regularization_from_iter = 7000), on the HIP
+kernels of this package: the end-to-end variant of SURVEY §8(d).
+
+Per iteration, in the reference's order:
+  getters (gaussian_model.py:146-212, torch)  -> render() with require_depth
+  (gaussian_renderer.render -> GaussianRasterizer, render_fwd.hip)
+  -> L1 (loss_utils.py:28-29; app_model NO)  -> depth_to_normal + normal loss
+  (train.py:171-176; depth_normal.hip)  -> PatchMatch (loss_utils.py:140-267:
+  the median-depth points re-observed from the nearest camera through
+  sample_depth (sample.hip), the geometric loss, warp_patch_ncc (ncc.hip) on
+  the consistent pixels)  -> fused SSIM (ssim.hip)  -> loss.backward()
+  (render_bwd / preprocess_bwd / sample_bwd ...)  -> densification statistics
+  (train.py:236-237, optim.hip)  -> Adam step + zero_grad (train.py:262-263,
+  FusedAdam, optim.hip).
+Out of the step, as in the reference's steady state: densify/prune (every 100
+iterations until 15000), the 3D filter recomputation and logging.
+
+The torch glue between the kernels (loss arithmetic, the PatchMatch
+projections and masks) is the reference's own torch code restated; the hot
+ops are the package's HIP kernels.  Synthetic data (no datasets here): the
+ground-truth images are renders of a perturbed copy of the Gaussians.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+import gsr_scene as S
+from fused_ssim import fused_ssim
+from gaussian_renderer import render, sample_depth
+from gsr_geometry import depth_to_normal
+from gsr_optim import FusedAdam, add_densification_stats
+import warp_patch_ncc
+
+
+@dataclass
+class TrainView:
+    """The attributes of scene/cameras.py::Camera a training iteration reads
+    (R, T in the reference's convention: world_view_transform = [R^T | T]^T)."""
+
+    image_width: int
+    image_height: int
+    FoVx: float
+    FoVy: float
+    world_view_transform: torch.Tensor
+    full_proj_transform: torch.Tensor
+    camera_center: torch.Tensor
+    R: torch.Tensor
+    T: torch.Tensor
+    Fx: float
+    Fy: float
+    Cx: float
+    Cy: float
+    original_image: torch.Tensor | None = None
+    gray_image: torch.Tensor | None = None
+
+
+def train_view(W: int, H: int, R: np.ndarray, T: np.ndarray, device) -> TrainView:
+    c = S.make_camera(W, H, R, T).to(device)
+    Fx = W / (2 * math.tan(c.FoVx / 2.0))
+    Fy = H / (2 * math.tan(c.FoVy / 2.0))
+    return TrainView(W, H, c.FoVx, c.FoVy, c.world_view_transform, c.full_proj_transform, c.camera_center,
+                     torch.tensor(R, dtype=torch.float32, device=device), torch.tensor(T, dtype=torch.float32,
+                                                                                        device=device),
+                     Fx, Fy, float(W - 1) / 2, float(H - 1) / 2)
+
+
+def orbit_views(n: int, W: int, H: int, device, center_z: float = 6.0, max_deg: float = 20.0):
+    """C4's orbit (gsr_scene.orbit_cameras) as training views."""
+    views = []
+    c = np.array([0.0, 0.0, center_z])
+    for a in (np.linspace(-max_deg, max_deg, n) if n > 1 else np.zeros(1)):
+        th = math.radians(float(a))
+        Rc = np.array([[math.cos(th), 0, math.sin(th)], [0, 1, 0], [-math.sin(th), 0, math.cos(th)]])
+        pos = c - Rc @ np.array([0.0, 0.0, center_z])
+        views.append(train_view(W, H, Rc, -Rc.T @ pos, device))
+    return views
+
+
+class TrainGaussians(torch.nn.Module):
+    """GaussianModel's trained state (gaussian_model.py): raw parameters,
+    the 3D filter, Adam (FusedAdam with the reference's parameter groups and
+    eps = 1e-15, gaussian_model.py:342-351) and the densification statistics."""
+
+    def __init__(self, raw: S.RawGaussians, spatial_lr_scale: float = 1.0, sh_degree: int = 3, sg_degree: int = 0):
+        super().__init__()
+        P = lambda t: torch.nn.Parameter(t.detach().clone().contiguous())  # noqa: E731
+        self._xyz, self._features_dc, self._features_rest = P(raw.xyz), P(raw.features_dc), P(raw.features_rest)
+        self._scaling, self._rotation, self._opacity = P(raw.scaling), P(raw.rotation), P(raw.opacity)
+        self._sg_axis, self._sg_sharpness, self._sg_color = P(raw.sg_axis), P(raw.sg_sharpness), P(raw.sg_color)
+        self.register_buffer("filter_3D", raw.filter_3D.detach().clone())
+        self.active_sh_degree, self.active_sg_degree = sh_degree, sg_degree
+        n = raw.xyz.shape[0]
+        dev = raw.xyz.device
+        self.max_radii2D = torch.zeros(n, device=dev)
+        self.xyz_gradient_accum = torch.zeros(n, 1, device=dev)
+        self.xyz_gradient_accum_abs = torch.zeros(n, 1, device=dev)
+        self.denom = torch.zeros(n, 1, device=dev)
+        # OptimizationParams defaults (arguments/__init__.py:85-99)
+        groups = [("xyz", self._xyz, 0.00016 * spatial_lr_scale), ("f_dc", self._features_dc, 0.0013),
+                  ("f_rest", self._features_rest, 0.00011), ("opacity", self._opacity, 0.05),
+                  ("scaling", self._scaling, 0.005), ("rotation", self._rotation, 0.001)]
+        if raw.sg_color.shape[1]:
+            groups += [("sg_axis", self._sg_axis, 0.002), ("sg_sharpness", self._sg_sharpness, 0.095),
+                       ("sg_color", self._sg_color, 0.00064)]
+        self.optimizer = FusedAdam([{"params": [p], "lr": lr, "name": nm} for nm, p, lr in groups], lr=0.0,
+                                   eps=1e-15)
+
+    # ---- getters (gaussian_model.py:146-212) ----
+    @property
+    def get_xyz(self):
+        return self._xyz
+
+    @property
+    def get_scaling(self):
+        return torch.exp(self._scaling)
+
+    @property
+    def get_scaling_with_3D_filter(self):
+        return torch.sqrt(torch.square(self.get_scaling) + torch.square(self.filter_3D))
+
+    @property
+    def get_opacity_with_3D_filter(self):
+        sq = torch.square(self.get_scaling)
+        coef = torch.sqrt(sq.prod(dim=1) / (sq + torch.square(self.filter_3D)).prod(dim=1))
+        return torch.sigmoid(self._opacity) * coef[..., None]
+
+    @property
+    def get_scaling_n_opacity_with_3D_filter(self):
+        sq = torch.square(self.get_scaling)
+        after = sq + torch.square(self.filter_3D)
+        coef = sq.prod(dim=1).sqrt() * after.prod(dim=1).rsqrt()
+        return after.sqrt(), torch.sigmoid(self._opacity) * coef[..., None]
+
+    @property
+    def get_rotation(self):
+        return F.normalize(self._rotation)
+
+    @property
+    def get_features(self):
+        return torch.cat((self._features_dc, self._features_rest), dim=1)
+
+    @property
+    def get_sg_axis(self):
+        return F.normalize(self._sg_axis, dim=2)
+
+    @property
+    def get_sg_sharpness(self):
+        return F.softplus(self._sg_sharpness)
+
+    @property
+    def get_sg_color(self):
+        return self._sg_color
+
+
+class _Pipe:
+    debug = False
+    compute_cov3D_python = False
+
+
+# loss weights and PatchMatch settings (arguments/__init__.py:106-118)
+LAMBDA_DSSIM, LAMBDA_DEPTH_NORMAL, LAMBDA_NCC, LAMBDA_GEO = 0.2, 0.05, 0.6, 0.02
+PATCH_SIZE, PIXEL_NOISE_TH = 3, 1.0
+
+
+def patchmatch(gaussians, render_pkg, view, nearest, depth_normal, kernel_size, pipe):
+    """PatchMatch.__call__ (utils/loss_utils.py:140-267) without its debug
+    image dumps: the median-depth points of `view` re-observed from `nearest`
+    (sample_depth), the pixel-reprojection geometric loss, and the multi-view
+    NCC of 7x7 half-step patches (warp_patch_ncc) at the consistent pixels."""
+    H, W = view.image_height, view.image_width
+    dev = render_pkg["median_depth"].device
+    with torch.no_grad():
+        ix = (torch.arange(W, device=dev, dtype=torch.float32) - view.Cx) / view.Fx
+        iy = (torch.arange(H, device=dev, dtype=torch.float32) - view.Cy) / view.Fy
+        view_to_nearest_T = (-view.world_view_transform[:3, :3].T @ nearest.R @ nearest.T
+                             + view.world_view_transform[3, :3])
+        nearest_to_view_R = nearest.R.transpose(1, 0) @ view.world_view_transform[:3, :3]
+    depth_reshape = render_pkg["median_depth"].squeeze().unsqueeze(-1)
+    pts = torch.cat([depth_reshape * ix[None, :, None], depth_reshape * iy[:, None, None], depth_reshape], dim=-1)
+    pts = (pts - view.T) @ view.R.T
+    sampled = sample_depth(pts, nearest, gaussians, pipe, kernel_size)
+    pts_in_nearest = sampled["sampled_depth"]
+    pts_in_view = view_to_nearest_T + pts_in_nearest @ nearest_to_view_R
+    proj = pts_in_view[..., :2] / torch.clamp_min(pts_in_view[..., 2:], 1e-7)
+    proj = torch.addcmul(proj.new_tensor([view.Cx, view.Cy]), proj.new_tensor([view.Fx, view.Fy]), proj)
+    gx, gy = torch.meshgrid(torch.arange(W, device=dev, dtype=torch.int32),
+                            torch.arange(H, device=dev, dtype=torch.int32), indexing="xy")
+    pixels = torch.stack([gx, gy], dim=-1)
+    pixel_noise = torch.pairwise_distance(proj, pixels.float())
+    with torch.no_grad():
+        d_mask = (sampled["inside"] & (pts_in_nearest[..., -1] > 0.2) & (pts_in_view[..., -1] > 0.2)
+                  & (pixel_noise < PIXEL_NOISE_TH) & (render_pkg["median_depth"].squeeze() > 0))
+        weights = torch.exp(-pixel_noise)
+        weights[~d_mask] = 0
+    geo_loss = ((weights * pixel_noise)[d_mask]).mean()
+    with torch.no_grad():
+        d_flat = torch.flatten(d_mask)
+        valid = torch.argwhere(d_flat).squeeze(1)
+        w_sel = torch.flatten(weights)[valid]
+        px = torch.index_select(pixels.view(-1, 2), dim=0, index=valid)
+        r_rel = nearest.world_view_transform[:3, :3].transpose(-1, -2) @ view.world_view_transform[:3, :3]
+        t_rel = -r_rel @ view.world_view_transform[3, :3] + nearest.world_view_transform[3, :3]
+    depth_sel = torch.index_select(render_pkg["median_depth"].view(-1), dim=0, index=valid)
+    normal_sel = F.normalize(torch.index_select(render_pkg["normal"].view(3, -1), dim=1, index=valid).T, dim=-1)
+    cc, valid_mask = warp_patch_ncc.warp_patch_ncc(
+        depth_sel, normal_sel, px, r_rel.T, t_rel, view.gray_image.squeeze(), nearest.gray_image.squeeze(),
+        view.Fx, view.Fy, view.Cx, view.Cy, nearest.Fx, nearest.Fy, nearest.Cx, nearest.Cy, False)
+    ncc = torch.clamp(1 - cc, 0.0, 2.0)
+    ncc_mask = (ncc < 0.9) & valid_mask
+    ncc = (ncc.squeeze() * w_sel)[ncc_mask.squeeze()]
+    # (the reference returns 0 when no pixel qualifies; the mean of an empty set is NaN)
+    ncc_loss = ncc.mean() if ncc.numel() else ncc.new_zeros(())
+    return ncc_loss, geo_loss
+
+
+class TrainStep:
+    """The iteration; `step(view, nearest)` runs it, `stamps` (when timing)
+    holds CUDA events at the component boundaries of the last call."""
+
+    COMPONENTS = ("render", "depth_normal", "patchmatch", "rgb_loss", "backward", "densify_stats", "adam")
+
+    def __init__(self, gaussians: TrainGaussians, kernel_size: float = 0.0, bg=None, densify: bool = True):
+        self.g = gaussians
+        self.kernel_size = kernel_size
+        dev = gaussians._xyz.device
+        self.bg = torch.zeros(3, device=dev) if bg is None else bg
+        self.pipe = _Pipe()
+        self.densify = densify
+        self.timing = False
+        self.stamps = []
+
+    def _mark(self):
+        if self.timing:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.stamps.append(e)
+
+    def step(self, view: TrainView, nearest: TrainView) -> torch.Tensor:
+        g = self.g
+        self.stamps = []
+        self._mark()
+        pkg = render(view, g, self.pipe, self.bg, self.kernel_size, require_depth=True)
+        image = pkg["render"]
+        self._mark()
+        depth_normal, valid_points = depth_to_normal(view, pkg["median_depth"])
+        err = 1 - torch.linalg.vecdot(pkg["normal"], depth_normal, dim=0)
+        normal_loss = torch.where(valid_points.squeeze(), err, torch.zeros_like(err)).mean()
+        self._mark()
+        ncc_loss, geo_loss = patchmatch(g, pkg, view, nearest, depth_normal, self.kernel_size, self.pipe)
+        self._mark()
+        gt = view.original_image
+        l1 = torch.abs(image - gt).mean()
+        rgb_loss = (1.0 - LAMBDA_DSSIM) * l1 + LAMBDA_DSSIM * (1.0 - fused_ssim(image.unsqueeze(0), gt.unsqueeze(0),
+                                                                                 padding="valid"))
+        loss = rgb_loss + LAMBDA_DEPTH_NORMAL * normal_loss + LAMBDA_NCC * ncc_loss + LAMBDA_GEO * geo_loss
+        self._mark()
+        loss.backward()
+        self._mark()
+        with torch.no_grad():
+            if self.densify:  # train.py:236-237 (iterations < densify_until_iter)
+                add_densification_stats(g, pkg["viewspace_points"], pkg["radii"])
+            self._mark()
+            g.optimizer.step()
+            g.optimizer.zero_grad(set_to_none=True)
+        self._mark()
+        return loss.detach()
+
+    def component_ms(self) -> dict:
+        """Milliseconds per component of the last timed step (synchronises)."""
+        torch.cuda.synchronize()
+        e = self.stamps
+        return {name: e[k].elapsed_time(e[k + 1]) for k, name in enumerate(self.COMPONENTS)}
+
+
+def synthetic_training_setup(P: int, W: int, H: int, sh_degree: int = 3, sg_degree: int = 0, device="cuda",
+                             seed: int = 0):
+    """(TrainStep, view, nearest view): the bench scene's Gaussians as the
+    trained state, two orbit views 5.7 degrees apart, and ground-truth images
+    rendered from a copy of the Gaussians with perturbed colours and positions."""
+    raw = S.make_gaussians(P, sh_degree=sh_degree, sg_degree=sg_degree, seed=seed, aspect=H / W).to(device)
+    views = orbit_views(8, W, H, device)
+    view, nearest = views[3], views[4]
+    gen = torch.Generator(device="cpu").manual_seed(seed + 1)
+    gt_raw = S.RawGaussians(*[getattr(raw, f).clone() for f in raw.__dataclass_fields__])
+    gt_raw.features_dc += (torch.randn(gt_raw.features_dc.shape, generator=gen) * 0.1).to(device)
+    gt_raw.xyz += (torch.randn(gt_raw.xyz.shape, generator=gen) * 0.01).to(device)
+    gt = TrainGaussians(gt_raw, sh_degree=sh_degree, sg_degree=sg_degree)
+    with torch.no_grad():
+        for v in (view, nearest):
+            img = render(v, gt, _Pipe(), torch.zeros(3, device=device), 0.0, require_depth=False)["render"]
+            v.original_image = img.clamp(0.0, 1.0).contiguous()
+            v.gray_image = (0.299 * img[0] + 0.587 * img[1] + 0.114 * img[2])[None].contiguous()
+    del gt
+    return TrainStep(TrainGaussians(raw, sh_degree=sh_degree, sg_degree=sg_degree)), view, nearest

@@ -430,18 +430,14 @@ int gsr_timing_collect(double* ms, int* launches);
 const char* gsr_stage_name(int stage);
 
 /*
- * Process-wide switches selecting A/B variants of a kernel, for measuring one
- * against the other in the same process (all variants but GSR_OPT_NO_REFINE
- * give bit-identical results), and diagnostics.  Ids 0, 7 and 8 belonged to
- * retired variants (a bisection shortcut, per-tile sort binning and a two-wave
- * backward layout, all measured slower) and are rejected with GSR_ERR_ARGS.
+ * Process-wide switches selecting the alternative kernel paths the parity
+ * tests use as references for the default ones (all but GSR_OPT_NO_REFINE
+ * give bit-identical results) and the forward's diagnostic counters.  Ids 0,
+ * 2-4, 7 and 8 belonged to retired variants and diagnostics (a bisection
+ * shortcut, bisection-pass and pre-pass timing switches, an unordered tile
+ * launch, per-tile sort binning, a two-wave backward layout) and are rejected
+ * with GSR_ERR_ARGS.
  */
-/* GSR_OPT_BISECT_PASSES (diagnostic, default 0 = all 5): run only n median-depth
- * bisection passes (n < 0: none) to time them; median depth is then wrong. */
-/* GSR_OPT_NO_TILE_ORDER (A/B, default 0): launch the per-tile raster kernels in
- * XCD-contiguous tile order instead of heaviest-tile-first (backward). */
-/* GSR_OPT_BWD_NO_PREPASS (diagnostic): skip the backward's median-depth pre-pass
- * (its gradient terms are then wrong), to time it. */
 /* GSR_OPT_BWD_NO_CACHE (A/B, default 0): the backward recomputes dT/dt_m at every
  * pixel in its pre-pass (render_backward.cu:835-880) instead of taking the
  * forward's cached value. */
@@ -455,9 +451,6 @@ const char* gsr_stage_name(int stage);
  * refinement (render_fwd.hip; results agree to ~1e-7 of the depth, not bitwise). */
 enum gsr_option {
     GSR_OPT_RENDER_STATS = 1,
-    GSR_OPT_BISECT_PASSES = 2,
-    GSR_OPT_BWD_NO_PREPASS = 3,
-    GSR_OPT_NO_TILE_ORDER = 4,
     GSR_OPT_NO_REFINE = 5,
     GSR_OPT_BWD_NO_CACHE = 6,
     GSR_OPT_ROCPRIM_DSORT = 9,
@@ -491,6 +484,14 @@ int gsr_debug_image(const void* image_buffer, int width, int height, uint32_t* n
  */
 int gsr_debug_sample_points(const void* point_buffer, int PN, float* median_depth_out, uint32_t* last_out,
                             void* stream);
+
+/*
+ * Introspection of a forward's tile buffer (test / measurement hook): the
+ * per-tile max contributor (the last list position any pixel of the tile
+ * blended, 1-based; the backward walks each tile's list up to it), one
+ * uint32 per tile; synchronises `stream`.
+ */
+int gsr_debug_tile_stats(const void* tile_buffer, int width, int height, uint32_t* max_contrib_out, void* stream);
 
 /* Human-readable message for the last non-OK status on this thread. */
 const char* gsr_last_error(void);

@@ -229,14 +229,16 @@ def test_library_exports_header_symbols():
 
 
 def test_retired_options_are_rejected():
-    """Option ids 0, 7, 8 (retired A/B variants) and out-of-range ids fail
-    loudly instead of being silently ignored (host-only call, no GPU)."""
+    """Option ids 0, 2-4, 7, 8 (retired variants and diagnostics) and
+    out-of-range ids fail loudly instead of being silently ignored (host-only
+    call, no GPU); the test-oracle paths remain."""
     from diff_gaussian_rasterization import _C
 
-    for opt in (0, 7, 8, 11, -1):
+    for opt in (0, 2, 3, 4, 7, 8, 11, -1):
         with pytest.raises(RuntimeError, match="unknown option"):
             _C.set_option(opt, 1)
-    _C.set_option(_C.OPT_NO_TILE_ORDER, 0)
+    for opt in (_C.OPT_RENDER_STATS, _C.OPT_NO_REFINE, _C.OPT_BWD_NO_CACHE, _C.OPT_ROCPRIM_DSORT, _C.OPT_PBWD_STAGE):
+        _C.set_option(opt, 0)
 
 
 def test_library_targets_gfx950():

@@ -2,7 +2,7 @@
 # rocprofv3 passes for bench.py (run on the GPU box from the repo root):
 #   1. kernel trace + stats  2. --pmc FETCH_SIZE  3. --pmc WRITE_SIZE
 #   4. --pmc SQ VALU instruction mix (all, transcendental, FMA/ADD/MUL f32, int32) and VALU cycles
-#   4b. --pmc SQ wave/wait/busy cycles, SALU / LDS / CVT instructions
+#   4b. --pmc SQ wave / wait cycles, SALU / LDS instructions, LDS-array cycles and bank conflicts
 #   5. --pmc L2 requests / busy / tag stalls / hits   6. --pmc TA busy
 #   7. kernel trace + stats of tools/bench_sample.py (sample_depth kernels; default workload only)
 # (counters in their own passes; never combined with other trace domains).
@@ -23,7 +23,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $SHORT > $OUT/fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $SHORT > $OUT/write.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- python3 $SHORT > $OUT/sq.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq2 -o run -- python3 $SHORT > $OUT/sq2.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq2 -o run -- python3 $SHORT > $OUT/sq2.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc TCC_REQ_sum TCC_BUSY_avr TCC_TAG_STALL_sum TCC_HIT_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/tcc -o run -- python3 $SHORT > $OUT/tcc.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc TA_BUSY_avr TA_TA_BUSY_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/ta -o run -- python3 $SHORT > $OUT/ta.log 2>&1 && \
 if [ -z "$WL" ]; then timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sample -o run -- python3 $ROOT/tools/bench_sample.py 10 > $OUT/sample.log 2>&1; fi
