@@ -211,6 +211,7 @@ size_t carve_tiles(void* base, int T, TileState& s) {
     s.ranges = c.take<uint2>(T);
     s.max_contrib = c.take<uint32_t>(T);
     s.order = c.take<uint32_t>(T);
+    s.blend_mask = c.take<uint32_t>((size_t)T * kBlendWords);
     return c.off + 256;
 }
 

@@ -114,10 +114,17 @@ struct ImageState {
     uint32_t* md_check;  // bits of the mdepth output it belongs to (NaN pattern: not cached)
 };
 constexpr uint32_t kNoCache = 0x7fffffffu;
+// The first kBlendWords * 32 entries of a tile's list: bit set where at least
+// one pixel of the tile blended the entry in the forward composite (render_fwd).
+// For an entry before a pixel's last contributor, "blended" is exactly the
+// backward's per-pixel validity (power <= 0, alpha >= 1/255 with the same
+// rounding), so the backward skips the unset entries without evaluating them.
+constexpr int kBlendWords = 8;
 struct TileState {
     uint2* ranges;
     uint32_t* max_contrib;
-    uint32_t* order;  // launch order of the tiles, heaviest first (tile_order_kernel)
+    uint32_t* order;       // launch order of the tiles, heaviest first (tile_order_kernel)
+    uint32_t* blend_mask;  // [T][kBlendWords]
 };
 // ---- sample_depth state (PointState / DuplicatedTileState, rasterizer_impl.h) ----
 constexpr uint32_t kNoTile = 0xffffffffu;

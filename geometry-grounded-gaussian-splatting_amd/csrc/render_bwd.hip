@@ -26,6 +26,7 @@ struct RenderBwdArgs {
     const float* dT_dtm;
     const uint32_t* md_check;
     const uint32_t* max_contrib;
+    const uint32_t* blend_mask;  // [tiles][kBlendWords]: entries some pixel blended in the forward
     int W, H;
     uint32_t grid_x, num_tiles;
     float focal_x, focal_y;
@@ -149,6 +150,7 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
     constexpr int kThreads = 128 / NP;
     __shared__ float4 s_w0[kBwdBatch], s_w1[kBwdBatch], s_w2[kBwdBatch], s_w3[kBwdBatch];
     __shared__ uint32_t s_id[kBwdBatch];
+    __shared__ uint32_t s_bm[kBlendWords];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -260,31 +262,44 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
         sc[k] = sn[k] = zero;
     }
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
+    // the entries no pixel of the tile blended in the forward: skipped without evaluation (entries past the
+    // mask's kBlendWords * 32 are all walked)
+    if (tid < kBlendWords) s_bm[tid] = a.blend_mask[(size_t)tile * kBlendWords + tid];
+    __syncthreads();
+    auto needed = [&](int e) { return e >= kBlendWords * 32 || ((s_bm[e >> 5] >> (e & 31)) & 1u) != 0u; };
     int toDo = max_contrib;
+    static_assert(kBwdBatch == 128 && kThreads == 64, "one wave stages a 128-record batch, two ballots");
     for (int i = 0; i < rounds; i++, toDo -= kBwdBatch) {
+        // this batch's entries (back to front: slot k holds entry max_contrib - 1 - (i * kBwdBatch + k))
+        const int c0 = i * kBwdBatch + tid, c1 = c0 + kThreads;
+        const bool need0 = c0 < max_contrib && needed(max_contrib - 1 - c0);
+        const bool need1 = c1 < max_contrib && needed(max_contrib - 1 - c1);
+        unsigned long long m0 = __ballot(need0), m1 = __ballot(need1);
+        if ((m0 | m1) == 0ull) continue;  // (wave-uniform: one wave per tile)
         __syncthreads();
         {
-            // every list entry of the batch, then every record, requested before
+            // every needed list entry of the batch, then every record, requested before
             // any is stored (left to itself the compiler waited on each of the
             // four record loads in turn, reusing one register quad)
             constexpr int kPer = kBwdBatch / kThreads;
+            const bool need[kPer] = {need0, need1};
             uint32_t g[kPer];
 #pragma unroll
             for (int u = 0; u < kPer; u++) {
                 const int c = i * kBwdBatch + tid + u * kThreads;
-                g[u] = c < max_contrib ? a.point_list[range.x + max_contrib - c - 1] : 0u;
+                g[u] = need[u] ? a.point_list[range.x + max_contrib - c - 1] : 0u;
             }
             float4 r[kPer][4];
 #pragma unroll
             for (int u = 0; u < kPer; u++) {
                 const float4* sp = reinterpret_cast<const float4*>(a.splats + g[u]);
 #pragma unroll
-                for (int w = 0; w < 4; w++) r[u][w] = sp[w];
+                for (int w = 0; w < 4; w++) r[u][w] = need[u] ? sp[w] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
             for (int u = 0; u < kPer; u++) {
                 const int k = tid + u * kThreads;
-                if (i * kBwdBatch + k < max_contrib) {
+                if (need[u]) {
                     s_id[k] = g[u];
                     s_w0[k] = r[u][0];
                     s_w1[k] = r[u][1];
@@ -294,9 +309,16 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
             }
         }
         __syncthreads();
-        const int n = min(kBwdBatch, toDo);
-        for (int j = 0; j < n; j++) {
-            contributor--;
+        while ((m0 | m1) != 0ull) {
+            int j;
+            if (m0) {
+                j = __builtin_ctzll(m0);
+                m0 &= m0 - 1ull;
+            } else {
+                j = 64 + __builtin_ctzll(m1);
+                m1 &= m1 - 1ull;
+            }
+            contributor = (uint32_t)(max_contrib - 1 - (i * kBwdBatch + j));
             const float4 w0 = s_w0[j];
             const float4 w1 = s_w1[j];
             const float dx = w0.x - pixx;
@@ -449,6 +471,7 @@ hipError_t launch_render_bwd(const BwdParams& b, const GeomState& gs, const Binn
     a.dT_dtm = is.dT_dtm;
     a.md_check = is.md_check;
     a.max_contrib = ts.max_contrib;
+    a.blend_mask = ts.blend_mask;
     a.W = p.W;
     a.H = p.H;
     a.grid_x = p.grid_x;

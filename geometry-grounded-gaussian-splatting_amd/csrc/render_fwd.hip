@@ -34,6 +34,7 @@
 #include <algorithm>
 
 #include "gsr_kernels.h"
+#include "tiles.h"
 
 namespace gsr {
 
@@ -63,6 +64,7 @@ struct RenderFwdArgs {
     float* dT_dtm;
     uint32_t* md_check;
     uint32_t* max_contrib;
+    uint32_t* blend_mask;  // [tiles][kBlendWords] (render path)
     float* out_color;
     float* out_alpha;
     float* out_normal;
@@ -171,10 +173,18 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
 // (the slowest lane), max |refined - bisected| = 2.4e-7, no lane left to the
 // passes.  (The previous scheme ran the reference's first two passes and
 // refined from the pass-2 cell: one more 7-sample walk per contributor.)
-constexpr int kProbes = 11;
+#ifndef GSR_PROBES
+#define GSR_PROBES 11
+#endif
+constexpr int kProbes = GSR_PROBES;  // 11 or 7 (the window ends, m0 and 8 or 4 offsets around it)
+#if GSR_PROBES == 7
+__constant__ constexpr float kProbeOffsets[kProbes] = {0.f, -0.5f, -0.125f, 0.f, 0.125f, 0.5f, 0.f};
+#else
 __constant__ constexpr float kProbeOffsets[kProbes] = {0.f,    -0.5f,   -0.25f, -0.125f, -0.0625f, 0.f,
                                                         0.0625f, 0.125f, 0.25f,  0.5f,    0.f};
-constexpr uint32_t kPubRefined = 1u, kPubOut = 2u;  // phase results: root found / not in range
+#endif
+constexpr uint32_t kPubRefined = 1u, kPubOut = 2u, kPubIll = 4u;  // phase results: root found / not in range /
+                                                                   // root found, ill-conditioned (below)
 #ifndef GSR_REFINE_WALKS
 #define GSR_REFINE_WALKS 4
 #endif
@@ -204,6 +214,18 @@ constexpr float kTwoLn2 = 1.38629436111989061883f;
 #ifndef GSR_HNOISE
 #define GSR_HNOISE 1e-5f
 #endif
+// A converged root whose noise-induced uncertainty kHNoise / |H'| is above the
+// kCondTol bar but below kIllTol max(t, 1) (T flat near 1/2 between two
+// splats' peaks: C2 leaves 98k of 640k pixels so) is kept as the median depth
+// (within kIllTol of the reference's own noise-decided bisection answer) and
+// its dT/dt_m is computed exactly by the reference's pre-pass formula at that
+// depth in one more walk — instead of the reference's five passes plus that
+// walk.  (The continued H'' value refined lanes use would be off by ~kCurvTol^2
+// relative, which the implicit gradient's 1 / dT/dt_m amplifies at such pixels.)
+#ifndef GSR_ILL_ACCEPT
+#define GSR_ILL_ACCEPT 1
+#endif
+constexpr float kIllTol = 1e-5f;
 constexpr float kHNoise = GSR_HNOISE;  // rounding noise assumed in log2 T (~10x a 64-factor product's; 2e-6 measured: C2 render_fwd 0.763 -> 0.717 ms, but a small scene's dL/dmeans2D drifts to 1.3e-4 of the oracle through the implicit median-depth gradient)
 
 __device__ __forceinline__ void refine_step(float& A, float& B, float& D, float& E, float& F, float t, float alpha,
@@ -275,6 +297,38 @@ __device__ unsigned long long g_render_stats[8];
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
+// Strip culling of the composite (render path): a wave covers a 16 x 4 strip
+// of the tile, and a record whose alpha >= 1/255 region misses the strip (the
+// tile culling's exact ellipse test, tiles.h, on the strip's 4 pixel rows and
+// the tile's 16 columns) fails the power / alpha test at every pixel of it.
+// The staging thread computes the record's 4 strip bits; each wave then walks
+// only its records, the next index found by a scalar find-first-set over two
+// 64-bit ballots of the batch, so a skipped record costs no vector work.
+#ifndef GSR_STRIP_CULL
+#define GSR_STRIP_CULL 0
+#endif
+
+// Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
+// pixel rows [y0 + 4 s, y0 + 4 s + 3] x columns [x0, x0 + 15].
+__device__ __forceinline__ uint32_t strip_bits(const float4& w0, const float4& w1, int x0, int y0) {
+    const Ellipse E = make_ellipse(w0, w1, 0.f);
+    if (E.mode == 2) return 0u;
+    if (E.mode == 1) return 15u;
+    uint32_t bits = 0u;
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+        const float vlo = fmaxf(E.my - (float)(y0 + 4 * st + 3), -E.vmax);
+        const float vhi = fminf(E.my - (float)(y0 + 4 * st), E.vmax);
+        const float vu = fminf(fmaxf(-E.b * E.kst, vlo), vhi);
+        const float vl = fminf(fmaxf(E.b * E.kst, vlo), vhi);
+        const float umax = (-E.b * vu + sqrtf(fmaxf(E.a * E.tau - E.det * vu * vu, 0.f))) * E.ia;
+        const float umin = (-E.b * vl - sqrtf(fmaxf(E.a * E.tau - E.det * vl * vl, 0.f))) * E.ia;
+        // pixel centres x in [mx - umax, mx - umin] meet [x0, x0 + 15]
+        const bool hit = vlo <= vhi && E.mx - umax <= (float)(x0 + 15) && E.mx - umin >= (float)x0;
+        bits |= hit ? (1u << st) : 0u;
+    }
+    return bits;
+}
 template <bool GEOM, bool STATS = false, bool SAMPLE = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, 8))) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 128 x 16 B = 8 KB) aliased with the
@@ -284,6 +338,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     // blended contributors per pixel, word-major (word w of lane t at w * 256 + t: conflict-free)
     __shared__ uint32_t s_mask[GEOM ? kTilePixels * kMaskWords : 1];
     __shared__ int s_alive[2][4];
+    constexpr bool kStrip = GSR_STRIP_CULL && !SAMPLE;
+    __shared__ uint8_t s_strip[kStrip ? kBatch : 1];
+    __shared__ uint32_t s_union[kBlendWords];  // (render path) entries some pixel of the tile blended
     __shared__ uint32_t s_max[4];
     // (render path, GEOM) the median-depth phases: per pixel the composite's last contributor,
     // m0 and T, then the worker's result (flags, md_out, dT/dt_m); the grid pixels' roots
@@ -345,6 +402,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         for (int q = 0; q < kMaskWords; q++) my_mask[q * kTilePixels] = 0u;
     }
 
+    if constexpr (!SAMPLE) {
+        if (tid < kBlendWords) s_union[tid] = 0u;  // (ordered by the first batch's barrier)
+    }
     float T = 1.0f, T_pt = 1.0f;
     uint32_t last = 0;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
@@ -377,6 +437,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             if ((tid & 63) == __builtin_ctzll(m)) cst[1] += __popcll(m);
         }
         const float aT = alpha * T;
+        if constexpr (!SAMPLE && !GEOM) {  // (GEOM: from the blended-set masks after the composite)
+            if (g < kBlendWords * 32) {
+                const unsigned long long m = __ballot(1);
+                if ((tid & 63) == __builtin_ctzll(m)) atomicOr(&s_union[g >> 5], 1u << (g & 31));
+            }
+        }
         const float4 w2 = w2f();
         if constexpr (SAMPLE && !GEOM) {
             // vacancy transmittance at the point (sample_forward.cu:152-160)
@@ -423,18 +489,48 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         const int k = i * kBatch + tid;
         if (tid < kBatch && k < total) {
             const Splat* sp = a.splats + a.point_list[range.x + k];
-            s_w0[tid] = sp->w0;
-            s_w1[tid] = sp->w1;
+            const float4 w0 = sp->w0, w1 = sp->w1;
+            s_w0[tid] = w0;
+            s_w1[tid] = w1;
             s_w2[tid] = sp->w2;
             if constexpr (!SAMPLE) s_w3[tid] = sp->w3;
+            if constexpr (kStrip) s_strip[tid] = (uint8_t)strip_bits(w0, w1, px - (tid & 15), py - (tid >> 4));
         }
         __syncthreads();
         const int n = min(kBatch, toDo);
-        for (int j = 0; !done && j < n; j++)
-            step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+        if constexpr (kStrip) {
+            // this wave's records of the batch, walked in list order by find-first-set
+            const int l = tid & 63;
+            unsigned long long m0 = __ballot(l < n && ((s_strip[l] >> wave) & 1u));
+            unsigned long long m1 = __ballot(64 + l < n && ((s_strip[64 + l] >> wave) & 1u));
+            while (!done && (m0 | m1) != 0ull) {
+                int j;
+                if (m0) {
+                    j = __builtin_ctzll(m0);
+                    m0 &= m0 - 1ull;
+                } else {
+                    j = 64 + __builtin_ctzll(m1);
+                    m1 &= m1 - 1ull;
+                }
+                step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+            }
+        } else {
+            for (int j = 0; !done && j < n; j++)
+                step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+        }
     }
 
-    if constexpr (GEOM) my_mask[mask_w * kTilePixels] = mask_cur;
+    if constexpr (GEOM) {
+        my_mask[mask_w * kTilePixels] = mask_cur;
+        if constexpr (!SAMPLE) {  // the tile's union of the blended sets (the lane's own column: no barrier)
+            static_assert(kMaskWords >= kBlendWords, "the blended-set masks cover the blend mask");
+#pragma unroll
+            for (int q = 0; q < kBlendWords; q++) {
+                const uint32_t v = my_mask[q * kTilePixels];
+                if (v) atomicOr(&s_union[q], v);
+            }
+        }
+    }
     if constexpr (!SAMPLE) {
         // the composite's outputs are final: written before the median depth
         // (their registers are free for it)
@@ -459,6 +555,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     const uint32_t wmax = wave_max_u(last);
     if ((tid & 63) == 0) s_max[wave] = wmax;
     __syncthreads();
+    if constexpr (!SAMPLE) {
+        if (tid < kBlendWords) a.blend_mask[(size_t)tile * kBlendWords + tid] = s_union[tid];
+    }
     const uint32_t max_contrib = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
 
     // (render path) the pixel's coordinates recomputed where they are needed
@@ -655,13 +754,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         // window ends e0, e8 and sets in_range.  A lane still live on return continues from
         // (t, lo, hi).
         struct Refine {
-            bool refined, in_range, live;
+            bool refined, ill, in_range, live;
             float t_ref, ref_t, ref_D, ref_E;
             float t, lo, hi;
         };
         auto halley = [&](auto&& src, bool grouped, bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
                           int walks, float scale) {
-            Refine r{false, in_range0, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            Refine r{false, false, in_range0, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             const float tol = kRefineTol * scale, tol_cond = kCondTol * scale, tol_loose = kLooseTol * scale;
             const f32x2 TSE[1] = {f32x2{e0, e8}};
             for (int k = 0; k < walks && a.passes > 1; k++) {
@@ -700,13 +799,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
                     float tn = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
                     if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
-                    const bool done = (D > 0.f && fabsf(H) <= tol * D) || hi - lo <= tol ||
-                                      (D > 0.f && fabsf(H) <= tol_loose * D && fabsf(H) * F <= kCurvTol * D * D);
+                    // (converged by the Newton step, or by the bracket closing — the latter also at a jump of T
+                    // across 1/2, where H need not be small)
+                    const bool newton = (D > 0.f && fabsf(H) <= tol * D) ||
+                                        (D > 0.f && fabsf(H) <= tol_loose * D && fabsf(H) * F <= kCurvTol * D * D);
+                    const bool done = newton || hi - lo <= tol;
                     if (done) {
                         // accepted only where the root is well conditioned: rounding noise of
                         // ~kHNoise in log2 T moves it by less than tol_cond (T flat near 1/2 — a
                         // pixel between two splats' peaks — leaves it to the reference's passes)
                         r.refined = D * tol_cond >= kHNoise;
+                        // (an ill-conditioned root only where T itself is at 1/2: converged by the Newton step)
+                        r.ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
                         r.t_ref = tn;
                         live = false;
                         r.ref_t = t;
@@ -810,13 +914,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     p = opaque_int(p);  // (the LDS addresses at the store, not kept from the reads)
                     uint32_t flags = r.in_range ? 0u : kPubOut;
                     float mo = 0.f, dt = 0.f;
-                    if (r.in_range && r.refined) {
-                        flags = kPubRefined;
+                    if (r.in_range && (r.refined || r.ill)) {
+                        flags = r.refined ? kPubRefined : kPubIll;
                         const float nrm = pixel_ray_norm((float)(x0 + (p & 15)), (float)(y0 + (p >> 4)), a.W, a.H,
                                                          a.focal_x, a.focal_y);
                         mo = r.t_ref * (1.0f / nrm);
                         const float mb = mo * nrm;
-                        if (mb != 0.f) dt = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(r.ref_E, mb - r.ref_t, -r.ref_D);
+                        if (r.refined && mb != 0.f)
+                            dt = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(r.ref_E, mb - r.ref_t, -r.ref_D);
                     }
                     s_pub_last[p] = flags;
                     s_pub_T[p] = mo;
@@ -918,6 +1023,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 __syncthreads();
                 const int me = opaque_int(tid);
                 const uint32_t flags = s_pub_last[me];
+                const bool ill = (flags & kPubIll) != 0u;  // root in s_pub_T[me]; dT/dt_m by the walk below
                 if (flags & kPubRefined) {
                     refined = true;
                     have_out = true;
@@ -931,30 +1037,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 // pixel no longer runs the passes with all of its lanes (C2, a sparse 800x800 scene: 134k
                 // of 640k pixels left, in 85% of the waves).  Per pixel the same walks in the same order
                 // as its owner lane would run them: the same outputs.
+                // The list holds the pixels that need the passes first, then the ill-conditioned roots
+                // (one walk each), so the waves working the latter skip the passes.
                 const bool left3 = in_range && !refined;
-                const unsigned long long bl3 = __ballot(left3);
-                if ((tid & 63) == 0) s_max[wave] = (uint32_t)__popcll(bl3);
+                const bool left3p = left3 && !ill;
+                const unsigned long long bl3 = __ballot(left3p), bl3i = __ballot(left3 && ill);
+                if ((tid & 63) == 0) {
+                    s_max[wave] = (uint32_t)__popcll(bl3);
+                    s_alive[0][wave] = __popcll(bl3i);
+                }
                 __syncthreads();  // (every owner has read its flags)
-                uint32_t before3 = 0, n_left = 0;
+                uint32_t before3 = 0, n_pass = 0, before3i = 0, n_ill = 0;
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
                     before3 += w < wave ? s_max[w] : 0u;
-                    n_left += s_max[w];
+                    n_pass += s_max[w];
+                    before3i += w < wave ? (uint32_t)s_alive[0][w] : 0u;
+                    n_ill += (uint32_t)s_alive[0][w];
                 }
-                if constexpr (STATS) st[7] += left3 ? 1 : 0;
+                const uint32_t n_left = n_pass + n_ill;
+                if constexpr (STATS) st[7] += left3p ? 1 : 0;
                 if (n_left > 0) {  // (block-uniform)
                     if (left3) {
-                        s_list[before3 + __popcll(bl3 & ((1ull << (tid & 63)) - 1ull))] = (uint8_t)me;
+                        const unsigned long long lower = (1ull << (tid & 63)) - 1ull;
+                        const uint32_t slot = ill ? n_pass + before3i + __popcll(bl3i & lower)
+                                                  : before3 + __popcll(bl3 & lower);
+                        s_list[slot] = (uint8_t)me;
                         s_pub_last[me] = last;
-                        s_pub_m0[me] = m_init;
+                        s_pub_m0[me] = m_init;  // (an ill root stays in s_pub_T[me])
                     }
                     __syncthreads();
                     const bool own_in = in_range, own_refined = refined;  // (the worker role reuses them)
                     const bool work = (uint32_t)tid < n_left;
+                    const bool work_pass = (uint32_t)tid < n_pass;
                     if (__ballot(work) != 0ull) {  // (waves past the list skip)
-                        if constexpr (STATS) {
-                            if ((tid & 63) == 0) st[5] += 1;
-                        }
                         auto wsrc = [&] {
                             const int pp = s_list[opaque_int(tid)];
                             return PixSrc{s_mask + pp, s_pub_last[pp], (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
@@ -962,13 +1078,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         };
                         const int pw = work ? (int)s_list[tid] : 0;
                         const float wm0 = s_pub_m0[pw];
-                        in_range = work;
+                        in_range = work_pass;
                         refined = false;
-                        dmin = fmaxf(wm0 - a.sample_range, 0.f);
-                        dmax = fmaxf(wm0 + a.sample_range, 0.f);
-                        pass(std::true_type{}, wsrc);
+                        if (__ballot(work_pass) != 0ull) {
+                            if constexpr (STATS) {
+                                if ((tid & 63) == 0) st[5] += 1;
+                            }
+                            dmin = fmaxf(wm0 - a.sample_range, 0.f);
+                            dmax = fmaxf(wm0 + a.sample_range, 0.f);
+                            pass(std::true_type{}, wsrc);
 #pragma unroll 1
-                        for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, wsrc);
+                            for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, wsrc);
+                        }
                         // the median depth and dT/dt_m as the owner path below computes them
                         float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
                         w_max = fminf(fmaxf(w_max, 0.f), 1.f);
@@ -976,7 +1097,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         const float md = in_range ? __builtin_fmaf(w_max, dmax, w_min * dmin) : 0.f;
                         const PixSrc ps = wsrc();
                         const float nrm = pixel_ray_norm(ps.x, ps.y, a.W, a.H, a.focal_x, a.focal_y);
-                        const float mo = md * (1.0f / nrm);
+                        // (an ill-conditioned root: published as the output already)
+                        const bool wi = work && !work_pass;
+                        const float mo = wi ? s_pub_T[pw] : md * (1.0f / nrm);
+                        in_range = in_range || wi;
                         const float mb = mo * nrm;
                         float dT = 0.f;
                         walk(ps.mask, ps.plast, ps.x, ps.y, ~0u, work && mb != 0.f && ps.plast != 0,
@@ -1146,6 +1270,7 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.dT_dtm = is.dT_dtm;
     a.md_check = is.md_check;
     a.max_contrib = ts.max_contrib;
+    a.blend_mask = ts.blend_mask;
     a.tile_order = ts.order;
     a.out_color = out_color;
     a.out_alpha = out_alpha;

@@ -100,6 +100,14 @@ class PixelChains:
         return mdepth_px * math.sqrt(nx * nx + ny * ny + 1.0)
 
 
+def chain_margin(ch, x, y, upto):
+    """The smallest float64 margin of the composite's decisions over the
+    pixel's first `upto` list entries: a pixel whose images differ between
+    two fp32 forwards without a near-tie there is not explained by rounding."""
+    _, _, _, margins = ch.composite(x, y)
+    return float(np.min(margins[:upto])) if upto > 0 and len(margins) else math.inf
+
+
 def ncontrib_flip_margin(ch, x, y, a, b):
     """The decision that separates last contributor a from b (positions in
     the pixel's list): the smallest float64 margin among entries (min, max]."""

@@ -671,14 +671,18 @@ def _audit_full_images(c, out, o, report=None):
     """Every pixel of every image against the oracle, with an exact account of
     the pixels where the two fp32 forwards decide differently (tests/flip_audit.py):
       * last contributor: equal to the oracle's everywhere except at flip
-        pixels (at most 1e-5 of the image, 2 on small images), each proven a near-tie — some
-        decision between the two last contributors is within 2e-4 (relative,
-        float64) of its threshold (T (1 - alpha) = 1e-4, alpha = 1/255);
-      * colour, alpha, normal: every other pixel within 1e-4 of the image max;
-      * median depth: every other pixel within 1e-4, except where the
-        bisection's own decisions are ill-conditioned — each such pixel is
-        proven so in float64 (T within 1e-4 of 1/2 at both depths and between
-        them, or at the in-range tests) and they number at most 1e-4 of the image (2 on small ones).
+        pixels, each proven a near-tie — some decision between the two last
+        contributors is within 2e-4 (relative, float64) of its threshold
+        (T (1 - alpha) = 1e-4, alpha = 1/255, power = 0);
+      * colour, alpha, normal, median depth: within 1e-4 of the image max at
+        every pixel, except pixels proven to sit on a rounding-level decision:
+        a composite decision over the pixel's entries up to its last
+        contributor + 1 within 2e-4 of its threshold (a weak contributor's
+        alpha at 1/255 changes the colour without moving the last
+        contributor), at most 1e-5 of the image (2 on small images); or, for
+        the median depth alone, the bisection's own decisions ill-conditioned
+        — T within 1e-4 of 1/2 at both depths and between them, or at the
+        in-range tests — at most 1e-4 of the image (2 on small ones).
     Must run before the oracle state takes the GPU's contributors."""
     import flip_audit as FA
 
@@ -692,25 +696,50 @@ def _audit_full_images(c, out, o, report=None):
                   for y, x in np.argwhere(flip)]
     rep = {"pixels": H * W, "n_contrib_flips": int(flip.sum()),
            "n_contrib_flip_max_margin": max(nc_margins, default=0.0)}
+    bad_img = np.zeros((H, W), bool)
     for name, t in (("color", color), ("alpha", alpha), ("normal", normal)):
         a_, b_ = t.cpu().numpy().astype(np.float64), o[name].astype(np.float64)
         bad = (np.abs(a_ - b_) > 1e-4 * np.abs(b_).max()).reshape(-1, H, W).any(0)
-        rep[name + "_bad_off_flip"] = int((bad & ~flip).sum())
-        rep[name + "_bad_at_flip"] = int((bad & flip).sum())
+        rep[name + "_bad"] = int(bad.sum())
+        bad_img |= bad
     md_g, md_o = mdepth.cpu().numpy()[0].astype(np.float64), o["mdepth"][0].astype(np.float64)
-    md_bad = (np.abs(md_g - md_o) > 1e-4 * np.abs(md_o).max()) & ~flip
-    md_margins = [FA.mdepth_flip_margin(ch, int(x), int(y), ch.depth_of(int(x), int(y), md_g[y, x]),
-                                        ch.depth_of(int(x), int(y), md_o[y, x])) for y, x in np.argwhere(md_bad)]
-    rep.update(mdepth_bad_off_flip=int(md_bad.sum()), mdepth_max_margin=max(md_margins, default=0.0))
+    md_bad = np.abs(md_g - md_o) > 1e-4 * np.abs(md_o).max()
+    rep["mdepth_bad"] = int(md_bad.sum())
+    n_chain = n_md = 0
+    worst_chain = worst_md = 0.0
+    unexplained = []
+    for y, x in np.argwhere(bad_img | md_bad | flip):
+        upto = int(max(nc_gpu[y, x], nc_orc[y, x])) + 1
+        cm = FA.chain_margin(ch, int(x), int(y), upto)
+        if cm <= 2e-4:
+            n_chain += 1
+            worst_chain = max(worst_chain, cm)
+            continue
+        if flip[y, x] or bad_img[y, x]:
+            unexplained.append(dict(x=int(x), y=int(y), chain_margin=cm, last_gpu=int(nc_gpu[y, x]),
+                                    last_oracle=int(nc_orc[y, x])))
+            continue
+        tg, to = ch.depth_of(int(x), int(y), md_g[y, x]), ch.depth_of(int(x), int(y), md_o[y, x])
+        mm = FA.mdepth_flip_margin(ch, int(x), int(y), tg, to)
+        if mm <= 1e-4:
+            n_md += 1
+            worst_md = max(worst_md, mm)
+        else:
+            last, T_final, m0, _ = ch.composite(int(x), int(y))
+            unexplained.append(dict(x=int(x), y=int(y), gpu=float(md_g[y, x]), oracle=float(md_o[y, x]), t_gpu=tg,
+                                    t_oracle=to, last=last, T_final=T_final, m0=m0, md_margin=mm,
+                                    T_at=[float(v) for v in ch.vacancy(int(x), int(y), last, [tg, to])]))
+    rep.update(composite_tie_pixels=n_chain, composite_tie_max_margin=worst_chain, mdepth_tie_pixels=n_md,
+               mdepth_tie_max_margin=worst_md, unexplained=len(unexplained))
     print("image audit:", rep)
+    if unexplained:
+        print("unexplained pixels:", unexplained[:8])
     if report is not None:
         report.update(rep)
-    assert rep["n_contrib_flips"] <= max(2, 1e-5 * H * W), rep
+    assert not unexplained, (rep, unexplained[:4])
     assert rep["n_contrib_flip_max_margin"] <= 2e-4, rep
-    for name in ("color", "alpha", "normal"):
-        assert rep[name + "_bad_off_flip"] == 0, (name, rep)
-    assert rep["mdepth_bad_off_flip"] <= max(2, 1e-4 * H * W), rep
-    assert rep["mdepth_max_margin"] <= 1e-4, rep
+    assert n_chain <= max(2, 1e-5 * H * W), rep
+    assert n_md <= max(2, 1e-4 * H * W), rep
 
 
 def _full_parity(c, dead_sample):
@@ -786,13 +815,31 @@ def test_c3_stats_instance_is_bit_exact(c3):
         assert torch.equal(ref[k], got[k]), k
 
 
+def _check_refined_depths(a, b, max_loose_frac):
+    """Refined median depths `a` against the reference passes' `b` (same GPU):
+    within 2e-6 relative (the reference's final cell is 2.4e-5 wide; both land
+    within ~1e-7 of the root of T = 1/2 where it is well conditioned), except
+    at the ill-conditioned roots the refinement keeps (render_fwd.hip
+    kIllTol: T flat within rounding of 1/2, where the reference's own answer
+    is decided by rounding noise): within 1.5e-5 of max(mdepth, 1) there, and at
+    most `max_loose_frac` of the pixels."""
+    a64, b64 = a.double(), b.double()
+    d = (a64 - b64).abs()
+    tight = d <= 2e-6 * b64.abs()
+    loose = d <= 1.5e-5 * b64.abs().clamp_min(1.0)  # (mdepth = t rln, rln >= 0.8 here)
+    assert bool(loose.all()), float(d.max())
+    n_loose = int((~tight).sum())
+    print(f"refined depths: {n_loose} of {a.numel()} pixels beyond 2e-6 (ill-conditioned roots), max |d| {float(d.max()):.2e}")
+    assert n_loose <= max_loose_frac * a.numel(), n_loose
+
+
 def test_c3_refinement_matches_bisection(c3):
     """The median-depth root refinement (render_fwd.hip: one walk probing T
     at the window ends and around m0, then bracketed Halley steps) against all
     five reference passes on the same GPU at full C3: colour, alpha, normal
-    and the in-range pattern bit-identical, depths within 2e-6 relative (the
-    reference's final cell is 2.4e-5 wide; both land within ~1e-7 of the
-    root of T = 1/2).  The refinement must be the path C3 takes: at most 2%
+    and the in-range pattern bit-identical, depths as _check_refined_depths
+    (2e-6 relative, ill-conditioned roots within 1.5e-5 of max(mdepth, 1), at most
+    1e-4 of the pixels).  The refinement must be the path C3 takes: at most 2%
     of the waves send a lane to the reference's passes."""
     from diff_gaussian_rasterization import _C
 
@@ -807,8 +854,7 @@ def test_c3_refinement_matches_bisection(c3):
         assert torch.equal(ref[k], got[k]), k
     a, b = got[4], ref[4]
     assert torch.equal(a == 0, b == 0)
-    err = float((a - b).abs().max()) / float(b.abs().max())
-    assert err <= 2e-6, err
+    _check_refined_depths(a, b, max_loose_frac=1e-4)
     waves, fallback_waves = st[4], st[5]
     assert waves > 0 and fallback_waves <= 0.02 * waves, st
 
@@ -844,12 +890,14 @@ def test_c2_forward_parity(c2):
 
 
 def test_c2_compacted_fallback_matches_bisection(c2):
-    """The pixels the refinement leaves to the reference's passes (C2: ~20%,
-    spread over most waves) are compacted and run by the first lanes of the
-    block (render_fwd.hip phase 3): against all five reference passes on the
-    same GPU, colour, alpha, normal and the in-range pattern bit-identical,
-    depths within 2e-6 relative, and the passes run in at most 35% of the
-    waves (one wave per tile holding such pixels)."""
+    """The pixels the refinement leaves to the reference's passes (C2: ~6%
+    not converged, spread over many waves) are compacted and run by the first
+    lanes of the block (render_fwd.hip phase 3), and the ill-conditioned
+    roots it keeps (C2: ~15% of the pixels) get their dT/dt_m there in one
+    walk: against all five reference passes on the same GPU, colour, alpha,
+    normal and the in-range pattern bit-identical, depths as
+    _check_refined_depths (at most 25% of the pixels beyond 2e-6), and the
+    passes run in at most 35% of the waves."""
     from diff_gaussian_rasterization import _C
 
     ga = [_gpu(x) for x in Hh.oracle_args(c2)] + [False]
@@ -866,10 +914,10 @@ def test_c2_compacted_fallback_matches_bisection(c2):
         assert torch.equal(ref[k], got[k]), k
     a, b = got[4], ref[4]
     assert torch.equal(a == 0, b == 0)
-    err = float((a - b).abs().max()) / float(b.abs().max())
-    assert err <= 2e-6, err
+    _check_refined_depths(a, b, max_loose_frac=0.25)
     waves, pass_waves, left = st[4], st[5], st[7]
-    assert left > 0.05 * 800 * 800, st  # the case this test is about
+    print("render stats", st)
+    assert left > 0.02 * 800 * 800, st  # the case this test is about
     assert waves > 0 and pass_waves <= 0.35 * waves, st
 
 
