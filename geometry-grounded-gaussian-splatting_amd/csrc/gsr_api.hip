@@ -212,6 +212,7 @@ size_t carve_tiles(void* base, int T, TileState& s) {
     s.max_contrib = c.take<uint32_t>(T);
     s.order = c.take<uint32_t>(T);
     s.blend_mask = c.take<uint32_t>((size_t)T * kBlendWords);
+    s.bwd_cost = c.take<uint32_t>(T);
     return c.off + 256;
 }
 
@@ -757,7 +758,7 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
         // ordered by one workgroup while the others clear the accumulators
         const size_t zbytes = (size_t)(reinterpret_cast<char*>(ws.tile_order) - static_cast<char*>(wb));
         GSR_STAGE(GSR_STAGE_BWD_CLEAR,
-                  launch_bwd_prepare(wb, zbytes, (uint32_t)tiles, ts.max_contrib, ws.tile_order, stream),
+                  launch_bwd_prepare(wb, zbytes, (uint32_t)tiles, ts.bwd_cost, ws.tile_order, stream),
                   "clear accumulators + tile order");
     } else {
         GSR_STAGE(GSR_STAGE_BWD_CLEAR, hipMemsetAsync(wb, 0, wbytes, stream), "memset accumulators");

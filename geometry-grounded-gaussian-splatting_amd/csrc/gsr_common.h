@@ -125,6 +125,7 @@ struct TileState {
     uint32_t* max_contrib;
     uint32_t* order;       // launch order of the tiles, heaviest first (tile_order_kernel)
     uint32_t* blend_mask;  // [T][kBlendWords]
+    uint32_t* bwd_cost;    // [T] entries the backward walks: set bits of blend_mask + entries past it
 };
 // ---- sample_depth state (PointState / DuplicatedTileState, rasterizer_impl.h) ----
 constexpr uint32_t kNoTile = 0xffffffffu;

@@ -65,6 +65,7 @@ struct RenderFwdArgs {
     uint32_t* md_check;
     uint32_t* max_contrib;
     uint32_t* blend_mask;  // [tiles][kBlendWords] (render path)
+    uint32_t* bwd_cost;    // [tiles] (render path) the backward's walk length, its LPT launch order's cost
     float* out_color;
     float* out_alpha;
     float* out_normal;
@@ -579,7 +580,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     auto lane_mask = [&]() -> const uint32_t* { return s_mask + (GEOM ? opaque_int(tid) : 0); };
     float mDepth = 0.f, md_out = 0.f, md_dT = 0.f;
     bool md_ok = false, md_in_range = false;
-    if constexpr (GEOM) {
+#ifndef GSR_TIME_COMPOSITE_ONLY
+#define GSR_TIME_COMPOSITE_ONLY 0  // (timing builds only: skip the median depth, its outputs are then wrong)
+#endif
+    if constexpr (GEOM && !(GSR_TIME_COMPOSITE_ONLY && !SAMPLE)) {
         unsigned long long st[8] = {0, 0, cst[0], cst[1], 0, 0, 0, 0};
         float Tp[kSplit + 1];
         // the reference's first window (render_forward.cu:560-562)
@@ -1249,7 +1253,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             a.out_normal[2 * HW + pix] = 0.f;
         }
     }
-    if (tid == 0) a.max_contrib[tile] = max_contrib;
+    if (tid == 0) {
+        a.max_contrib[tile] = max_contrib;
+        // the backward walks the blended entries of the mask plus every entry past it
+        uint32_t n = max_contrib > (uint32_t)(kBlendWords * 32) ? max_contrib - (uint32_t)(kBlendWords * 32) : 0u;
+#pragma unroll
+        for (int q = 0; q < kBlendWords; q++) n += (uint32_t)__popc(s_union[q]);
+        a.bwd_cost[tile] = n;
+    }
 }
 
 hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const BinningState& bs, const ImageState& is,
@@ -1271,6 +1282,7 @@ hipError_t launch_render_fwd(const FwdParams& p, const GeomState& gs, const Binn
     a.md_check = is.md_check;
     a.max_contrib = ts.max_contrib;
     a.blend_mask = ts.blend_mask;
+    a.bwd_cost = ts.bwd_cost;
     a.tile_order = ts.order;
     a.out_color = out_color;
     a.out_alpha = out_alpha;
