@@ -46,6 +46,26 @@ constexpr int kRowSegBig = GSR_ROW_SEG_BIG;
 constexpr int kRowSegBigP = 2000000;
 static_assert(kRowSeg % 64 == 0 && kRowSegBig % 64 == 0, "row-pass segments are whole 64-entry chunks");
 constexpr int kTileSeg = GSR_TILE_SEG;  // row entries per tile-pass segment
+#ifndef GSR_ROW_WAVES
+#define GSR_ROW_WAVES 1
+#endif
+// Row-pass waves per workgroup: each wave still owns one segment and its own
+// LDS share (no cross-wave step), so a wave orders its LDS phases with a
+// wave-scope fence instead of a workgroup barrier; more than one wave per
+// workgroup only changes how many segments a CU can hold at once.
+constexpr int kRowWaves = GSR_ROW_WAVES;
+
+// orders one wave's LDS phases (LDS instructions of a wave execute in issue
+// order; this keeps the compiler from moving them across the point)
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void row_lds_order() {
+    if constexpr (kRowWaves == 1) __syncthreads();
+    else wave_lds_order();
+}
 
 // ------------------------------------------- exclusive scan, device-sized
 // The counting passes' [bucket][segment] count arrays are scanned by a
@@ -258,14 +278,16 @@ __device__ __forceinline__ QGauss load_q(int q, int q1, const uint32_t* order, c
 constexpr int kRecSpans = 6;
 constexpr uint32_t kNoSpan = 0xffffffffu;  // (spans are lo | hi << 16 with hi < 1024)
 
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64 * kRowWaves)
     rows_count_kernel(int P, int nseg, int rowseg, uint32_t gy, float pad, const uint32_t* __restrict__ order,
                       const uint4* __restrict__ foot, uint32_t* __restrict__ M, uint4* __restrict__ qrec) {
     extern __shared__ unsigned long long s_dyn[];
-    uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn);
-    const int seg = (int)xcd_remap(blockIdx.x, gridDim.x), lane = threadIdx.x;  // XCD-contiguous segments
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn) + wave * gy;
+    const int seg = (int)xcd_remap(blockIdx.x, gridDim.x) * kRowWaves + wave;  // XCD-contiguous segments
+    if (seg >= nseg) return;
     for (uint32_t y = lane; y < gy; y += 64) s_cnt[y] = 0u;
-    __syncthreads();
+    row_lds_order();
     const int q0 = seg * rowseg, q1 = min(P, q0 + rowseg);
     for (int q = q0 + lane; q < q1; q += 64) {
         const QGauss G = load_q(q, q1, order, foot, pad);
@@ -287,7 +309,7 @@ __global__ void __launch_bounds__(64)
         for (uint32_t y = G.R.y0 + kRecSpans; y < G.R.y1; y++)
             if (row_span(G.E, G.R, y, &lo, &hi)) atomicAdd(&s_cnt[y], 1u);
     }
-    __syncthreads();
+    row_lds_order();
     for (uint32_t y = lane; y < gy; y += 64) M[(size_t)y * nseg + seg] = s_cnt[y];
 }
 
@@ -298,14 +320,16 @@ __global__ void __launch_bounds__(64)
 // slot into the other half of a ping-pong pair, so one walk over the
 // entries does rank, write and advance.  The row-wide prologue of each chunk
 // carries the untouched running slots over and clears the next chunk's masks.
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64 * kRowWaves)
     rows_emit_kernel(int P, int nseg, int rowseg, uint32_t gy, float pad, const uint32_t* __restrict__ order,
                      const uint4* __restrict__ foot, const uint32_t* __restrict__ O, const uint4* __restrict__ qrec,
                      uint2* __restrict__ rows) {
-    extern __shared__ unsigned long long s_dyn[];  // 2 x [gy] masks, then 2 x [gy] running slots
-    unsigned long long* s_cov = s_dyn;
-    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_dyn + 2 * gy);
-    const int seg = (int)xcd_remap(blockIdx.x, gridDim.x), lane = threadIdx.x;  // XCD-contiguous segments
+    extern __shared__ unsigned long long s_dyn[];  // per wave: 2 x [gy] masks, then 2 x [gy] running slots
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long* s_cov = s_dyn + (size_t)wave * 3 * gy;
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_cov + 2 * gy);
+    const int seg = (int)xcd_remap(blockIdx.x, gridDim.x) * kRowWaves + wave;  // XCD-contiguous segments
+    if (seg >= nseg) return;
     const int q0 = seg * rowseg, q1 = min(P, q0 + rowseg);
     // the first chunk's records are requested before the strided running-slot
     // loads, so the two round trips overlap; later chunks' one chunk ahead
@@ -318,7 +342,7 @@ __global__ void __launch_bounds__(64)
         s_run[y] = O[(size_t)y * nseg + seg];
         s_cov[y] = 0ull;
     }
-    __syncthreads();
+    row_lds_order();
     const unsigned long long bit = 1ull << lane, below = bit - 1ull;
     uint32_t cur = 0;
     for (int c0 = q0; c0 < q1; c0 += 64, cur ^= 1u) {
@@ -351,7 +375,7 @@ __global__ void __launch_bounds__(64)
         if (tall)
             for (uint32_t y = y0 + kRecSpans; y < y1; y++)
                 if (row_span(G.E, G.R, y, &lo, &hi)) atomicOr(&cov[y], bit);
-        __syncthreads();  // one wave: orders the LDS phases for the compiler
+        row_lds_order();
         auto emit = [&](uint32_t y, uint32_t sp) {
             const unsigned long long m = cov[y];
             const uint32_t rs = run[y];
@@ -364,7 +388,7 @@ __global__ void __launch_bounds__(64)
         if (tall)
             for (uint32_t y = y0 + kRecSpans; y < y1; y++)
                 if (row_span(G.E, G.R, y, &lo, &hi)) emit(y, lo | (hi << 16));
-        __syncthreads();
+        row_lds_order();
     }
 }
 
@@ -839,7 +863,8 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     const ListLayout& L = bs.lists;
     hipError_t e;
     // rows pass
-    hipLaunchKernelGGL(rows_count_kernel, dim3(L.nseg_rows), dim3(64), 4 * gy, stream, p.P, L.nseg_rows, L.rowseg, gy,
+    const uint32_t row_blocks = (uint32_t)((L.nseg_rows + kRowWaves - 1) / kRowWaves);
+    hipLaunchKernelGGL(rows_count_kernel, dim3(row_blocks), dim3(64 * kRowWaves), 4 * gy * kRowWaves, stream, p.P, L.nseg_rows, L.rowseg, gy,
                        p.cull_pad, gs.order, (const uint4*)gs.foot, bs.rows_count, bs.qrec);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     uint32_t* sums = reinterpret_cast<uint32_t*>(bs.list_tmp);
@@ -848,7 +873,7 @@ hipError_t launch_list_binning(const FwdParams& p, const GeomState& gs, const in
     if ((e = launch_scan_excl(bs.rows_count, bs.rows_off, nrows - 1, (uint32_t)(nrows - 1), nullptr, 1u, sums,
                               stream)) != hipSuccess)
         return e;
-    hipLaunchKernelGGL(rows_emit_kernel, dim3(L.nseg_rows), dim3(64), 24 * gy, stream, p.P, L.nseg_rows, L.rowseg, gy,
+    hipLaunchKernelGGL(rows_emit_kernel, dim3(row_blocks), dim3(64 * kRowWaves), 24 * gy * kRowWaves, stream, p.P, L.nseg_rows, L.rowseg, gy,
                        p.cull_pad, gs.order, (const uint4*)gs.foot, bs.rows_off, bs.qrec, bs.rows);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // tiles pass
