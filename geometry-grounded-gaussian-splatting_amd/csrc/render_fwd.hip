@@ -309,6 +309,16 @@ __device__ unsigned long long g_render_stats[8];
 #define GSR_STRIP_CULL 0
 #endif
 
+// Wave-uniform composite loop (render path): every lane of the wave walks
+// every record of the batch, its per-lane early-outs folded into predicates
+// (blend = passes the power / alpha tests, not saturated, not done), and the
+// blending work is skipped only when no lane of the wave blends.  The
+// accumulators take fma(col, a T, C) with a T = 0 on non-blending lanes:
+// C + 0 = C exactly for the finite colours and normals the preprocess writes.
+#ifndef GSR_COMP_UNIFORM
+#define GSR_COMP_UNIFORM 0
+#endif
+
 // Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
 // pixel rows [y0 + 4 s, y0 + 4 s + 3] x columns [x0, x0 + 15].
 __device__ __forceinline__ uint32_t strip_bits(const float4& w0, const float4& w1, int x0, int y0) {
@@ -480,6 +490,45 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         T = test_T;
         last = (uint32_t)g + 1u;  // the reference's 1-based contributor index
     };
+    // GSR_COMP_UNIFORM: one record for the whole wave (see above)
+    auto ustep = [&](int j, int g) {
+        const float4 w0 = s_w0[j], w1 = s_w1[j];
+        const float dx = w0.x - pixx, dy = w0.y - pixy;
+        const float power = splat_power(w0, w1, dx, dy);
+        const float alpha = fminf(0.99f, w1.y * __expf(power));
+        const float test_T = T * (1.f - alpha);
+        const bool pass = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const bool sat = test_T < 0.0001f;
+        const bool blend = pass && !sat && !done;
+        done = done || (pass && sat);
+        const unsigned long long bm = __ballot(blend);
+        if (bm == 0ull) return;  // (wave-uniform)
+        const float aT = blend ? alpha * T : 0.f;
+        if constexpr (!GEOM) {
+            if (g < kBlendWords * 32 && (tid & 63) == __builtin_ctzll(bm)) atomicOr(&s_union[g >> 5], 1u << (g & 31));
+        }
+        const float4 w2 = s_w2[j], w3 = s_w3[j];
+        C0 = __builtin_fmaf(w2.z, aT, C0);
+        C1 = __builtin_fmaf(w2.w, aT, C1);
+        C2 = __builtin_fmaf(w3.x, aT, C2);
+        if constexpr (GEOM) {
+            N0 = __builtin_fmaf(w3.y, aT, N0);
+            N1 = __builtin_fmaf(w3.z, aT, N1);
+            N2 = __builtin_fmaf(w3.w, aT, N2);
+            const float t = splat_tpeak(w1, w2, dx, dy);
+            m_init = (blend && T > 0.5f) ? t : m_init;
+            if (g < kResident) {
+                if ((g >> 5) != mask_w) {  // (g is wave-uniform: so is the word switch)
+                    my_mask[mask_w * kTilePixels] = mask_cur;
+                    mask_cur = 0u;
+                    mask_w = g >> 5;
+                }
+                mask_cur |= blend ? 1u << (g & 31) : 0u;
+            }
+        }
+        T = blend ? test_T : T;
+        last = blend ? (uint32_t)g + 1u : last;
+    };
     int toDo = total;
     for (int i = 0; i < rounds; i++, toDo -= kBatch) {
         // block-wide early exit: every wave publishes whether any lane is live
@@ -514,6 +563,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     m1 &= m1 - 1ull;
                 }
                 step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+            }
+        } else if constexpr (GSR_COMP_UNIFORM && !SAMPLE) {
+            for (int j = 0; j < n; j++) {
+                if (__ballot(!done) == 0ull) break;
+                ustep(j, i * kBatch + j);
             }
         } else {
             for (int j = 0; !done && j < n; j++)
