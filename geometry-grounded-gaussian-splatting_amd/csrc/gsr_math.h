@@ -202,65 +202,144 @@ __device__ __forceinline__ void store_sh_grad(float* row, int SHM, int n, const 
 }
 
 // ---- symmetric 3x3 eigen-decomposition (cov3D_precomp path) --------------
-// The reference runs glm's Householder + QL solver (auxiliary.h:155-340); any
-// solver that returns the same eigen-pairs up to sign gives the same results,
-// because every use is sign-invariant (Vrk^-1 = E diag(1/l) E^T, and
-// projectors e e^T).  Closed form: trigonometric eigenvalues, eigenvectors
-// from the largest cross product of two rows of (A - l I).
-__device__ inline void sym3_eigvec(const float* A, float lam, float* e) {
-    const float r0[3] = {A[0] - lam, A[1], A[2]};
-    const float r1[3] = {A[3], A[4] - lam, A[5]};
-    const float r2[3] = {A[6], A[7], A[8] - lam};
-    float c[3][3];
-    const float* rs[3][2] = {{r0, r1}, {r0, r2}, {r1, r2}};
-    int best = 0;
-    float bn = -1.f;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const float* a = rs[k][0];
-        const float* b = rs[k][1];
-        c[k][0] = a[1] * b[2] - a[2] * b[1];
-        c[k][1] = a[2] * b[0] - a[0] * b[2];
-        c[k][2] = a[0] * b[1] - a[1] * b[0];
-        const float n = c[k][0] * c[k][0] + c[k][1] * c[k][1] + c[k][2] * c[k][2];
-        if (n > bn) { bn = n; best = k; }
+// The reference's solver (glm_modification::findEigenvaluesSymReal,
+// auxiliary.h:155-340): Householder reduction to tridiagonal form, then
+// implicit QL iterations, in fp32 with its 1e-7 zero tests — restated here
+// (as in oracle/gsr_oracle.c) because the inverse of a thin Gaussian's
+// covariance is only as accurate as its smallest eigenvalue, and a closed-form
+// (trigonometric) solver loses that one to cancellation: normals 4e-4 off the
+// oracle's on tests/golden/cov3d.npz against 1e-4 for this solver.
+// Every use is sign- and order-invariant (E diag(1/l) E^T, e e^T).
+__device__ inline float sym3_pythag(float a, float b) {
+    float aa = fabsf(a), ab = fabsf(b);
+    if (aa > ab) {
+        ab /= aa;
+        ab *= ab;
+        return aa * sqrtf(1.f + ab);
     }
-    if (bn <= 1e-30f) { e[0] = 1.f; e[1] = 0.f; e[2] = 0.f; return; }
-    const float in = 1.0f / sqrtf(bn);
-    e[0] = c[best][0] * in; e[1] = c[best][1] * in; e[2] = c[best][2] * in;
+    if (ab <= 1e-7f) return 0.f;
+    aa /= ab;
+    aa *= aa;
+    return ab * sqrtf(1.f + aa);
 }
 
 // eigenvalues ascending in l[0..2], eigenvectors as rows of E (E[3k..3k+2] for l[k])
 __device__ inline void sym3_eigen(const float* A, float* l, float* E) {
-    const float p1 = A[1] * A[1] + A[2] * A[2] + A[5] * A[5];
-    const float q = (A[0] + A[4] + A[8]) * (1.0f / 3.0f);
-    const float p2 = (A[0] - q) * (A[0] - q) + (A[4] - q) * (A[4] - q) + (A[8] - q) * (A[8] - q) + 2.f * p1;
-    const float p = sqrtf(p2 * (1.0f / 6.0f));
-    if (p <= 1e-30f) {
-        l[0] = l[1] = l[2] = q;
-        E[0] = 1; E[1] = 0; E[2] = 0; E[3] = 0; E[4] = 1; E[5] = 0; E[6] = 0; E[7] = 0; E[8] = 1;
-        return;
+    constexpr float eps = 1e-7f;
+    // a: row-major working copy (the matrix is symmetric, so glm's column order reads the same)
+    float a[9], d[3], e[3];
+#pragma unroll
+    for (int k = 0; k < 9; k++) a[k] = A[k];
+    // Householder: rows 2, 1 (tred2 with n = 3)
+    for (int i = 2; i >= 1; i--) {
+        const int lm = i - 1;  // last column of the row's sub-diagonal part
+        float h = 0.f;
+        if (lm > 0) {
+            float scale = 0.f;
+            for (int k = 0; k <= lm; k++) scale += fabsf(a[3 * i + k]);
+            if (scale <= eps) {
+                e[i] = a[3 * i + lm];
+            } else {
+                for (int k = 0; k <= lm; k++) {
+                    a[3 * i + k] /= scale;
+                    h += a[3 * i + k] * a[3 * i + k];
+                }
+                float f = a[3 * i + lm];
+                float g = f >= 0.f ? -sqrtf(h) : sqrtf(h);
+                e[i] = scale * g;
+                h -= f * g;
+                a[3 * i + lm] = f - g;
+                f = 0.f;
+                for (int j = 0; j <= lm; j++) {
+                    a[3 * j + i] = a[3 * i + j] / h;
+                    g = 0.f;
+                    for (int k = 0; k <= j; k++) g += a[3 * j + k] * a[3 * i + k];
+                    for (int k = j + 1; k <= lm; k++) g += a[3 * k + j] * a[3 * i + k];
+                    e[j] = g / h;
+                    f += e[j] * a[3 * i + j];
+                }
+                const float hh = f / (h + h);
+                for (int j = 0; j <= lm; j++) {
+                    f = a[3 * i + j];
+                    e[j] = g = e[j] - hh * f;
+                    for (int k = 0; k <= j; k++) a[3 * j + k] -= (f * e[k] + g * a[3 * i + k]);
+                }
+            }
+        } else {
+            e[i] = a[3 * i + lm];
+        }
+        d[i] = h;
     }
-    const float ip = 1.0f / p;
-    const float B[9] = {(A[0] - q) * ip, A[1] * ip, A[2] * ip, A[3] * ip, (A[4] - q) * ip, A[5] * ip,
-                        A[6] * ip, A[7] * ip, (A[8] - q) * ip};
-    float r = 0.5f * (B[0] * (B[4] * B[8] - B[5] * B[7]) - B[1] * (B[3] * B[8] - B[5] * B[6]) +
-                      B[2] * (B[3] * B[7] - B[4] * B[6]));
-    r = fminf(1.f, fmaxf(-1.f, r));
-    const float phi = acosf(r) * (1.0f / 3.0f);
-    const float hi = q + 2.f * p * cosf(phi);
-    const float lo = q + 2.f * p * cosf(phi + 2.0943951023931953f);
-    l[0] = lo;
-    l[2] = hi;
-    l[1] = 3.f * q - hi - lo;
-    sym3_eigvec(A, l[0], E);
-    sym3_eigvec(A, l[2], E + 6);
-    // middle eigenvector orthogonal to the other two
-    E[3] = E[7] * E[2] - E[8] * E[1];
-    E[4] = E[8] * E[0] - E[6] * E[2];
-    E[5] = E[6] * E[1] - E[7] * E[0];
-    const float n = sqrtf(E[3] * E[3] + E[4] * E[4] + E[5] * E[5]);
-    if (n > 0) { E[3] /= n; E[4] /= n; E[5] /= n; }
+    d[0] = 0.f;
+    e[0] = 0.f;
+    // accumulate the transformations
+    for (int i = 0; i < 3; i++) {
+        if (!(fabsf(d[i]) <= eps)) {
+            for (int j = 0; j < i; j++) {
+                float g = 0.f;
+                for (int k = 0; k < i; k++) g += a[3 * i + k] * a[3 * k + j];
+                for (int k = 0; k < i; k++) a[3 * k + j] -= g * a[3 * k + i];
+            }
+        }
+        d[i] = a[3 * i + i];
+        a[3 * i + i] = 1.f;
+        for (int j = 0; j < i; j++) a[3 * j + i] = a[3 * i + j] = 0.f;
+    }
+    // implicit QL on the tridiagonal (d, e)
+    e[0] = e[1];
+    e[1] = e[2];
+    e[2] = 0.f;
+    for (int ll = 0; ll < 3; ll++) {
+        int iter = 0, m;
+        do {
+            for (m = ll; m < 2; m++)
+                if (fabsf(e[m]) <= eps) break;
+            if (m != ll) {
+                if (iter++ == 30) break;
+                float g = (d[ll + 1] - d[ll]) / (2.f * e[ll]);
+                float r = sym3_pythag(g, 1.f);
+                g = d[m] - d[ll] + e[ll] / (g + (g >= 0.f ? fabsf(r) : -fabsf(r)));
+                float s = 1.f, c = 1.f, p = 0.f;
+                int i;
+                bool zero = false;
+                for (i = m - 1; i >= ll; i--) {
+                    const float f = s * e[i];
+                    const float b = c * e[i];
+                    e[i + 1] = r = sym3_pythag(f, g);
+                    if (r <= eps) {
+                        d[i + 1] -= p;
+                        e[m] = 0.f;
+                        zero = true;
+                        break;
+                    }
+                    s = f / r;
+                    c = g / r;
+                    g = d[i + 1] - p;
+                    r = (d[i] - g) * s + 2.f * c * b;
+                    d[i + 1] = g + (p = s * r);
+                    g = c * r - b;
+                    for (int k = 0; k < 3; k++) {
+                        const float fk = a[3 * k + i + 1];
+                        a[3 * k + i + 1] = s * a[3 * k + i] + c * fk;
+                        a[3 * k + i] = c * a[3 * k + i] - s * fk;
+                    }
+                }
+                if (zero && i >= ll) continue;
+                d[ll] -= p;
+                e[ll] = g;
+                e[m] = 0.f;
+            }
+        } while (m != ll);
+    }
+    // ascending, eigenvector k = column k of a
+    int o[3] = {0, 1, 2};
+    if (d[o[1]] < d[o[0]]) { const int t = o[0]; o[0] = o[1]; o[1] = t; }
+    if (d[o[2]] < d[o[1]]) { const int t = o[1]; o[1] = o[2]; o[2] = t; }
+    if (d[o[1]] < d[o[0]]) { const int t = o[0]; o[0] = o[1]; o[1] = t; }
+    for (int k = 0; k < 3; k++) {
+        l[k] = d[o[k]];
+        for (int r = 0; r < 3; r++) E[3 * k + r] = a[3 * r + o[k]];
+    }
 }
 
 // Vrk^-1 when the smallest eigenvalue exceeds 1e-8 (returns true), else the

@@ -295,6 +295,16 @@ __device__ unsigned long long g_render_stats[8];
 // blocks per CU) 0.893; a 192-record cache 0.820; 64-record batches 0.825.
 // Tiles whose contributing prefix exceeds the cache take the wave-uniform
 // walk (C3's largest per-tile max contributor is 184).
+// Development: -DGSR_DBG_PX=x -DGSR_DBG_PY=y prints the median-depth phases' results for one pixel.
+#ifdef GSR_DBG_PX
+#define GSR_DBG(p, ...) \
+    do { if (x0 + ((p) & 15) == GSR_DBG_PX && y0 + ((p) >> 4) == GSR_DBG_PY) printf(__VA_ARGS__); } while (0)
+#define GSR_DBG_NEAR(p, ...) \
+    do { if (abs(x0 + ((p) & 15) - GSR_DBG_PX) <= 1 && abs(y0 + ((p) >> 4) - GSR_DBG_PY) <= 1) printf(__VA_ARGS__); } while (0)
+#else
+#define GSR_DBG(p, ...) do { } while (0)
+#define GSR_DBG_NEAR(p, ...) do { } while (0)
+#endif
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
@@ -855,8 +865,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     if (H >= 0.f) lo = t;
                     else hi = t;
                     // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
-                    float tn = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
-                    if (!(tn >= lo && tn <= hi)) tn = 0.5f * (lo + hi);
+                    const float th = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
+                    const bool halley_in = th >= lo && th <= hi;
+                    float tn = halley_in ? th : 0.5f * (lo + hi);
                     // (converged by the Newton step, or by the bracket closing — the latter also at a jump of T
                     // across 1/2, where H need not be small)
                     const bool newton = (D > 0.f && fabsf(H) <= tol * D) ||
@@ -869,7 +880,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         r.refined = D * tol_cond >= kHNoise;
                         // (an ill-conditioned root only where T itself is at 1/2: converged by the Newton step)
                         r.ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
-                        r.t_ref = tn;
+                        // (converged by the Newton test with the Halley iterate out of the bracket — H'' large
+                        // against H' near a splat's peak — the root is the Newton iterate, not the midpoint)
+                        r.t_ref = newton && !halley_in ? fminf(fmaxf(t + fast_div(H, D), lo), hi) : tn;
                         live = false;
                         r.ref_t = t;
                         r.ref_D = D;
@@ -999,6 +1012,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     if (q == 0) {
                         const int lane = opaque_int(tid);
                         s_groot[lane >> 2] = (r.in_range && r.refined) ? r.t_ref : -1.f;
+                        GSR_DBG_NEAR(grid_pixel(lane), "p1 (%d,%d): m0 %.7f -> live %d in %d ref %d ill %d t_ref %.7f D %g\n",
+                                     x0 + (grid_pixel(lane) & 15), y0 + (grid_pixel(lane) >> 4), gm0, (int)r.live,
+                                     (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.ref_D);
                         publish(grid_pixel(lane), r);
                     }
                 }
@@ -1039,6 +1055,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     const float t0 = cnt ? fminf(fmaxf(sum / (float)cnt, e0), e8) : e0;
                     auto src = [&] { return PixSrc{s_mask + p, ql, qx, qy, ~0u}; };  // (one walk)
                     const Refine r = halley(src, false, qin && cnt > 0, t0, e0, e8, true, e0, e8, qin, 1, fmaxf(t0, 1.f));
+                    GSR_DBG(p, "p2: m0 %.7f cnt %d t0 %.7f -> live %d in %d ref %d ill %d t_ref %.7f t %.7f [%.7f %.7f] D %g\n",
+                            qm0, cnt, t0, (int)r.live, (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.t, r.lo,
+                            r.hi, r.ref_D);
                     live2 = r.live;
                     if (live2) {  // continued by a lane group below
                         s_pub_last[p] = ql;
@@ -1076,6 +1095,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     };
                     const Refine r = halley(src, true, true, t, s_pub_m0[p], s_pub_hi[p], false, 0.f, 0.f, true,
                                             kRefineWalks - 1, fmaxf(t, 1.f));
+                    if ((tid & 3) == 0)
+                        GSR_DBG(p, "p2b: from %.7f -> live %d in %d ref %d ill %d t_ref %.7f t %.7f [%.7f %.7f] D %g\n", t,
+                                (int)r.live, (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.t, r.lo, r.hi, r.ref_D);
                     if ((tid & 3) == 0) publish(s_list[opaque_int((int)e)], r);
                 }
                 __syncthreads();
@@ -1167,6 +1189,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                                  const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
                                  dT += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
                              });
+                        if (work) GSR_DBG(pw, "p3: pass %d m0 %.7f [%.7f %.7f] Tp0 %.7f Tp8 %.7f in %d mo %.7f dT %g\n",
+                                          (int)work_pass, wm0, dmin, dmax, Tp[0], Tp[kSplit], (int)in_range, mo, dT);
                         if (work) {
                             const int q = s_list[opaque_int(tid)];
                             s_pub_T[q] = mo;

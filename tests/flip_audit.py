@@ -48,10 +48,12 @@ class PixelChains:
         t_peak = rp[:, 0] * dx + rp[:, 1] * dy + rp[:, 2]
         return power, alpha, t_peak, rp[:, 3]
 
-    def composite(self, x, y):
+    def composite(self, x, y, toggle=-1):
         """(last contributor, final T, m0, per-entry margins) of the float64
         composite; margins[k] = the smallest relative distance of entry k+1's
-        three decisions to their thresholds."""
+        three decisions to their thresholds.  `toggle` = k takes the other
+        outcome of entry k's nearest decision (skip / blend / stop), as an fp32
+        evaluation on the other side of that threshold would."""
         power, alpha, t_peak, _ = self.contributors(x, y)
         n = len(power)
         T, last, m0 = 1.0, 0, 0.0
@@ -59,16 +61,25 @@ class PixelChains:
         self.m0_margin = math.inf  # the T > 1/2 test that picks m0
         for k in range(n):
             mk = abs(power[k]) / max(1e-30, abs(power[k]) + 1.0) * 1e3  # power = 0 decides only at exactly 0
-            if power[k] > 0:
+            ma = abs(alpha[k] * 255.0 - 1.0)
+            test_T = T * (1.0 - alpha[k])
+            ms = abs(test_T / 1e-4 - 1.0)
+            skip = power[k] > 0 or alpha[k] < 1.0 / 255.0
+            stop = not skip and test_T < 1e-4
+            if k == toggle:
+                if min(mk, ma) <= ms:
+                    skip, stop = not skip, False
+                    stop = not skip and test_T < 1e-4
+                else:
+                    skip, stop = False, not stop
+            if power[k] > 0 and k != toggle:
                 margins[k] = mk
                 continue
-            ma = abs(alpha[k] * 255.0 - 1.0)
-            if alpha[k] < 1.0 / 255.0:
+            if skip:
                 margins[k] = min(mk, ma)
                 continue
-            test_T = T * (1.0 - alpha[k])
-            margins[k] = min(mk, ma, abs(test_T / 1e-4 - 1.0))
-            if test_T < 1e-4:
+            margins[k] = min(mk, ma, ms)
+            if stop:
                 break
             self.m0_margin = min(self.m0_margin, abs(T / 0.5 - 1.0))
             if T > 0.5:
@@ -106,6 +117,21 @@ def chain_margin(ch, x, y, upto):
     two fp32 forwards without a near-tie there is not explained by rounding."""
     _, _, _, margins = ch.composite(x, y)
     return float(np.min(margins[:upto])) if upto > 0 and len(margins) else math.inf
+
+
+def ncontrib_flip_explained(ch, x, y, last_gpu, tol=2e-4):
+    """Whether the GPU's last contributor is the float64 composite's with one
+    decision at most `tol` from its threshold taking its other outcome: the
+    flip is then a rounding-level tie, directly (the decision between the two
+    last contributors) or upstream (a weak contributor's alpha at 1/255 moves
+    T by up to 1/255 relative, and a later saturation test with it)."""
+    last, _, _, margins = ch.composite(x, y)
+    if last == last_gpu:
+        return True
+    for k in np.flatnonzero(margins[:max(last, last_gpu) + 1] <= tol):
+        if ch.composite(x, y, toggle=int(k))[0] == last_gpu:
+            return True
+    return False
 
 
 def ncontrib_flip_margin(ch, x, y, a, b):

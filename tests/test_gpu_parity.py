@@ -348,9 +348,21 @@ def test_cov3d_precomp_path_pinned_to_reference_covariance(geom):
     assert o_sr[0] == o_cv[0] and torch.equal(o_sr[5], o_cv[5])
     assert int((o_sr[5] > 0).sum()) > P // 2
     names = ["color", "alpha"] + (["normal", "mdepth"] if geom else [])
+    # the normals and median depths go through the inverse covariance (render_forward.cu:162-189 against
+    # :143-160): for thin Gaussians the two inputs' inverses differ by their conditioning, in the oracle too —
+    # each GPU path is held to the oracle's same path, and the gap between the paths to the oracle's gap
+    orc_f = {"sr": O.forward(*_fwd_args(c)), "cv": O.forward(*_fwd_args(c, cov3D=cov))}
     for k, name in zip((1, 2, 3, 4), names):
         err = Hh.rel_err(o_cv[k].cpu().numpy(), o_sr[k].cpu().numpy())
-        assert err <= 1e-4, (name, err)
+        o_gap = Hh.rel_err(orc_f["cv"][name], orc_f["sr"][name])
+        bar = max(1e-4, 2 * o_gap + 1e-5)
+        e_sr = Hh.rel_err(o_sr[k].cpu().numpy(), orc_f["sr"][name])
+        e_cv = Hh.rel_err(o_cv[k].cpu().numpy(), orc_f["cv"][name])
+        print(f"{name}: gpu path gap {err:.2e}, oracle path gap {o_gap:.2e}, gpu vs oracle sr {e_sr:.2e} cv {e_cv:.2e}")
+        assert e_sr <= 1e-4, (name, "sr", e_sr)
+        # (the covariance input's inverse is only as accurate as its conditioning allows, in either fp32 program)
+        assert e_cv <= bar, (name, "cv", e_cv, o_gap)
+        assert err <= bar, (name, err, o_gap)
     if geom:
         return
     g = {k: _gpu(v) for k, v in S.upstream_grads(c["H"], c["W"], seed=61).items()}
@@ -671,9 +683,10 @@ def _audit_full_images(c, out, o, report=None):
     """Every pixel of every image against the oracle, with an exact account of
     the pixels where the two fp32 forwards decide differently (tests/flip_audit.py):
       * last contributor: equal to the oracle's everywhere except at flip
-        pixels, each proven a near-tie — some decision between the two last
-        contributors is within 2e-4 (relative, float64) of its threshold
-        (T (1 - alpha) = 1e-4, alpha = 1/255, power = 0);
+        pixels, each proven a near-tie — the float64 composite with one
+        decision within 2e-4 (relative) of its threshold (T (1 - alpha) =
+        1e-4, alpha = 1/255, power = 0) taking its other outcome reproduces
+        the GPU's last contributor (flip_audit.ncontrib_flip_explained);
       * colour, alpha, normal, median depth: within 1e-4 of the image max at
         every pixel, except pixels proven to sit on a rounding-level decision:
         a composite decision over the pixel's entries up to its last
@@ -694,8 +707,10 @@ def _audit_full_images(c, out, o, report=None):
     ch = FA.PixelChains(o, W, H, c["tanx"], c["tany"])
     nc_margins = [FA.ncontrib_flip_margin(ch, int(x), int(y), nc_gpu[y, x], nc_orc[y, x])
                   for y, x in np.argwhere(flip)]
+    nc_unexplained = [(int(x), int(y)) for y, x in np.argwhere(flip)
+                      if not FA.ncontrib_flip_explained(ch, int(x), int(y), int(nc_gpu[y, x]))]
     rep = {"pixels": H * W, "n_contrib_flips": int(flip.sum()),
-           "n_contrib_flip_max_margin": max(nc_margins, default=0.0)}
+           "n_contrib_flip_max_margin": max(nc_margins, default=0.0), "n_contrib_flips_unexplained": nc_unexplained}
     bad_img = np.zeros((H, W), bool)
     for name, t in (("color", color), ("alpha", alpha), ("normal", normal)):
         a_, b_ = t.cpu().numpy().astype(np.float64), o[name].astype(np.float64)
@@ -737,7 +752,7 @@ def _audit_full_images(c, out, o, report=None):
     if report is not None:
         report.update(rep)
     assert not unexplained, (rep, unexplained[:4])
-    assert rep["n_contrib_flip_max_margin"] <= 2e-4, rep
+    assert not nc_unexplained, rep  # every flip reproduced by toggling one decision within 2e-4 of its threshold
     assert n_chain <= max(2, 1e-5 * H * W), rep
     assert n_md <= max(2, 1e-4 * H * W), rep
 
@@ -821,12 +836,16 @@ def _check_refined_depths(a, b, max_loose_frac):
     within ~1e-7 of the root of T = 1/2 where it is well conditioned), except
     at the ill-conditioned roots the refinement keeps (render_fwd.hip
     kIllTol: T flat within rounding of 1/2, where the reference's own answer
-    is decided by rounding noise): within 1.5e-5 of max(mdepth, 1) there, and at
-    most `max_loose_frac` of the pixels."""
+    is decided by rounding noise): there the root is known to kIllTol max(t, 1)
+    and the reference's answer is a linear interpolation inside its final
+    bisection cell (0.8 / 8^5 = 2.4e-5 wide) between noise-level T values, so
+    within 1.5e-5 max(mdepth, 1) + 2.4e-5 — at most `max_loose_frac` of the
+    pixels."""
     a64, b64 = a.double(), b.double()
     d = (a64 - b64).abs()
     tight = d <= 2e-6 * b64.abs()
-    loose = d <= 1.5e-5 * b64.abs().clamp_min(1.0)  # (mdepth = t rln, rln >= 0.8 here)
+    cell = 0.8 / 8 ** 5  # (mdepth = t rln, rln <= 1: a cell in t is at most as wide in mdepth)
+    loose = d <= 1.5e-5 * b64.abs().clamp_min(1.0) + cell
     assert bool(loose.all()), float(d.max())
     n_loose = int((~tight).sum())
     print(f"refined depths: {n_loose} of {a.numel()} pixels beyond 2e-6 (ill-conditioned roots), max |d| {float(d.max()):.2e}")
@@ -838,7 +857,7 @@ def test_c3_refinement_matches_bisection(c3):
     at the window ends and around m0, then bracketed Halley steps) against all
     five reference passes on the same GPU at full C3: colour, alpha, normal
     and the in-range pattern bit-identical, depths as _check_refined_depths
-    (2e-6 relative, ill-conditioned roots within 1.5e-5 of max(mdepth, 1), at most
+    (2e-6 relative, ill-conditioned roots within 1.5e-5 max(mdepth, 1) + one final cell, at most
     1e-4 of the pixels).  The refinement must be the path C3 takes: at most 2%
     of the waves send a lane to the reference's passes."""
     from diff_gaussian_rasterization import _C
