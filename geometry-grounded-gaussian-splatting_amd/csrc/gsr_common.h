@@ -202,6 +202,18 @@ __device__ __forceinline__ float add_lane_xor32(float a) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// OR over the 64 lanes of a wave, result in every lane; VALU only (as wave_sum_dpp)
+__device__ __forceinline__ uint32_t wave_or_dpp(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppRowMirror, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppRowHalfMirror, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppXor2, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppXor1, 0xF, 0xF, false);
+    auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = r[0] | r[1];
+    r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return r[0] | r[1];
+}
+
 // Sum over the 64 lanes of a wave, result in every lane; VALU only.  Within
 // a 16-lane row the partners are l^15, l^7 (mirrors: each stage pairs the two
 // halves of a group bijectively, so each lane is counted once), then l^2, l^1.

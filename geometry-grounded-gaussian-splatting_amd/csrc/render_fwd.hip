@@ -270,8 +270,11 @@ struct PixSrc {
 // [0] per-lane walk wave-steps and [1] their active lanes; [2] composite
 // wave-steps and [3] their blending lanes;
 // [4] waves running the refinement, [5] waves sending a lane to the
-// reference's passes, [6] refinement lane-walks, [7] lanes left to the passes.
-__device__ unsigned long long g_render_stats[8];
+// reference's passes, [6] refinement lane-walks, [7] lanes left to the passes;
+// [8 + 2 f], [9 + 2 f]: walk wave-steps and their active lanes of render-path
+// phase f = 0 (1: grid pixels), 1 (2: first walk), 2 (2b: grouped), 3 (3: passes / dT walks).
+constexpr int kRenderStats = 16;
+__device__ unsigned long long g_render_stats[kRenderStats];
 
 // SAMPLE: queries at arbitrary points — lanes hold points of one tile's
 // chunk and the outputs are per point.  Everything else (batching,
@@ -589,10 +592,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         my_mask[mask_w * kTilePixels] = mask_cur;
         if constexpr (!SAMPLE) {  // the tile's union of the blended sets (the lane's own column: no barrier)
             static_assert(kMaskWords >= kBlendWords, "the blended-set masks cover the blend mask");
+            // OR over the wave first (DPP, VALU only), then one lane per wave: 64 lanes' atomics on
+            // one LDS word would serialize
+            // (per-lane atomics instead: render_fwd 0.766 -> 0.821 ms at C3)
 #pragma unroll
             for (int q = 0; q < kBlendWords; q++) {
-                const uint32_t v = my_mask[q * kTilePixels];
-                if (v) atomicOr(&s_union[q], v);
+                const uint32_t v = wave_or_dpp(my_mask[q * kTilePixels]);
+                if ((tid & 63) == 0 && v) atomicOr(&s_union[q], v);
             }
         }
     }
@@ -648,7 +654,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
 #define GSR_TIME_COMPOSITE_ONLY 0  // (timing builds only: skip the median depth, its outputs are then wrong)
 #endif
     if constexpr (GEOM && !(GSR_TIME_COMPOSITE_ONLY && !SAMPLE)) {
-        unsigned long long st[8] = {0, 0, cst[0], cst[1], 0, 0, 0, 0};
+        unsigned long long st[kRenderStats] = {0, 0, cst[0], cst[1]};
+        int st_phase = 0;  // (STATS) render-path phase of the walks below
         float Tp[kSplit + 1];
         // the reference's first window (render_forward.cu:560-562)
         // (set where the passes start: only m_init stays live until then)
@@ -702,6 +709,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     if ((tid & 63) == __builtin_ctzll(m)) {
                         st[0] += 1;
                         st[1] += __popcll(m);
+                        st[8 + 2 * st_phase] += 1;
+                        st[9 + 2 * st_phase] += __popcll(m);
                     }
                 }
                 const float4 a0 = c_w0[j1], b0 = c_w0[j2];
@@ -1020,6 +1029,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 }
                 __syncthreads();
                 const int skip = (int)(blockIdx.x & 3u);  // the wave left idle (rotated over the SIMDs)
+                if constexpr (STATS) st_phase = 1;
                 bool live2 = false;  // phase-2 pixel not converged after its first walk
                 int p2 = 0;
                 if (wave != skip) {  // phase 2, first walk
@@ -1083,6 +1093,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     n_live += s_max[w];
                 }
                 uint8_t* s_list = reinterpret_cast<uint8_t*>(s_groot);
+                if constexpr (STATS) st_phase = 2;
                 if (live2) s_list[before + __popcll(bl & ((1ull << (tid & 63)) - 1ull))] = (uint8_t)p2;
                 __syncthreads();
                 for (uint32_t e = (uint32_t)(tid >> 2); e < n_live; e += kTilePixels / 4) {
@@ -1121,6 +1132,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 // (one walk each), so the waves working the latter skip the passes.
                 const bool left3 = in_range && !refined;
                 const bool left3p = left3 && !ill;
+                if constexpr (STATS) st_phase = 3;
                 const unsigned long long bl3 = __ballot(left3p), bl3i = __ballot(left3 && ill);
                 if ((tid & 63) == 0) {
                     s_max[wave] = (uint32_t)__popcll(bl3);
@@ -1238,7 +1250,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             for (int it = 1; it < a.passes; it++) pass(std::false_type{}, own_src);
         }
         if constexpr (STATS) {
-            for (int q = 0; q < 8; q++)
+            for (int q = 0; q < kRenderStats; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
         }
         md_in_range = in_range;
@@ -1513,9 +1525,9 @@ hipError_t launch_chunk_order(uint32_t bound, const uint32_t* n_dev, const uint3
 }
 
 hipError_t read_render_stats(unsigned long long* out, bool reset) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_render_stats), sizeof(unsigned long long) * 8);
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_render_stats), sizeof(unsigned long long) * kRenderStats);
     if (e == hipSuccess && reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[kRenderStats] = {};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_render_stats), z, sizeof(z));
     }
     return e;

@@ -27,3 +27,5 @@ print("walk wave-steps", st[0], "active lanes/step", round(st[1] / max(st[0], 1)
 print("composite wave-steps", st[2], "blending lanes/step", round(st[3] / max(st[2], 1), 2))
 print(f"P={P} {W}x{H}")
 print("refine waves", st[4], "fallback waves", st[5], "refine lane-walks", st[6], "lanes left", st[7])
+for f, name in enumerate(("1 grid", "2 first walk", "2b grouped", "3 passes/dT")):
+    print(f"phase {name}: walk wave-steps {st[8 + 2 * f]} active lanes/step {st[9 + 2 * f] / max(st[8 + 2 * f], 1):.2f}")
