@@ -322,14 +322,14 @@ __device__ unsigned long long g_render_stats[kRenderStats];
 #define GSR_STRIP_CULL 0
 #endif
 
-// Wave-uniform composite loop (render path): every lane of the wave walks
-// every record of the batch, its per-lane early-outs folded into predicates
-// (blend = passes the power / alpha tests, not saturated, not done), and the
-// blending work is skipped only when no lane of the wave blends.  The
-// accumulators take fma(col, a T, C) with a T = 0 on non-blending lanes:
-// C + 0 = C exactly for the finite colours and normals the preprocess writes.
-#ifndef GSR_COMP_UNIFORM
-#define GSR_COMP_UNIFORM 0
+#ifndef GSR_WALK_PREFETCH
+#define GSR_WALK_PREFETCH 0  // (variant) the median-depth walks request the next contributor pair ahead
+#endif
+// Composite record prefetch: the next record's footprint words are read from
+// LDS while the current one is worked (the loop otherwise waits on the read at
+// the top of every step).
+#ifndef GSR_COMP_PREFETCH
+#define GSR_COMP_PREFETCH 0
 #endif
 
 // Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
@@ -503,45 +503,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         T = test_T;
         last = (uint32_t)g + 1u;  // the reference's 1-based contributor index
     };
-    // GSR_COMP_UNIFORM: one record for the whole wave (see above)
-    auto ustep = [&](int j, int g) {
-        const float4 w0 = s_w0[j], w1 = s_w1[j];
-        const float dx = w0.x - pixx, dy = w0.y - pixy;
-        const float power = splat_power(w0, w1, dx, dy);
-        const float alpha = fminf(0.99f, w1.y * __expf(power));
-        const float test_T = T * (1.f - alpha);
-        const bool pass = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-        const bool sat = test_T < 0.0001f;
-        const bool blend = pass && !sat && !done;
-        done = done || (pass && sat);
-        const unsigned long long bm = __ballot(blend);
-        if (bm == 0ull) return;  // (wave-uniform)
-        const float aT = blend ? alpha * T : 0.f;
-        if constexpr (!GEOM) {
-            if (g < kBlendWords * 32 && (tid & 63) == __builtin_ctzll(bm)) atomicOr(&s_union[g >> 5], 1u << (g & 31));
-        }
-        const float4 w2 = s_w2[j], w3 = s_w3[j];
-        C0 = __builtin_fmaf(w2.z, aT, C0);
-        C1 = __builtin_fmaf(w2.w, aT, C1);
-        C2 = __builtin_fmaf(w3.x, aT, C2);
-        if constexpr (GEOM) {
-            N0 = __builtin_fmaf(w3.y, aT, N0);
-            N1 = __builtin_fmaf(w3.z, aT, N1);
-            N2 = __builtin_fmaf(w3.w, aT, N2);
-            const float t = splat_tpeak(w1, w2, dx, dy);
-            m_init = (blend && T > 0.5f) ? t : m_init;
-            if (g < kResident) {
-                if ((g >> 5) != mask_w) {  // (g is wave-uniform: so is the word switch)
-                    my_mask[mask_w * kTilePixels] = mask_cur;
-                    mask_cur = 0u;
-                    mask_w = g >> 5;
-                }
-                mask_cur |= blend ? 1u << (g & 31) : 0u;
-            }
-        }
-        T = blend ? test_T : T;
-        last = blend ? (uint32_t)g + 1u : last;
-    };
     int toDo = total;
     for (int i = 0; i < rounds; i++, toDo -= kBatch) {
         // block-wide early exit: every wave publishes whether any lane is live
@@ -577,10 +538,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 }
                 step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
             }
-        } else if constexpr (GSR_COMP_UNIFORM && !SAMPLE) {
-            for (int j = 0; j < n; j++) {
-                if (__ballot(!done) == 0ull) break;
-                ustep(j, i * kBatch + j);
+        } else if constexpr (GSR_COMP_PREFETCH) {
+            float4 nw0 = s_w0[0], nw1 = s_w1[0];
+            for (int j = 0; !done && j < n; j++) {
+                const float4 w0 = nw0, w1 = nw1;
+                const int jn = j + 1 < n ? j + 1 : j;
+                nw0 = s_w0[jn];
+                nw1 = s_w1[jn];
+                step(w0, w1, [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
             }
         } else {
             for (int j = 0; !done && j < n; j++)
@@ -696,6 +661,52 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             const int nwords = active ? (int)((plast + 31) >> 5) : 0;
             int w = 0;
             uint32_t bits = nwords ? (mask[0] & filter) : 0u;
+#if GSR_WALK_PREFETCH
+            // (variant) the next pair's footprint words requested before the current pair is worked
+            auto next = [&](int& j1, int& j2, bool& two) {
+                while (bits == 0u && w + 1 < nwords) bits = mask[++w * kTilePixels] & filter;
+                if (bits == 0u) return false;
+                j1 = (w << 5) + __builtin_ctz(bits);
+                bits &= bits - 1u;
+                two = bits != 0u;
+                j2 = two ? (w << 5) + __builtin_ctz(bits) : j1;
+                bits &= bits - 1u;
+                return true;
+            };
+            int n1 = 0, n2 = 0;
+            bool ntwo = false;
+            bool have = next(n1, n2, ntwo);
+            float4 na0 = c_w0[n1], nb0 = c_w0[n2], na1 = c_w1[n1], nb1 = c_w1[n2];
+            while (have) {
+                const int j1 = n1, j2 = n2;
+                const bool two = ntwo;
+                const float4 a0 = na0, b0 = nb0, a1 = na1, b1 = nb1;
+                have = next(n1, n2, ntwo);
+                if (have) {
+                    na0 = c_w0[n1];
+                    nb0 = c_w0[n2];
+                    na1 = c_w1[n1];
+                    nb1 = c_w1[n2];
+                }
+                if constexpr (STATS) {
+                    const unsigned long long m = __ballot(1);
+                    if ((tid & 63) == __builtin_ctzll(m)) {
+                        st[0] += 1;
+                        st[1] += __popcll(m);
+                        st[8 + 2 * st_phase] += 1;
+                        st[9 + 2 * st_phase] += __popcll(m);
+                    }
+                }
+                const float adx = a0.x - ppx, ady = a0.y - ppy;
+                const float bdx = b0.x - ppx, bdy = b0.y - ppy;
+                const float alpha_a = fminf(0.99f, a1.y * __expf(splat_power(a0, a1, adx, ady)));
+                const float alpha_b = two ? fminf(0.99f, b1.y * __expf(splat_power(b0, b1, bdx, bdy))) : 0.f;
+                const float4 a2 = c_w2[j1], b2 = c_w2[j2];
+                body(alpha_a, splat_tpeak(a1, a2, adx, ady), a2);
+                body(alpha_b, splat_tpeak(b1, b2, bdx, bdy), b2);
+            }
+            return;
+#endif
             while (true) {
                 while (bits == 0u && w + 1 < nwords) bits = mask[++w * kTilePixels] & filter;
                 if (bits == 0u) break;

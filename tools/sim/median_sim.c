@@ -688,6 +688,7 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
             const uint32_t* point_list, const float* xy, const float* co, const float* rp, int nk, const float* off,
             float tol_rel, int maxit, float hnoise, double* out) {
     contrib_t* buf = malloc(sizeof(contrib_t) * 65536);
+    const int G = getenv("SIM_GRID") ? atoi(getenv("SIM_GRID")) : 2;  /* grid stride of phase 1 */
     for (int ti = 0; ti < ntiles; ti++) {
         const uint32_t tile = tiles[ti];
         const uint32_t tx = tile % gx, ty = tile / gx;
@@ -700,7 +701,7 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
             have[l] = 0;
             walksv[l] = 0;
             const int lx = l & 15, ly = l >> 4;
-            if ((lx & 1) || (ly & 1)) continue;
+            if ((lx % G) || (ly % G)) continue;
             const int px = tx * 16 + lx, py = ty * 16 + ly;
             if (px >= W || py >= H) continue;
             float Tf, m0;
@@ -756,7 +757,7 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
         int lane = 0, wmax2 = 0;
         for (int l = 0; l < 256; l++) {
             const int lx = l & 15, ly = l >> 4;
-            if (!((lx & 1) || (ly & 1))) continue;
+            if (!((lx % G) || (ly % G))) continue;
             const int px = tx * 16 + lx, py = ty * 16 + ly;
             int wk = 0;
             if (px < W && py < H) {
@@ -766,13 +767,18 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
                 const float mr = ref_bisect(buf, n, m0, Tf, &ir);
                 if (ir) {
                     out[0] += 1;
-                    float sum = 0.f;
-                    int cnt = 0;
-                    for (int yy = ly - (ly & 1); yy <= ly + (ly & 1); yy += 2)
-                        for (int xx = lx - (lx & 1); xx <= lx + (lx & 1); xx += 2)
+                    float sum = 0.f, cnt = 0.f;
+                    /* bilinear over the surrounding grid pixels present (G = 2: the mean of the 1, 2 or 4 of them) */
+                    const int x0g = lx - lx % G, y0g = ly - ly % G;
+                    for (int yy = y0g; yy <= y0g + G; yy += G)
+                        for (int xx = x0g; xx <= x0g + G; xx += G)
                             if (yy >= 0 && yy < 16 && xx >= 0 && xx < 16 && have[yy * 16 + xx]) {
-                                sum += root[yy * 16 + xx];
-                                cnt++;
+                                const float wx = xx == x0g ? (float)(G - lx % G) : (float)(lx % G);
+                                const float wy = yy == y0g ? (float)(G - ly % G) : (float)(ly % G);
+                                const float wgt = wx * wy;
+                                if (wgt <= 0.f) continue;
+                                sum += wgt * root[yy * 16 + xx];
+                                cnt += wgt;
                             }
                     const float dmin = fmaxf(m0 - RANGE, 0.f), dmax = fmaxf(m0 + RANGE, 0.f);
                     float res = mr;
@@ -781,6 +787,7 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
                         wk = 100;
                     } else {
                         const float t0 = fminf(fmaxf(sum / cnt, dmin), dmax);
+                        (void)0;
                         wk = halley_from(buf, n, t0, dmin, dmax, tol_rel, maxit, hnoise, &res);
                         if (wk < 0) { out[2] += 1; res = mr; wk = 100; }
                     }
