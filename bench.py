@@ -59,6 +59,11 @@ SIMDS = 256 * 4  # 256 CUs x 4 SIMD-32
 # (v_exp / v_rsq / v_rcp / v_sqrt / v_log) twice that (one wave alone: 8)
 VALU_PEAK_CYCLES = 2
 TRANS_PEAK_CYCLES = 4
+# The plain-VALU issue rate measured on the box (tools/probe/valu_rate.hip, profiles/r4_valu_rate_probe.txt):
+# 16 independent v_fma_f32 chains per wave at 8 waves per SIMD sustain 4.41 cycles per wave64 instruction
+# per SIMD (2.4 GHz assumed, like the rates above) — the datasheet's 2 is not reached by plain fp32 code;
+# v_pk_fma_f32 (two fmas per lane) issues at about the same rate.
+VALU_MEASURED_CYCLES = 4.41
 
 
 def log(*a):
@@ -589,7 +594,10 @@ def main():
                     "frac": round(valu_frac, 4), "insts_per_launch": int(valu_insts),
                     "trans_insts_per_launch": None if trans_insts is None else int(trans_insts),
                     "peak_cycles_per_inst": VALU_PEAK_CYCLES, "peak_cycles_per_trans": TRANS_PEAK_CYCLES,
-                    "clock_hz": CLOCK_HZ, "simds": SIMDS},
+                    "clock_hz": CLOCK_HZ, "simds": SIMDS,
+                    "frac_of_measured_issue_rate": round(valu_insts * VALU_MEASURED_CYCLES / simd_cycles, 4),
+                    "measured_cycles_per_inst": VALU_MEASURED_CYCLES,
+                    "measured_source": "profiles/r4_valu_rate_probe.txt"},
                 "pmc_source": None if pmc_file is None else f"profiles/{pmc_file}",
                 "stage_ms": {k: round(v, 4) for k, v in per_launch.items()}}
     total_algo = sum(v for k, v in algo.items() if per_launch.get(k, 0.0) > 0.0)  # the stages this step ran
