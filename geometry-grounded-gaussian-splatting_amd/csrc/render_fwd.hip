@@ -175,11 +175,18 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
 // passes.  (The previous scheme ran the reference's first two passes and
 // refined from the pass-2 cell: one more 7-sample walk per contributor.)
 #ifndef GSR_PROBES
-#define GSR_PROBES 11
+#define GSR_PROBES 9  // (11: 0.769 -> 0.758 ms render_fwd at C3 with 9, profiles/r4_ab_probes.txt)
 #endif
-constexpr int kProbes = GSR_PROBES;  // 11 or 7 (the window ends, m0 and 8 or 4 offsets around it)
+constexpr int kProbes = GSR_PROBES;  // 11 or 7 (the window ends, m0 and 8 or 4 offsets around it); 9 (no ends)
+// With 9 probes the window ends are not sampled: T is non-increasing in t, so a bracket between the
+// inner probes (m0 -/+ SAMPLE_RANGE / 2) implies the reference's in_range test (T(e0) >= 1/2 >= T(e8));
+// a pixel whose root lies outside them is left to the reference's passes.
+constexpr bool kProbeEnds = kProbes != 9;
 #if GSR_PROBES == 7
 __constant__ constexpr float kProbeOffsets[kProbes] = {0.f, -0.5f, -0.125f, 0.f, 0.125f, 0.5f, 0.f};
+#elif GSR_PROBES == 9
+__constant__ constexpr float kProbeOffsets[kProbes] = {-0.5f, -0.25f, -0.125f, -0.0625f, 0.f,
+                                                        0.0625f, 0.125f, 0.25f, 0.5f};
 #else
 __constant__ constexpr float kProbeOffsets[kProbes] = {0.f,    -0.5f,   -0.25f, -0.125f, -0.0625f, 0.f,
                                                         0.0625f, 0.125f, 0.25f,  0.5f,    0.f};
@@ -322,16 +329,6 @@ __device__ unsigned long long g_render_stats[kRenderStats];
 #define GSR_STRIP_CULL 0
 #endif
 
-#ifndef GSR_WALK_PREFETCH
-#define GSR_WALK_PREFETCH 0  // (variant) the median-depth walks request the next contributor pair ahead
-#endif
-// Composite record prefetch: the next record's footprint words are read from
-// LDS while the current one is worked (the loop otherwise waits on the read at
-// the top of every step).
-#ifndef GSR_COMP_PREFETCH
-#define GSR_COMP_PREFETCH 0
-#endif
-
 // Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
 // pixel rows [y0 + 4 s, y0 + 4 s + 3] x columns [x0, x0 + 15].
 __device__ __forceinline__ uint32_t strip_bits(const float4& w0, const float4& w1, int x0, int y0) {
@@ -376,6 +373,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
+    // (development, STATS builds with -DGSR_PHASE_CLOCK=1: shader clocks at the render path's phase
+    // boundaries, summed per wave into render stats [8..13] in place of the per-phase walk counts)
+#ifndef GSR_PHASE_CLOCK
+#define GSR_PHASE_CLOCK 0
+#endif
+    constexpr bool kClock = GSR_PHASE_CLOCK && STATS && !SAMPLE;
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+    auto stamp = [&](int k) {
+        if constexpr (kClock) ph[k] = clock64();
+    };
+    stamp(0);
     uint32_t tile, chunk = 0, pid = 0;
     int px = 0, py = 0;
     bool inside;
@@ -538,21 +546,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 }
                 step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
             }
-        } else if constexpr (GSR_COMP_PREFETCH) {
-            float4 nw0 = s_w0[0], nw1 = s_w1[0];
-            for (int j = 0; !done && j < n; j++) {
-                const float4 w0 = nw0, w1 = nw1;
-                const int jn = j + 1 < n ? j + 1 : j;
-                nw0 = s_w0[jn];
-                nw1 = s_w1[jn];
-                step(w0, w1, [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
-            }
         } else {
             for (int j = 0; !done && j < n; j++)
                 step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
         }
     }
 
+    stamp(1);
     if constexpr (GEOM) {
         my_mask[mask_w * kTilePixels] = mask_cur;
         if constexpr (!SAMPLE) {  // the tile's union of the blended sets (the lane's own column: no barrier)
@@ -661,52 +661,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             const int nwords = active ? (int)((plast + 31) >> 5) : 0;
             int w = 0;
             uint32_t bits = nwords ? (mask[0] & filter) : 0u;
-#if GSR_WALK_PREFETCH
-            // (variant) the next pair's footprint words requested before the current pair is worked
-            auto next = [&](int& j1, int& j2, bool& two) {
-                while (bits == 0u && w + 1 < nwords) bits = mask[++w * kTilePixels] & filter;
-                if (bits == 0u) return false;
-                j1 = (w << 5) + __builtin_ctz(bits);
-                bits &= bits - 1u;
-                two = bits != 0u;
-                j2 = two ? (w << 5) + __builtin_ctz(bits) : j1;
-                bits &= bits - 1u;
-                return true;
-            };
-            int n1 = 0, n2 = 0;
-            bool ntwo = false;
-            bool have = next(n1, n2, ntwo);
-            float4 na0 = c_w0[n1], nb0 = c_w0[n2], na1 = c_w1[n1], nb1 = c_w1[n2];
-            while (have) {
-                const int j1 = n1, j2 = n2;
-                const bool two = ntwo;
-                const float4 a0 = na0, b0 = nb0, a1 = na1, b1 = nb1;
-                have = next(n1, n2, ntwo);
-                if (have) {
-                    na0 = c_w0[n1];
-                    nb0 = c_w0[n2];
-                    na1 = c_w1[n1];
-                    nb1 = c_w1[n2];
-                }
-                if constexpr (STATS) {
-                    const unsigned long long m = __ballot(1);
-                    if ((tid & 63) == __builtin_ctzll(m)) {
-                        st[0] += 1;
-                        st[1] += __popcll(m);
-                        st[8 + 2 * st_phase] += 1;
-                        st[9 + 2 * st_phase] += __popcll(m);
-                    }
-                }
-                const float adx = a0.x - ppx, ady = a0.y - ppy;
-                const float bdx = b0.x - ppx, bdy = b0.y - ppy;
-                const float alpha_a = fminf(0.99f, a1.y * __expf(splat_power(a0, a1, adx, ady)));
-                const float alpha_b = two ? fminf(0.99f, b1.y * __expf(splat_power(b0, b1, bdx, bdy))) : 0.f;
-                const float4 a2 = c_w2[j1], b2 = c_w2[j2];
-                body(alpha_a, splat_tpeak(a1, a2, adx, ady), a2);
-                body(alpha_b, splat_tpeak(b1, b2, bdx, bdy), b2);
-            }
-            return;
-#endif
             while (true) {
                 while (bits == 0u && w + 1 < nwords) bits = mask[++w * kTilePixels] & filter;
                 if (bits == 0u) break;
@@ -846,10 +800,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             float t_ref, ref_t, ref_D, ref_E;
             float t, lo, hi;
         };
+        // One walk's update of a live pixel: log2 T, its derivatives -D, E and the curvature bound F at t
+        // (the products and sums of the walk), the bracket, the Halley iterate, and acceptance.
+        auto root_update = [&](Refine& r, bool& live, float& t, float& lo, float& hi, float A, float B, float D, float E,
+                               float F, float scale) {
+            const float tol = kRefineTol * scale, tol_cond = kCondTol * scale, tol_loose = kLooseTol * scale;
+            if constexpr (STATS) st[6] += 1;
+            const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
+            if (H >= 0.f) lo = t;
+            else hi = t;
+            // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
+            const float th = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
+            const bool halley_in = th >= lo && th <= hi;
+            float tn = halley_in ? th : 0.5f * (lo + hi);
+            // (converged by the Newton step, or by the bracket closing — the latter also at a jump of T
+            // across 1/2, where H need not be small)
+            const bool newton = (D > 0.f && fabsf(H) <= tol * D) ||
+                                (D > 0.f && fabsf(H) <= tol_loose * D && fabsf(H) * F <= kCurvTol * D * D);
+            const bool done = newton || hi - lo <= tol;
+            if (done) {
+                // accepted only where the root is well conditioned: rounding noise of
+                // ~kHNoise in log2 T moves it by less than tol_cond (T flat near 1/2 — a
+                // pixel between two splats' peaks — leaves it to the reference's passes)
+                r.refined = D * tol_cond >= kHNoise;
+                // (an ill-conditioned root only where T itself is at 1/2: converged by the Newton step)
+                r.ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
+                // (converged by the Newton test with the Halley iterate out of the bracket — H'' large
+                // against H' near a splat's peak — the root is the Newton iterate, not the midpoint)
+                r.t_ref = newton && !halley_in ? fminf(fmaxf(t + fast_div(H, D), lo), hi) : tn;
+                live = false;
+                r.ref_t = t;
+                r.ref_D = D;
+                r.ref_E = E;
+            }
+            t = tn;
+        };
         auto halley = [&](auto&& src, bool grouped, bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
                           int walks, float scale) {
             Refine r{false, false, in_range0, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            const float tol = kRefineTol * scale, tol_cond = kCondTol * scale, tol_loose = kLooseTol * scale;
             const f32x2 TSE[1] = {f32x2{e0, e8}};
             for (int k = 0; k < walks && a.passes > 1; k++) {
                 if (__ballot(live) == 0ull) break;
@@ -879,37 +867,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     r.in_range = r.in_range && T0 >= 0.5f && T8 <= 0.5f;
                     live = live && r.in_range;
                 }
-                if (live) {
-                    if constexpr (STATS) st[6] += 1;
-                    const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
-                    if (H >= 0.f) lo = t;
-                    else hi = t;
-                    // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
-                    const float th = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
-                    const bool halley_in = th >= lo && th <= hi;
-                    float tn = halley_in ? th : 0.5f * (lo + hi);
-                    // (converged by the Newton step, or by the bracket closing — the latter also at a jump of T
-                    // across 1/2, where H need not be small)
-                    const bool newton = (D > 0.f && fabsf(H) <= tol * D) ||
-                                        (D > 0.f && fabsf(H) <= tol_loose * D && fabsf(H) * F <= kCurvTol * D * D);
-                    const bool done = newton || hi - lo <= tol;
-                    if (done) {
-                        // accepted only where the root is well conditioned: rounding noise of
-                        // ~kHNoise in log2 T moves it by less than tol_cond (T flat near 1/2 — a
-                        // pixel between two splats' peaks — leaves it to the reference's passes)
-                        r.refined = D * tol_cond >= kHNoise;
-                        // (an ill-conditioned root only where T itself is at 1/2: converged by the Newton step)
-                        r.ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
-                        // (converged by the Newton test with the Halley iterate out of the bracket — H'' large
-                        // against H' near a splat's peak — the root is the Newton iterate, not the midpoint)
-                        r.t_ref = newton && !halley_in ? fminf(fmaxf(t + fast_div(H, D), lo), hi) : tn;
-                        live = false;
-                        r.ref_t = t;
-                        r.ref_D = D;
-                        r.ref_E = E;
-                    }
-                    t = tn;
-                }
+                if (live) root_update(r, live, t, lo, hi, A, B, D, E, F, scale);
             }
             if (a.passes == 1 && r.in_range) {  // diagnostic timing of the probe walk alone
                 r.refined = true;
@@ -933,7 +891,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
 #pragma unroll
             for (int s = 0; s < kProbes; s++) {
                 const float off = kProbeOffsets[s] * a.sample_range;
-                tp[s] = s == 0 ? e0 : s == kProbes - 1 ? e8 : fminf(fmaxf(pm0 + off, e0), e8);
+                tp[s] = kProbeEnds && s == 0 ? e0 : kProbeEnds && s == kProbes - 1 ? e8 : fminf(fmaxf(pm0 + off, e0), e8);
             }
             // the m0 probe is the scalar sample, the others go in packed pairs
             constexpr int NP = (kProbes - 1) / 2, MID = (kProbes - 1) / 2;
@@ -958,7 +916,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 Tv[s1] = gprod(A[k].y, grouped) * __builtin_amdgcn_rsqf(gprod(B[k].y, grouped));
             }
             Tv[MID] = gprod(A1, grouped) * __builtin_amdgcn_rsqf(gprod(B1, grouped));
-            pin = (Tv[0] >= 0.5f) && (Tv[kProbes - 1] <= 0.5f) && pin;
+            const bool bracketed = (Tv[0] >= 0.5f) && (Tv[kProbes - 1] <= 0.5f);
+            if constexpr (kProbeEnds) pin = bracketed && pin;
             // bracket: the last probe with T >= 1/2 and the next one
             int k1 = 0;
 #pragma unroll
@@ -977,7 +936,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             float wsec = Hlo / (Hlo - Hhi);
             wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
             const float t = __builtin_fmaf(wsec, hi - lo, lo);
-            return halley(src, grouped, pin, t, lo, hi, false, 0.f, 0.f, pin, kRefineWalks,
+            return halley(src, grouped, pin && bracketed, t, lo, hi, false, 0.f, 0.f, pin, kRefineWalks,
                           fmaxf(t, 1.f));
         };
         bool have_out = false;  // (render path) md_out and dT/dt_m published by the pixel's worker
@@ -1039,27 +998,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     }
                 }
                 __syncthreads();
+                stamp(2);
                 const int skip = (int)(blockIdx.x & 3u);  // the wave left idle (rotated over the SIMDs)
                 if constexpr (STATS) st_phase = 1;
                 bool live2 = false;  // phase-2 pixel not converged after its first walk
                 int p2 = 0;
-                if (wave != skip) {  // phase 2, first walk
-                    const int k = (wave < skip ? wave : wave - 1) * 64 + (tid & 63);
-                    const int pair = k / 24, r24 = k - pair * 24;
-                    const int lx = r24 < 8 ? 2 * r24 + 1 : r24 - 8, ly = r24 < 8 ? 2 * pair : 2 * pair + 1;
-                    const int p = ly * 16 + lx;
-                    p2 = p;
-                    const float qx = (float)(x0 + lx), qy = (float)(y0 + ly);
-                    const uint32_t ql = s_pub_last[p];
-                    const float qm0 = s_pub_m0[p], qT = s_pub_T[p];
-                    float sum = 0.f;
-                    int cnt = 0;
+                // the grid neighbours' mean root of a phase-2 pixel: the pixel itself on even coordinates,
+                // both sides on odd ones
+                auto guess = [&](int lx, int ly, float& sum, int& cnt) {
+                    sum = 0.f;
+                    cnt = 0;
 #pragma unroll
                     for (int dy = -1; dy <= 1; dy++)
 #pragma unroll
                         for (int dx = -1; dx <= 1; dx++) {
                             const int nx = lx + dx, ny = ly + dy;
-                            // grid neighbours: the pixel itself on even coordinates, both sides on odd
                             const bool use = ((lx & 1) ? dx != 0 : dx == 0) && ((ly & 1) ? dy != 0 : dy == 0);
                             if (use && nx >= 0 && nx < 16 && ny >= 0 && ny < 16) {
                                 const float gr = s_groot[(ny >> 1) * 8 + (nx >> 1)];
@@ -1069,6 +1022,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                                 }
                             }
                         }
+                };
+                if (wave != skip) {  // phase 2, first walk
+                    const int k = (wave < skip ? wave : wave - 1) * 64 + (tid & 63);
+                    const int pair = k / 24, r24 = k - pair * 24;
+                    const int lx = r24 < 8 ? 2 * r24 + 1 : r24 - 8, ly = r24 < 8 ? 2 * pair : 2 * pair + 1;
+                    const int p = ly * 16 + lx;
+                    p2 = p;
+                    const float qx = (float)(x0 + lx), qy = (float)(y0 + ly);
+                    const uint32_t ql = s_pub_last[p];
+                    const float qm0 = s_pub_m0[p], qT = s_pub_T[p];
+                    float sum;
+                    int cnt;
+                    guess(lx, ly, sum, cnt);
                     const bool qin = qT <= kMinTransmittance;
                     const float lo_w = fmaxf(qm0 - a.sample_range, 0.f), hi_w = fmaxf(qm0 + a.sample_range, 0.f);
                     const float interval = (hi_w - lo_w) * (1.f / (float)kSplit);
@@ -1094,6 +1060,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 // The pixels not converged after one walk (~30% at C3), compacted and continued by
                 // groups of 4 lanes (as phase 1): their second walk no longer holds every lane of
                 // the three phase-2 waves.
+                stamp(3);
                 const unsigned long long bl = __ballot(live2);
                 if ((tid & 63) == 0) s_max[wave] = (uint32_t)__popcll(bl);
                 __syncthreads();  // also: every phase-2 lane has read s_groot
@@ -1123,6 +1090,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     if ((tid & 3) == 0) publish(s_list[opaque_int((int)e)], r);
                 }
                 __syncthreads();
+                stamp(4);
                 const int me = opaque_int(tid);
                 const uint32_t flags = s_pub_last[me];
                 const bool ill = (flags & kPubIll) != 0u;  // root in s_pub_T[me]; dT/dt_m by the walk below
@@ -1261,6 +1229,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             for (int it = 1; it < a.passes; it++) pass(std::false_type{}, own_src);
         }
         if constexpr (STATS) {
+            stamp(5);
+            if constexpr (kClock) {
+#pragma unroll
+                for (int k = 0; k < 5; k++) st[8 + k] = (tid & 63) == 0 ? ph[k + 1] - ph[k] : 0ull;
+                st[13] = (tid & 63) == 0 ? ph[5] - ph[0] : 0ull;
+                st[14] = st[15] = 0ull;
+            }
             for (int q = 0; q < kRenderStats; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);
         }
