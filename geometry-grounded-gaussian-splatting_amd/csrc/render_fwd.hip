@@ -437,6 +437,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     if constexpr (!SAMPLE) {
         if (tid < kBlendWords) s_union[tid] = 0u;  // (ordered by the first batch's barrier)
     }
+    uint32_t wbits = 0u;  // (render path, no depth) the lane's blended entries of the current 32-entry word
     float T = 1.0f, T_pt = 1.0f;
     uint32_t last = 0;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
@@ -469,12 +470,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             if ((tid & 63) == __builtin_ctzll(m)) cst[1] += __popcll(m);
         }
         const float aT = alpha * T;
-        if constexpr (!SAMPLE && !GEOM) {  // (GEOM: from the blended-set masks after the composite)
-            if (g < kBlendWords * 32) {
-                const unsigned long long m = __ballot(1);
-                if ((tid & 63) == __builtin_ctzll(m)) atomicOr(&s_union[g >> 5], 1u << (g & 31));
-            }
-        }
+        if constexpr (!SAMPLE && !GEOM) wbits |= 1u << (g & 31);  // (GEOM: from the blended-set masks)
         const float4 w2 = w2f();
         if constexpr (SAMPLE && !GEOM) {
             // vacancy transmittance at the point (sample_forward.cu:152-160)
@@ -547,8 +543,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
             }
         } else {
-            for (int j = 0; !done && j < n; j++)
-                step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+            if constexpr (!GEOM && !SAMPLE) {
+                // no depth: the batch in 32-entry words, each word's blended bits ORed over the wave
+                // (DPP) and set by one lane (one atomic per blending step: render_fwd 0.214 -> 0.181 ms
+                // without depth at C3; with no mask at all the backward walks every entry: 0.34 -> 0.40 ms)
+                for (int j0 = 0; j0 < n; j0 += 32) {
+                    wbits = 0u;
+                    const int j1 = min(n, j0 + 32);
+                    for (int j = j0; !done && j < j1; j++)
+                        step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+                    const int word = (i * kBatch + j0) >> 5;
+                    if (word < kBlendWords) {
+                        const uint32_t v = wave_or_dpp(wbits);
+                        if ((tid & 63) == 0 && v) atomicOr(&s_union[word], v);
+                    }
+                }
+            } else {
+                for (int j = 0; !done && j < n; j++)
+                    step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+            }
         }
     }
 
