@@ -379,7 +379,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
 #define GSR_PHASE_CLOCK 0
 #endif
     constexpr bool kClock = GSR_PHASE_CLOCK && STATS && !SAMPLE;
-    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     auto stamp = [&](int k) {
         if constexpr (kClock) ph[k] = clock64();
     };
@@ -921,6 +921,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, pin, [&](float alpha, float t_peak, float4 w2) {
                 bisect_step<NP, true>(A, B, TS, A1, B1, tp[MID], alpha, t_peak, w2.y, w2.z, w2.w);
             });
+            stamp(3);
             float Tv[kProbes];
 #pragma unroll
             for (int k = 0; k < NP; k++) {
@@ -973,6 +974,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 s_pub_m0[tid] = m_init;
                 s_pub_T[tid] = T;
                 __syncthreads();
+                stamp(2);
                 auto publish = [&](int p, const Refine& r) {
                     p = opaque_int(p);  // (the LDS addresses at the store, not kept from the reads)
                     uint32_t flags = r.in_range ? 0u : kPubOut;
@@ -1011,7 +1013,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     }
                 }
                 __syncthreads();
-                stamp(2);
+                stamp(4);
                 const int skip = (int)(blockIdx.x & 3u);  // the wave left idle (rotated over the SIMDs)
                 if constexpr (STATS) st_phase = 1;
                 bool live2 = false;  // phase-2 pixel not converged after its first walk
@@ -1073,7 +1075,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 // The pixels not converged after one walk (~30% at C3), compacted and continued by
                 // groups of 4 lanes (as phase 1): their second walk no longer holds every lane of
                 // the three phase-2 waves.
-                stamp(3);
+                stamp(5);
                 const unsigned long long bl = __ballot(live2);
                 if ((tid & 63) == 0) s_max[wave] = (uint32_t)__popcll(bl);
                 __syncthreads();  // also: every phase-2 lane has read s_groot
@@ -1103,7 +1105,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     if ((tid & 3) == 0) publish(s_list[opaque_int((int)e)], r);
                 }
                 __syncthreads();
-                stamp(4);
+                stamp(6);
                 const int me = opaque_int(tid);
                 const uint32_t flags = s_pub_last[me];
                 const bool ill = (flags & kPubIll) != 0u;  // root in s_pub_T[me]; dT/dt_m by the walk below
@@ -1242,12 +1244,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             for (int it = 1; it < a.passes; it++) pass(std::false_type{}, own_src);
         }
         if constexpr (STATS) {
-            stamp(5);
+            stamp(7);
             if constexpr (kClock) {
 #pragma unroll
-                for (int k = 0; k < 5; k++) st[8 + k] = (tid & 63) == 0 ? ph[k + 1] - ph[k] : 0ull;
-                st[13] = (tid & 63) == 0 ? ph[5] - ph[0] : 0ull;
-                st[14] = st[15] = 0ull;
+                for (int k = 0; k < 7; k++) st[8 + k] = (tid & 63) == 0 ? ph[k + 1] - ph[k] : 0ull;
+                st[15] = (tid & 63) == 0 ? ph[7] - ph[0] : 0ull;
             }
             for (int q = 0; q < kRenderStats; q++)
                 if (st[q]) atomicAdd(&g_render_stats[q], st[q]);

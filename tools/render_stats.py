@@ -28,10 +28,12 @@ print("composite wave-steps", st[2], "blending lanes/step", round(st[3] / max(st
 print(f"P={P} {W}x{H}")
 print("refine waves", st[4], "fallback waves", st[5], "refine lane-walks", st[6], "lanes left", st[7])
 if os.environ.get("GSR_PHASE_CLOCK"):  # a -DGSR_PHASE_CLOCK=1 build: per-wave clock sums by phase
-    names = ("composite", "phase 1", "phase 2", "phase 2b", "phase 3", "total to phase-3 end")
-    tot = max(st[13], 1)
+    names = ("composite", "outputs, staging, publish", "phase 1 probe walk", "phase 1 Halley walks", "phase 2",
+             "phase 2b", "phase 3")
+    tot = max(st[15], 1)
     for k, name in enumerate(names):
         print(f"clock {name}: {st[8 + k]:.4g} wave-cycles ({st[8 + k] / tot:.3f})")
+    print(f"clock total to phase-3 end: {st[15]:.4g}")
     sys.exit(0)
 for f, name in enumerate(("1 grid", "2 first walk", "2b grouped", "3 passes/dT")):
     print(f"phase {name}: walk wave-steps {st[8 + 2 * f]} active lanes/step {st[9 + 2 * f] / max(st[8 + 2 * f], 1):.2f}")

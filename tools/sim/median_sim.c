@@ -658,6 +658,7 @@ void sim_ref_depths(int W, int H, int gx, int ntiles, const uint32_t* tiles, con
 static long g_why_ill, g_why_nc, g_why_ok;  /* fallback reasons: ill-conditioned / not converged */
 static double g_why_D[8];  /* ill-conditioned: histogram of log10(D * scale) */
 void sim_why(long* o) { o[0] = g_why_ok; o[1] = g_why_ill; o[2] = g_why_nc; for (int i = 0; i < 8; i++) o[3 + i] = (long)g_why_D[i]; }
+static float g_last_t, g_last_lo, g_last_hi;  /* the iterate and bracket a non-converged call stopped at */
 static int halley_from(const contrib_t* c, int n, float t, float lo, float hi, float tol_rel, int maxit,
                        float hnoise, float* res) {
     const float tol = tol_rel * fmaxf(t, 1.f);
@@ -680,6 +681,9 @@ static int halley_from(const contrib_t* c, int n, float t, float lo, float hi, f
             return -walks;
         }
         t = tn;
+        g_last_t = t;
+        g_last_lo = lo;
+        g_last_hi = hi;
     }
     g_why_nc++;
     return -walks;
@@ -734,6 +738,38 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
             float w = hs[k1] / (hs[k1] - hs[k1 + 1]);
             w = (w != w) ? 0.5f : fminf(fmaxf(w, 0.f), 1.f);
             float t0 = ts[k1] + w * (ts[k1 + 1] - ts[k1]);
+            if (getenv("SIM_P1_INTERP")) {  /* variant: the root of the cubic through 4 probes around the bracket */
+                int a0 = k1 - 1;
+                if (a0 < 0) a0 = 0;
+                if (a0 + 3 > m - 1) a0 = m - 4;
+                if (a0 >= 0) {
+                    const float* X = ts + a0;
+                    const float* Y = hs + a0;
+                    int ok = 1;
+                    for (int q = 0; q < 3; q++) ok = ok && X[q + 1] > X[q];
+                    if (ok) {
+                        /* Newton on the Lagrange cubic from the secant guess, kept in the bracket */
+                        float x = t0;
+                        for (int it = 0; it < 8; it++) {
+                            double P = 0, dP = 0;
+                            for (int i = 0; i < 4; i++) {
+                                double li = 1, dli = 0;
+                                for (int j = 0; j < 4; j++) if (j != i) {
+                                    const double den = X[i] - X[j];
+                                    dli = dli * (x - X[j]) / den + li / den;
+                                    li *= (x - X[j]) / den;
+                                }
+                                P += Y[i] * li; dP += Y[i] * dli;
+                            }
+                            if (dP == 0) break;
+                            float xn = (float)(x - P / dP);
+                            if (!(xn >= ts[k1] && xn <= ts[k1 + 1])) break;
+                            x = xn;
+                        }
+                        t0 = x;
+                    }
+                }
+            }
             if (getenv("SIM_P1H")) {  /* variant: a Halley step from m0 (h, h', h'' taken in the probe walk) */
                 float h0, d1, d2;
                 const float tm = fminf(fmaxf(m0, dmin), dmax);
@@ -743,8 +779,29 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
                 if (th >= ts[k1] && th <= ts[k1 + 1]) t0 = th;
             }
             float res = mr;
-            int wk = halley_from(buf, n, t0, ts[k1], ts[k1 + 1], tol_rel, maxit, hnoise, &res);
+            /* SIM_P1_MAXIT=k: phase 1 stops after k Halley walks; a grid pixel not converged by then
+               publishes its current iterate as its neighbours' guess and continues in phase 2b */
+            const int k1max = getenv("SIM_P1_MAXIT") ? atoi(getenv("SIM_P1_MAXIT")) : maxit;
+            const long nc0 = g_why_nc;
+            int wk = halley_from(buf, n, t0, ts[k1], ts[k1 + 1], tol_rel, k1max, hnoise, &res);
+            if (wk < 0 && g_why_nc > nc0 && k1max < maxit) {
+                out[40] += 1;  /* stragglers */
+                const float tg = g_last_t;
+                float res2 = mr;
+                int wk2 = halley_from(buf, n, g_last_t, g_last_lo, g_last_hi, tol_rel, maxit - k1max, hnoise, &res2);
+                out[41] += wk2 < 0 ? -wk2 : wk2;
+                if (wk2 < 0) { out[2] += 1; res2 = mr; }
+                root[l] = tg;  /* (the guess phase 2 sees) */
+                have[l] = 1;
+                const double d = fabs((double)res2 - mr);
+                if (d > out[1]) out[1] = d;
+                wk = k1max;
+                if (wk > wmax1) wmax1 = wk;
+                out[32 + (wk < 7 ? wk : 7)] += 1;
+                continue;
+            }
             if (wk < 0) { out[2] += 1; res = mr; wk = 100; }
+            out[32 + (wk < 7 ? wk : 7)] += 1;
             root[l] = res;
             have[l] = 1;
             const double d = fabs((double)res - mr);
