@@ -329,6 +329,13 @@ __device__ unsigned long long g_render_stats[kRenderStats];
 #define GSR_STRIP_CULL 0
 #endif
 
+// Median-depth phases 2b and 3 (render path) give each listed pixel as many
+// lanes as one round of the block allows (up to 16), instead of 4 and 1.
+#ifndef GSR_ADAPT_GROUPS
+#define GSR_ADAPT_GROUPS 1
+#endif
+constexpr bool kAdaptGroups = GSR_ADAPT_GROUPS;
+
 // Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
 // pixel rows [y0 + 4 s, y0 + 4 s + 3] x columns [x0, x0 + 15].
 __device__ __forceinline__ uint32_t strip_bits(const float4& w0, const float4& w1, int x0, int y0) {
@@ -713,7 +720,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         // the lanes still in range and not refined; FIRST evaluates all 9
         // samples, later passes reuse the bracketing ends
         // (src: the pixel whose blended set the resident walk uses, PixSrc)
-        auto pass = [&](auto first_c, auto&& src) {
+        // A pixel may be worked by a group of G = 1, 2, 4, 8 or 16 aligned lanes (uniform over
+        // the wave): lane q walks the contributors with index % G == q (gfilter), and the group's
+        // products and sums are combined by DPP moves (xor 1, xor 2, half mirror, mirror: each
+        // step pairs the two halves of a doubled group), identical in the G lanes as float * and
+        // + commute — the same values, a different association than one lane's product.
+        auto gprod = [&](float v, int G) {
+            if (G >= 2) v *= dpp_mov<kDppXor1>(v);  // (DPP moves: no LDS addresses to keep)
+            if (G >= 4) v *= dpp_mov<kDppXor2>(v);
+            if (G >= 8) v *= dpp_mov<kDppRowHalfMirror>(v);
+            if (G >= 16) v *= dpp_mov<kDppRowMirror>(v);
+            return v;
+        };
+        auto gsum = [&](float v, int G) {
+            if (G >= 2) v += dpp_mov<kDppXor1>(v);
+            if (G >= 4) v += dpp_mov<kDppXor2>(v);
+            if (G >= 8) v += dpp_mov<kDppRowHalfMirror>(v);
+            if (G >= 16) v += dpp_mov<kDppRowMirror>(v);
+            return v;
+        };
+        // (the G lanes' share of a blended-set word, lane q of the group)
+        auto gfilter = [](int G, int q) -> uint32_t {
+            return G == 1 ? ~0u : G == 2 ? 0x55555555u << q : G == 4 ? 0x11111111u << q
+                 : G == 8 ? 0x01010101u << q : 0x00010001u << q;
+        };
+        auto pass = [&](auto first_c, auto&& src, int G) {
             constexpr bool FIRST = decltype(first_c)::value;
             constexpr int START = FIRST ? 0 : 1;
             constexpr int END = FIRST ? kSplit + 1 : kSplit;
@@ -764,10 +795,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             }
 #pragma unroll
             for (int k = 0; k < NP; k++) {
-                Tp[START + 2 * k] = A[k].x * __builtin_amdgcn_rsqf(B[k].x);
-                Tp[START + 2 * k + 1] = A[k].y * __builtin_amdgcn_rsqf(B[k].y);
+                Tp[START + 2 * k] = gprod(A[k].x, G) * __builtin_amdgcn_rsqf(gprod(B[k].x, G));
+                Tp[START + 2 * k + 1] = gprod(A[k].y, G) * __builtin_amdgcn_rsqf(gprod(B[k].y, G));
             }
-            if constexpr (HAS1) Tp[END - 1] = A1 * __builtin_amdgcn_rsqf(B1);
+            if constexpr (HAS1) Tp[END - 1] = gprod(A1, G) * __builtin_amdgcn_rsqf(gprod(B1, G));
             // (refined lanes did not walk: their in_range stands)
             if (FIRST && !refined) in_range = (Tp[0] >= 0.5f) && (Tp[kSplit] <= 0.5f) && in_range;
             int start_id = 0;
@@ -786,24 +817,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             Tp[kSplit] = hi;
         };
         // Root refinement for one pixel, shared by the phases below: probe
-        // walk + bracketed Halley walks.  A pixel may be worked by a group of
-        // 4 lanes (lane q walks the contributors with index % 4 == q; products
-        // and sums are combined with two xor quad moves, identical in the 4
-        // lanes as float * and + commute) — `grouped` must then be uniform.
-        auto gprod = [&](float v, bool grouped) {
-            if (grouped) {  // (DPP quad moves: no LDS addresses to keep)
-                v *= dpp_mov<kDppXor1>(v);
-                v *= dpp_mov<kDppXor2>(v);
-            }
-            return v;
-        };
-        auto gsum = [&](float v, bool grouped) {
-            if (grouped) {
-                v += dpp_mov<kDppXor1>(v);
-                v += dpp_mov<kDppXor2>(v);
-            }
-            return v;
-        };
+        // walk + bracketed Halley walks.
         // Up to `walks` Halley walks from t in the bracket [lo, hi] (H(lo) >= 0 >= H(hi)),
         // tolerances relative to `scale`.  With `ends`, the first walk also evaluates T at the
         // window ends e0, e8 and sets in_range.  A lane still live on return continues from
@@ -848,7 +862,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             }
             t = tn;
         };
-        auto halley = [&](auto&& src, bool grouped, bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
+        auto halley = [&](auto&& src, int grouped, bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
                           int walks, float scale) {
             Refine r{false, false, in_range0, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             const f32x2 TSE[1] = {f32x2{e0, e8}};
@@ -895,7 +909,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         };
         // Probe walk (window ends + m0 + kProbeOffsets * SAMPLE_RANGE), then the
         // Halley walks from the log-secant root of the bracketing probes.
-        auto probe_refine = [&](auto&& src, float pm0, float pT, bool grouped) {
+        auto probe_refine = [&](auto&& src, float pm0, float pT, int grouped) {
             bool pin = pT <= kMinTransmittance;
             const float lo_w = fmaxf(pm0 - a.sample_range, 0.f), hi_w = fmaxf(pm0 + a.sample_range, 0.f);
             const float interval = (hi_w - lo_w) * (1.f / (float)kSplit);
@@ -1002,7 +1016,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         return PixSrc{s_mask + gq, s_pub_last[gq], (float)(x0 + (gq & 15)), (float)(y0 + (gq >> 4)),
                                       0x11111111u << (lane & 3)};
                     };
-                    const Refine r = probe_refine(src, gm0, gT, true);
+                    const Refine r = probe_refine(src, gm0, gT, 4);
                     if (q == 0) {
                         const int lane = opaque_int(tid);
                         s_groot[lane >> 2] = (r.in_range && r.refined) ? r.t_ref : -1.f;
@@ -1056,7 +1070,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     const float e0 = lo_w, e8 = __builtin_fmaf(interval, (float)kSplit, lo_w);
                     const float t0 = cnt ? fminf(fmaxf(sum / (float)cnt, e0), e8) : e0;
                     auto src = [&] { return PixSrc{s_mask + p, ql, qx, qy, ~0u}; };  // (one walk)
-                    const Refine r = halley(src, false, qin && cnt > 0, t0, e0, e8, true, e0, e8, qin, 1, fmaxf(t0, 1.f));
+                    const Refine r = halley(src, 1, qin && cnt > 0, t0, e0, e8, true, e0, e8, qin, 1, fmaxf(t0, 1.f));
                     GSR_DBG(p, "p2: m0 %.7f cnt %d t0 %.7f -> live %d in %d ref %d ill %d t_ref %.7f t %.7f [%.7f %.7f] D %g\n",
                             qm0, cnt, t0, (int)r.live, (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.t, r.lo,
                             r.hi, r.ref_D);
@@ -1089,20 +1103,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 if constexpr (STATS) st_phase = 2;
                 if (live2) s_list[before + __popcll(bl & ((1ull << (tid & 63)) - 1ull))] = (uint8_t)p2;
                 __syncthreads();
-                for (uint32_t e = (uint32_t)(tid >> 2); e < n_live; e += kTilePixels / 4) {
+                // group size: as many lanes per pixel as one round of the block allows (4 .. 16)
+                const int lg2b = kAdaptGroups ? (n_live <= 16 ? 4 : n_live <= 32 ? 3 : 2) : 2;
+                const int G2b = 1 << lg2b;
+                for (uint32_t e = (uint32_t)(tid >> lg2b); e < n_live; e += (uint32_t)(kTilePixels >> lg2b)) {
                     const int p = s_list[e];
                     const float t = s_pub_T[p];
                     auto src = [&] {
                         const int pp = s_list[opaque_int((int)e)];
                         return PixSrc{s_mask + pp, s_pub_last[pp], (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
-                                      0x11111111u << (opaque_int(tid) & 3)};
+                                      gfilter(G2b, opaque_int(tid) & (G2b - 1))};
                     };
-                    const Refine r = halley(src, true, true, t, s_pub_m0[p], s_pub_hi[p], false, 0.f, 0.f, true,
+                    const Refine r = halley(src, G2b, true, t, s_pub_m0[p], s_pub_hi[p], false, 0.f, 0.f, true,
                                             kRefineWalks - 1, fmaxf(t, 1.f));
-                    if ((tid & 3) == 0)
+                    if ((tid & (G2b - 1)) == 0)
                         GSR_DBG(p, "p2b: from %.7f -> live %d in %d ref %d ill %d t_ref %.7f t %.7f [%.7f %.7f] D %g\n", t,
                                 (int)r.live, (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.t, r.lo, r.hi, r.ref_D);
-                    if ((tid & 3) == 0) publish(s_list[opaque_int((int)e)], r);
+                    if ((tid & (G2b - 1)) == 0) publish(s_list[opaque_int((int)e)], r);
                 }
                 __syncthreads();
                 stamp(6);
@@ -1154,15 +1171,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     }
                     __syncthreads();
                     const bool own_in = in_range, own_refined = refined;  // (the worker role reuses them)
-                    const bool work = (uint32_t)tid < n_left;
-                    const bool work_pass = (uint32_t)tid < n_pass;
+                    // a group of G3 lanes per listed pixel, as many as one round of the block allows
+                    const int lg3 = kAdaptGroups ? (n_left <= 16 ? 4 : n_left <= 32 ? 3 : n_left <= 64 ? 2
+                                                    : n_left <= 128 ? 1 : 0) : 0;
+                    const int G3 = 1 << lg3;
+                    const uint32_t e3 = (uint32_t)tid >> lg3;
+                    const bool work = e3 < n_left;
+                    const bool work_pass = e3 < n_pass;
                     if (__ballot(work) != 0ull) {  // (waves past the list skip)
                         auto wsrc = [&] {
-                            const int pp = s_list[opaque_int(tid)];
+                            const int pp = s_list[opaque_int(tid) >> lg3];
                             return PixSrc{s_mask + pp, s_pub_last[pp], (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
-                                          ~0u};
+                                          gfilter(G3, opaque_int(tid) & (G3 - 1))};
                         };
-                        const int pw = work ? (int)s_list[tid] : 0;
+                        const int pw = work ? (int)s_list[e3] : 0;
                         const float wm0 = s_pub_m0[pw];
                         in_range = work_pass;
                         refined = false;
@@ -1172,9 +1194,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                             }
                             dmin = fmaxf(wm0 - a.sample_range, 0.f);
                             dmax = fmaxf(wm0 + a.sample_range, 0.f);
-                            pass(std::true_type{}, wsrc);
+                            pass(std::true_type{}, wsrc, G3);
 #pragma unroll 1
-                            for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, wsrc);
+                            for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, wsrc, G3);
                         }
                         // the median depth and dT/dt_m as the owner path below computes them
                         float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
@@ -1189,16 +1211,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         in_range = in_range || wi;
                         const float mb = mo * nrm;
                         float dT = 0.f;
-                        walk(ps.mask, ps.plast, ps.x, ps.y, ~0u, work && mb != 0.f && ps.plast != 0,
+                        walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, work && mb != 0.f && ps.plast != 0,
                              [&](float alpha, float t_peak, float4 w2) {
                                  const float t_delta = (mb - t_peak) * w2.y;
                                  const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
                                  dT += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
                              });
+                        dT = gsum(dT, G3);
                         if (work) GSR_DBG(pw, "p3: pass %d m0 %.7f [%.7f %.7f] Tp0 %.7f Tp8 %.7f in %d mo %.7f dT %g\n",
                                           (int)work_pass, wm0, dmin, dmax, Tp[0], Tp[kSplit], (int)in_range, mo, dT);
-                        if (work) {
-                            const int q = s_list[opaque_int(tid)];
+                        if (work && (tid & (G3 - 1)) == 0) {
+                            const int q = s_list[opaque_int(tid) >> lg3];
                             s_pub_T[q] = mo;
                             s_pub_m0[q] = dT;
                             s_pub_last[q] = in_range ? 1u : 0u;
@@ -1215,7 +1238,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     }
                 }
             } else {
-                const Refine r = probe_refine(own_src, m_init, T, false);
+                const Refine r = probe_refine(own_src, m_init, T, 1);
                 in_range = r.in_range;
                 refined = r.refined;
                 t_ref = r.t_ref;
@@ -1232,16 +1255,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 }
                 dmin = win_lo();
                 dmax = win_hi();
-                pass(std::true_type{}, own_src);
+                pass(std::true_type{}, own_src, 1);
 #pragma unroll 1
-                for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, own_src);
+                for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, own_src, 1);
             }
         } else {
             dmin = win_lo();
             dmax = win_hi();
-            if (a.passes > 0) pass(std::true_type{}, own_src);
+            if (a.passes > 0) pass(std::true_type{}, own_src, 1);
 #pragma unroll 1
-            for (int it = 1; it < a.passes; it++) pass(std::false_type{}, own_src);
+            for (int it = 1; it < a.passes; it++) pass(std::false_type{}, own_src, 1);
         }
         if constexpr (STATS) {
             stamp(7);

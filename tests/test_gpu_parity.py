@@ -830,7 +830,7 @@ def test_c3_stats_instance_is_bit_exact(c3):
         assert torch.equal(ref[k], got[k]), k
 
 
-def _check_refined_depths(a, b, max_loose_frac):
+def _check_refined_depths(a, b, max_loose_frac, ties=None):
     """Refined median depths `a` against the reference passes' `b` (same GPU):
     within 2e-6 relative (the reference's final cell is 2.4e-5 wide; both land
     within ~1e-7 of the root of T = 1/2 where it is well conditioned), except
@@ -840,13 +840,26 @@ def _check_refined_depths(a, b, max_loose_frac):
     and the reference's answer is a linear interpolation inside its final
     bisection cell (0.8 / 8^5 = 2.4e-5 wide) between noise-level T values, so
     within 1.5e-5 max(mdepth, 1) + 2.4e-5 — at most `max_loose_frac` of the
-    pixels."""
+    pixels.  With `ties` (x, y, a, b) -> float64 margin: a pixel beyond that
+    is accepted only as a proven rounding tie of the bisection's decisions
+    (flip_audit.mdepth_flip_margin <= 1e-4: T within 1e-4 of 1/2 at both
+    depths and between them, or at the in-range tests), at most max(2, 1e-5)
+    of the pixels — the passes of a compacted pixel group run with a
+    different product association than one lane's."""
     a64, b64 = a.double(), b.double()
     d = (a64 - b64).abs()
     tight = d <= 2e-6 * b64.abs()
     cell = 0.8 / 8 ** 5  # (mdepth = t rln, rln <= 1: a cell in t is at most as wide in mdepth)
     loose = d <= 1.5e-5 * b64.abs().clamp_min(1.0) + cell
-    assert bool(loose.all()), float(d.max())
+    if ties is None:
+        assert bool(loose.all()), float(d.max())
+    else:
+        bad = (~loose).nonzero().cpu().numpy()
+        assert len(bad) <= max(2, 1e-5 * a.numel()), (len(bad), float(d.max()))
+        margins = [ties(int(x), int(y), float(a64[c, y, x]), float(b64[c, y, x])) for c, y, x in bad]
+        print(f"refined depths: {len(bad)} beyond the ill-root bound, proven ties (max float64 margin "
+              f"{max(margins, default=0.0):.2e})")
+        assert all(m <= 1e-4 for m in margins), margins
     n_loose = int((~tight).sum())
     print(f"refined depths: {n_loose} of {a.numel()} pixels beyond 2e-6 (ill-conditioned roots), max |d| {float(d.max()):.2e}")
     assert n_loose <= max_loose_frac * a.numel(), n_loose
@@ -913,10 +926,12 @@ def test_c2_compacted_fallback_matches_bisection(c2):
     not converged, spread over many waves) are compacted and run by the first
     lanes of the block (render_fwd.hip phase 3), and the ill-conditioned
     roots it keeps (C2: ~15% of the pixels) get their dT/dt_m there in one
-    walk: against all five reference passes on the same GPU, colour, alpha,
-    normal and the in-range pattern bit-identical, depths as
-    _check_refined_depths (at most 25% of the pixels beyond 2e-6), and the
-    passes run in at most 35% of the waves."""
+    walk: against all five reference passes on the same GPU, colour, alpha
+    and normal bit-identical, the in-range pattern and the depths as
+    _check_refined_depths (at most 25% of the pixels beyond 2e-6; beyond the
+    ill-root bound and in-range flips only proven float64 ties — a compacted
+    pixel's passes run on a group of lanes, whose products associate
+    differently), and the passes run in at most half of the waves."""
     from diff_gaussian_rasterization import _C
 
     ga = [_gpu(x) for x in Hh.oracle_args(c2)] + [False]
@@ -932,12 +947,26 @@ def test_c2_compacted_fallback_matches_bisection(c2):
     for k in (1, 2, 3, 5):
         assert torch.equal(ref[k], got[k]), k
     a, b = got[4], ref[4]
-    assert torch.equal(a == 0, b == 0)
-    _check_refined_depths(a, b, max_loose_frac=0.25)
+    # decisions of the passes that are rounding ties in float64 (tests/flip_audit.py) may go either way
+    import flip_audit as FA
+    O.set_threads(16)
+    o = O.forward(*Hh.oracle_args(c2))
+    ch = FA.PixelChains(o, c2["W"], c2["H"], c2["tanx"], c2["tany"])
+
+    def ties(x, y, ma, mb):
+        return FA.mdepth_flip_margin(ch, x, y, ch.depth_of(x, y, ma), ch.depth_of(x, y, mb))
+
+    flips = (a == 0) != (b == 0)
+    fl = flips.nonzero().cpu().numpy()
+    assert len(fl) <= max(2, 1e-5 * a.numel()), len(fl)
+    assert all(ties(int(x), int(y), float(a[c, y, x]), float(b[c, y, x])) <= 1e-4 for c, y, x in fl)
+    _check_refined_depths(torch.where(flips, b, a), b, max_loose_frac=0.25, ties=ties)
     waves, pass_waves, left = st[4], st[5], st[7]
     print("render stats", st)
     assert left > 0.02 * 800 * 800, st  # the case this test is about
-    assert waves > 0 and pass_waves <= 0.35 * waves, st
+    # (round 4: a listed pixel's passes run on a group of up to 16 lanes, so they occupy more waves
+    # for a shorter time; uncompacted, 8,508 of the 10,000 waves ran them)
+    assert waves > 0 and pass_waves <= 0.5 * waves, st
 
 
 def test_c3_backward_linearity(c3):
