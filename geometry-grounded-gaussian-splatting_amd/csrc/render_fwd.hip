@@ -335,6 +335,11 @@ __device__ unsigned long long g_render_stats[kRenderStats];
 #define GSR_ADAPT_GROUPS 1
 #endif
 constexpr bool kAdaptGroups = GSR_ADAPT_GROUPS;
+// Phase 2 without the window-end samples (in_range implied by a root well inside the window).
+#ifndef GSR_P2_NOENDS
+#define GSR_P2_NOENDS 1  // (0: ends sampled in the first walk; render_fwd 0.738 -> 0.682 ms at C3 with 1, profiles/r4_ab_p2_noends.txt)
+#endif
+constexpr bool kP2NoEnds = GSR_P2_NOENDS;
 
 // Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
 // pixel rows [y0 + 4 s, y0 + 4 s + 3] x columns [x0, x0 + 15].
@@ -1070,7 +1075,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     const float e0 = lo_w, e8 = __builtin_fmaf(interval, (float)kSplit, lo_w);
                     const float t0 = cnt ? fminf(fmaxf(sum / (float)cnt, e0), e8) : e0;
                     auto src = [&] { return PixSrc{s_mask + p, ql, qx, qy, ~0u}; };  // (one walk)
-                    const Refine r = halley(src, 1, qin && cnt > 0, t0, e0, e8, true, e0, e8, qin, 1, fmaxf(t0, 1.f));
+                    const Refine r = halley(src, 1, qin && cnt > 0, t0, e0, e8, !kP2NoEnds, e0, e8, qin, 1, fmaxf(t0, 1.f));
                     GSR_DBG(p, "p2: m0 %.7f cnt %d t0 %.7f -> live %d in %d ref %d ill %d t_ref %.7f t %.7f [%.7f %.7f] D %g\n",
                             qm0, cnt, t0, (int)r.live, (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.t, r.lo,
                             r.hi, r.ref_D);
@@ -1124,7 +1129,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 __syncthreads();
                 stamp(6);
                 const int me = opaque_int(tid);
-                const uint32_t flags = s_pub_last[me];
+                uint32_t flags = s_pub_last[me];
+                if constexpr (kP2NoEnds) {
+                    // phase 2 did not sample the window ends: a root found well inside the reference's
+                    // first window implies its in_range test (T is non-increasing); one near or past an
+                    // end is left to the passes, which decide in_range with their own samples
+                    if (flags & (kPubRefined | kPubIll)) {
+                        const float t_pub = s_pub_T[me] * pixel_ray_norm(lane_fx(), lane_fy(), a.W, a.H, a.focal_x,
+                                                                         a.focal_y);
+                        const float e0 = win_lo(), hi_w = win_hi();
+                        const float e8 = __builtin_fmaf((hi_w - e0) * (1.f / (float)kSplit), (float)kSplit, e0);
+                        const float margin = 1e-4f * fmaxf(t_pub, 1.f);
+                        if (!(t_pub > e0 + margin && t_pub < e8 - margin)) flags = 0u;
+                    }
+                }
                 const bool ill = (flags & kPubIll) != 0u;  // root in s_pub_T[me]; dT/dt_m by the walk below
                 if (flags & kPubRefined) {
                     refined = true;
