@@ -175,15 +175,15 @@ __device__ __forceinline__ void bisect_step(f32x2 (&A)[NP], f32x2 (&B)[NP], cons
 // passes.  (The previous scheme ran the reference's first two passes and
 // refined from the pass-2 cell: one more 7-sample walk per contributor.)
 #ifndef GSR_PROBES
-#define GSR_PROBES 9  // (11: 0.769 -> 0.758 ms render_fwd at C3 with 9, profiles/r4_ab_probes.txt)
+#define GSR_PROBES 7  // (11 -> 9 -> 7: render_fwd 0.769 -> 0.758 -> (later build) 0.683 -> 0.671 ms at C3, profiles/r4_ab_probes.txt)
 #endif
-constexpr int kProbes = GSR_PROBES;  // 11 or 7 (the window ends, m0 and 8 or 4 offsets around it); 9 (no ends)
+constexpr int kProbes = GSR_PROBES;  // 11 (the window ends, m0 and 8 offsets around it); 9 or 7 (no ends)
 // With 9 probes the window ends are not sampled: T is non-increasing in t, so a bracket between the
 // inner probes (m0 -/+ SAMPLE_RANGE / 2) implies the reference's in_range test (T(e0) >= 1/2 >= T(e8));
 // a pixel whose root lies outside them is left to the reference's passes.
-constexpr bool kProbeEnds = kProbes != 9;
+constexpr bool kProbeEnds = kProbes == 11;
 #if GSR_PROBES == 7
-__constant__ constexpr float kProbeOffsets[kProbes] = {0.f, -0.5f, -0.125f, 0.f, 0.125f, 0.5f, 0.f};
+__constant__ constexpr float kProbeOffsets[kProbes] = {-0.25f, -0.125f, -0.0625f, 0.f, 0.0625f, 0.125f, 0.25f};
 #elif GSR_PROBES == 9
 __constant__ constexpr float kProbeOffsets[kProbes] = {-0.5f, -0.25f, -0.125f, -0.0625f, 0.f,
                                                         0.0625f, 0.125f, 0.25f, 0.5f};

@@ -729,10 +729,18 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
                 continue;
             }
             int m = 0;
-            ts[m++] = dmin;
+            const int noends = getenv("SIM_NOENDS") != NULL;  /* the GPU's probe walk since round 4 */
+            if (!noends) ts[m++] = dmin;
             for (int k = 0; k < nk; k++) ts[m++] = fminf(fmaxf(m0 + off[k], dmin), dmax);
-            ts[m++] = dmax;
+            if (!noends) ts[m++] = dmax;
             for (int k = 0; k < m; k++) hs[k] = logf(vac(buf, n, ts[k])) + 0.69314718f;
+            if (noends && !(hs[0] >= 0.f && hs[m - 1] <= 0.f)) {  /* unbracketed: left to the passes */
+                out[2] += 1;
+                out[42] += 1;
+                root[l] = mr;
+                have[l] = 0;
+                continue;
+            }
             int k1 = 0;
             for (int k = 1; k < m - 1; k++) if (hs[k] >= 0.f) k1 = k;
             float w = hs[k1] / (hs[k1] - hs[k1 + 1]);

@@ -19,7 +19,7 @@ print(f"tol {tol}: lanes {out[0]:.0f} max|d| {out[1]:.3e} fallbacks {out[2]:.0f}
 print(f"phase-1 wave max walks {out[3]/out[4]:.2f}  phase-2 wave max walks {out[5]/out[6]:.2f} (fallback=100)")
 print("phase-2 lane walks hist", out[8:24].astype(int).tolist())
 print("phase-1 lane walks hist (SIM_P1)", out[25:32].astype(int).tolist())
-print("phase-1 grid pixel Halley walks hist [0..7+]", out[32:40].astype(int).tolist(), "stragglers", int(out[40]), "their 2b walks", int(out[41]))
+print("phase-1 grid pixel Halley walks hist [0..7+]", out[32:40].astype(int).tolist(), "stragglers", int(out[40]), "their 2b walks", int(out[41]), "unbracketed", int(out[42]))
 why = (ctypes.c_long * 11)()
 sim.sim_why(why)
 print("halley outcomes: ok", why[0], "ill-conditioned", why[1], "not converged", why[2], "ill D*scale log10 bins from -4:", list(why[3:11]))
