@@ -340,6 +340,12 @@ constexpr bool kAdaptGroups = GSR_ADAPT_GROUPS;
 #define GSR_P2_NOENDS 1  // (0: ends sampled in the first walk; render_fwd 0.738 -> 0.682 ms at C3 with 1, profiles/r4_ab_p2_noends.txt)
 #endif
 constexpr bool kP2NoEnds = GSR_P2_NOENDS;
+// Phase 1 with one Halley walk: a grid pixel that needs more continues in phase 2 on its own lane
+// (whose fourth wave was idle) from its iterate, which its neighbours take as their guess.
+#ifndef GSR_P1_ONE
+#define GSR_P1_ONE 1  // (0: up to 4 Halley walks in phase 1; render_fwd 0.672 -> 0.628 ms at C3 with 1, profiles/r4_ab_p1_one.txt)
+#endif
+constexpr bool kP1One = GSR_P1_ONE;
 
 // Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
 // pixel rows [y0 + 4 s, y0 + 4 s + 3] x columns [x0, x0 + 15].
@@ -381,6 +387,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     __shared__ uint32_t s_pub_last[kPub];
     __shared__ float s_pub_m0[kPub], s_pub_T[kPub];
     __shared__ float s_groot[(GEOM && !SAMPLE) ? 64 : 1];  // then the compacted phase-2 list (bytes)
+    __shared__ uint8_t s_glive[(GEOM && !SAMPLE) ? 64 : 1];  // (kP1One) grid pixel continued in phase 2
     __shared__ float s_pub_hi[kPub];
 
     const int tid = threadIdx.x;
@@ -854,12 +861,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 // accepted only where the root is well conditioned: rounding noise of
                 // ~kHNoise in log2 T moves it by less than tol_cond (T flat near 1/2 — a
                 // pixel between two splats' peaks — leaves it to the reference's passes)
-                r.refined = D * tol_cond >= kHNoise;
-                // (an ill-conditioned root only where T itself is at 1/2: converged by the Newton step)
-                r.ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
                 // (converged by the Newton test with the Halley iterate out of the bracket — H'' large
                 // against H' near a splat's peak — the root is the Newton iterate, not the midpoint)
                 r.t_ref = newton && !halley_in ? fminf(fmaxf(t + fast_div(H, D), lo), hi) : tn;
+                // dT/dt_m is continued from t to the root with H'' (publish): only over a step short
+                // against the curvature length of H — a thin splat's peak next to the root makes the
+                // continuation meaningless (a surfel scene had H' change sign across a 8.5e-5 step) —
+                // else the root is kept as an ill-conditioned one and dT/dt_m computed exactly (phase 3)
+                const bool smooth = fabsf(r.t_ref - t) * F <= kCurvTol * D;
+                r.refined = D * tol_cond >= kHNoise && smooth;
+                // (an ill-conditioned root only where T itself is at 1/2: converged by the Newton step)
+                r.ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
                 live = false;
                 r.ref_t = t;
                 r.ref_D = D;
@@ -914,7 +926,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         };
         // Probe walk (window ends + m0 + kProbeOffsets * SAMPLE_RANGE), then the
         // Halley walks from the log-secant root of the bracketing probes.
-        auto probe_refine = [&](auto&& src, float pm0, float pT, int grouped) {
+        auto probe_refine = [&](auto&& src, float pm0, float pT, int grouped, int walks) {
             bool pin = pT <= kMinTransmittance;
             const float lo_w = fmaxf(pm0 - a.sample_range, 0.f), hi_w = fmaxf(pm0 + a.sample_range, 0.f);
             const float interval = (hi_w - lo_w) * (1.f / (float)kSplit);
@@ -969,8 +981,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             float wsec = Hlo / (Hlo - Hhi);
             wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
             const float t = __builtin_fmaf(wsec, hi - lo, lo);
-            return halley(src, grouped, pin && bracketed, t, lo, hi, false, 0.f, 0.f, pin, kRefineWalks,
-                          fmaxf(t, 1.f));
+            return halley(src, grouped, pin && bracketed, t, lo, hi, false, 0.f, 0.f, pin, walks, fmaxf(t, 1.f));
         };
         bool have_out = false;  // (render path) md_out and dT/dt_m published by the pixel's worker
         if (a.refine && resident && a.passes > 0) {
@@ -1007,6 +1018,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         if (r.refined && mb != 0.f)
                             dt = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(r.ref_E, mb - r.ref_t, -r.ref_D);
                     }
+#ifdef GSR_DBG_DT
+                    if ((flags & kPubRefined) && !(dt < -1e-4f))
+                        printf("dbgdt publish (%d,%d) t_ref %.7f ref_t %.7f D %g E %g dt %g\n", x0 + (p & 15), y0 + (p >> 4),
+                               r.t_ref, r.ref_t, r.ref_D, r.ref_E, dt);
+#endif
                     s_pub_last[p] = flags;
                     s_pub_T[p] = mo;
                     s_pub_m0[p] = dt;
@@ -1021,14 +1037,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         return PixSrc{s_mask + gq, s_pub_last[gq], (float)(x0 + (gq & 15)), (float)(y0 + (gq >> 4)),
                                       0x11111111u << (lane & 3)};
                     };
-                    const Refine r = probe_refine(src, gm0, gT, 4);
+                    const Refine r = probe_refine(src, gm0, gT, 4, kP1One ? 1 : kRefineWalks);
                     if (q == 0) {
                         const int lane = opaque_int(tid);
-                        s_groot[lane >> 2] = (r.in_range && r.refined) ? r.t_ref : -1.f;
+                        // (kP1One: a grid pixel not converged after its one Halley walk hands its iterate to its
+                        // neighbours as their guess and continues in phase 2 on its own lane)
+                        const bool cont = kP1One && r.live;
+                        s_groot[lane >> 2] = (r.in_range && r.refined) ? r.t_ref : cont ? r.t : -1.f;
+                        if constexpr (kP1One) s_glive[lane >> 2] = cont ? 1 : 0;
                         GSR_DBG_NEAR(grid_pixel(lane), "p1 (%d,%d): m0 %.7f -> live %d in %d ref %d ill %d t_ref %.7f D %g\n",
                                      x0 + (grid_pixel(lane) & 15), y0 + (grid_pixel(lane) >> 4), gm0, (int)r.live,
                                      (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.ref_D);
-                        publish(grid_pixel(lane), r);
+                        if (!cont) publish(grid_pixel(lane), r);
                     }
                 }
                 __syncthreads();
@@ -1057,10 +1077,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                             }
                         }
                 };
-                if (wave != skip) {  // phase 2, first walk
-                    const int k = (wave < skip ? wave : wave - 1) * 64 + (tid & 63);
-                    const int pair = k / 24, r24 = k - pair * 24;
-                    const int lx = r24 < 8 ? 2 * r24 + 1 : r24 - 8, ly = r24 < 8 ? 2 * pair : 2 * pair + 1;
+                // (kP1One: every lane takes its own pixel — the 192 off-grid ones and the grid pixels phase 1
+                // left live, from their own iterate; otherwise 3 of the 4 waves take the 192 off-grid ones)
+                const int k = kP1One ? tid : (wave < skip ? wave : wave - 1) * 64 + (tid & 63);
+                const int pair = k / 24, r24 = k - pair * 24;
+                const int lx = kP1One ? (tid & 15) : r24 < 8 ? 2 * r24 + 1 : r24 - 8;
+                const int ly = kP1One ? (tid >> 4) : r24 < 8 ? 2 * pair : 2 * pair + 1;
+                const bool on_grid = !(lx & 1) && !(ly & 1);
+                const bool p2_todo = kP1One ? (!on_grid || s_glive[(ly >> 1) * 8 + (lx >> 1)] != 0) : wave != skip;
+                if (p2_todo) {  // phase 2, first walk
                     const int p = ly * 16 + lx;
                     p2 = p;
                     const float qx = (float)(x0 + lx), qy = (float)(y0 + ly);
@@ -1068,7 +1093,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     const float qm0 = s_pub_m0[p], qT = s_pub_T[p];
                     float sum;
                     int cnt;
-                    guess(lx, ly, sum, cnt);
+                    guess(lx, ly, sum, cnt);  // (a live grid pixel: its own iterate, the one grid neighbour it has)
                     const bool qin = qT <= kMinTransmittance;
                     const float lo_w = fmaxf(qm0 - a.sample_range, 0.f), hi_w = fmaxf(qm0 + a.sample_range, 0.f);
                     const float interval = (hi_w - lo_w) * (1.f / (float)kSplit);
@@ -1256,7 +1281,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     }
                 }
             } else {
-                const Refine r = probe_refine(own_src, m_init, T, 1);
+                const Refine r = probe_refine(own_src, m_init, T, 1, kRefineWalks);
                 in_range = r.in_range;
                 refined = r.refined;
                 t_ref = r.t_ref;
