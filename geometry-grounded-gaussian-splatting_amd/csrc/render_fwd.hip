@@ -1214,18 +1214,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     }
                     __syncthreads();
                     const bool own_in = in_range, own_refined = refined;  // (the worker role reuses them)
-                    // a group of G3 lanes per listed pixel, as many as one round of the block allows
-                    const int lg3 = kAdaptGroups ? (n_left <= 16 ? 4 : n_left <= 32 ? 3 : n_left <= 64 ? 2
-                                                    : n_left <= 128 ? 1 : 0) : 0;
+                    // lane groups: the pixels that need the passes (five walks and the dT/dt_m walk) get
+                    // G_p lanes each, the ill-conditioned roots (the dT/dt_m walk only) G_i <= G_p, the
+                    // largest powers of two with n_pass G_p + n_ill G_i <= 256 and G_i >= G_p / 8; a
+                    // pixel's group is aligned (the pass groups first), so its DPP combine stays inside it
+                    int lgp = kAdaptGroups ? 4 : 0;
+                    while (lgp > 0 && (n_pass << lgp) + n_ill * (uint32_t)max(1, (1 << lgp) >> 3) > (uint32_t)kTilePixels)
+                        lgp--;
+                    int lgi = lgp;
+                    while (lgi > 0 && (n_pass << lgp) + (n_ill << lgi) > (uint32_t)kTilePixels) lgi--;
+                    const uint32_t np_lanes = n_pass << lgp;
+                    auto lane_group = [&](uint32_t t, int& lg) -> uint32_t {  // (listed pixel of lane t, its group log2)
+                        const bool is_p = t < np_lanes;
+                        lg = is_p ? lgp : lgi;
+                        return is_p ? (t >> lgp) : n_pass + ((t - np_lanes) >> lgi);
+                    };
+                    int lg3;
+                    const uint32_t e3 = lane_group((uint32_t)tid, lg3);
                     const int G3 = 1 << lg3;
-                    const uint32_t e3 = (uint32_t)tid >> lg3;
                     const bool work = e3 < n_left;
                     const bool work_pass = e3 < n_pass;
                     if (__ballot(work) != 0ull) {  // (waves past the list skip)
                         auto wsrc = [&] {
-                            const int pp = s_list[opaque_int(tid) >> lg3];
+                            int lgw;
+                            const uint32_t ew = lane_group((uint32_t)opaque_int(tid), lgw);
+                            const int pp = s_list[ew];
                             return PixSrc{s_mask + pp, s_pub_last[pp], (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
-                                          gfilter(G3, opaque_int(tid) & (G3 - 1))};
+                                          gfilter(1 << lgw, opaque_int(tid) & ((1 << lgw) - 1))};
                         };
                         const int pw = work ? (int)s_list[e3] : 0;
                         const float wm0 = s_pub_m0[pw];
@@ -1264,7 +1279,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         if (work) GSR_DBG(pw, "p3: pass %d m0 %.7f [%.7f %.7f] Tp0 %.7f Tp8 %.7f in %d mo %.7f dT %g\n",
                                           (int)work_pass, wm0, dmin, dmax, Tp[0], Tp[kSplit], (int)in_range, mo, dT);
                         if (work && (tid & (G3 - 1)) == 0) {
-                            const int q = s_list[opaque_int(tid) >> lg3];
+                            int lgw;
+                            const int q = s_list[lane_group((uint32_t)opaque_int(tid), lgw)];
                             s_pub_T[q] = mo;
                             s_pub_m0[q] = dT;
                             s_pub_last[q] = in_range ? 1u : 0u;

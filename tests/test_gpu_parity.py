@@ -931,7 +931,7 @@ def test_c2_compacted_fallback_matches_bisection(c2):
     _check_refined_depths (at most 25% of the pixels beyond 2e-6; beyond the
     ill-root bound and in-range flips only proven float64 ties — a compacted
     pixel's passes run on a group of lanes, whose products associate
-    differently), and the passes run in at most half of the waves."""
+    differently)."""
     from diff_gaussian_rasterization import _C
 
     ga = [_gpu(x) for x in Hh.oracle_args(c2)] + [False]
@@ -964,9 +964,10 @@ def test_c2_compacted_fallback_matches_bisection(c2):
     waves, pass_waves, left = st[4], st[5], st[7]
     print("render stats", st)
     assert left > 0.02 * 800 * 800, st  # the case this test is about
-    # (round 4: a listed pixel's passes run on a group of up to 16 lanes, so they occupy more waves
-    # for a shorter time; uncompacted, 8,508 of the 10,000 waves ran them)
-    assert waves > 0 and pass_waves <= 0.5 * waves, st
+    # (round 4: a listed pixel's passes run on a group of up to 16 lanes, so the number of waves running
+    # them no longer measures the compaction — it is the wave-time that does, profiles/r4_ab_*; uncompacted
+    # and one lane per pixel, 8,508 of the 10,000 waves ran the passes)
+    assert waves > 0 and pass_waves <= waves, st
 
 
 def test_c3_backward_linearity(c3):
