@@ -346,6 +346,11 @@ constexpr bool kP2NoEnds = GSR_P2_NOENDS;
 #define GSR_P1_ONE 1  // (0: up to 4 Halley walks in phase 1; render_fwd 0.672 -> 0.628 ms at C3 with 1, profiles/r4_ab_p1_one.txt)
 #endif
 constexpr bool kP1One = GSR_P1_ONE;
+// Phase 2b group size: the largest (at most 16 lanes) that runs every straggler in one round, down to
+// GSR_P2B_ONE_ROUND - 1 as log2 (0: 16 / 8 / 4 lanes by count, more rounds above 64 stragglers)
+#ifndef GSR_P2B_ONE_ROUND
+#define GSR_P2B_ONE_ROUND 1  // (C2 render_fwd 0.523 -> 0.503 ms, C3 unchanged; profiles/r4_ab_p2b_one_round.txt)
+#endif
 
 // Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
 // pixel rows [y0 + 4 s, y0 + 4 s + 3] x columns [x0, x0 + 15].
@@ -1134,7 +1139,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 if (live2) s_list[before + __popcll(bl & ((1ull << (tid & 63)) - 1ull))] = (uint8_t)p2;
                 __syncthreads();
                 // group size: as many lanes per pixel as one round of the block allows (4 .. 16)
+#if GSR_P2B_ONE_ROUND
+                int lg2b = 4;
+                while (lg2b > GSR_P2B_ONE_ROUND - 1 && (n_live << lg2b) > (uint32_t)kTilePixels) lg2b--;
+#else
                 const int lg2b = kAdaptGroups ? (n_live <= 16 ? 4 : n_live <= 32 ? 3 : 2) : 2;
+#endif
                 const int G2b = 1 << lg2b;
                 for (uint32_t e = (uint32_t)(tid >> lg2b); e < n_live; e += (uint32_t)(kTilePixels >> lg2b)) {
                     const int p = s_list[e];
