@@ -262,6 +262,13 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
         sc[k] = sn[k] = zero;
     }
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
+    // factor of field lane >> 2 after the reduction: the NDC scale of dL/dmean2D, -1/2 of dL/dconic's
+    // three terms (exact: a power of two)
+    const int field = lane >> 2;
+    const float post_scale = field == kAccMean2D     ? ddelx_dx
+                             : field == kAccMean2D + 1 ? ddely_dy
+                             : (field >= kAccConic && field < kAccConic + 3) ? -0.5f
+                                                                              : 1.f;
     // the entries no pixel of the tile blended in the forward: skipped without evaluation (entries past the
     // mask's kBlendWords * 32 are all walked)
     if (tid < kBlendWords) s_bm[tid] = a.blend_mask[(size_t)tile * kBlendWords + tid];
@@ -427,11 +434,12 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
             f[kAccColor + 0] = hsum(Fc0);
             f[kAccColor + 1] = hsum(Fc1);
             f[kAccColor + 2] = hsum(Fc2);
-            f[kAccMean2D + 0] = hsum(Fmx) * ddelx_dx;
-            f[kAccMean2D + 1] = hsum(Fmy) * ddely_dy;
-            f[kAccConic + 0] = hsum(Fq) * (-0.5f * dx * dx);
-            f[kAccConic + 1] = hsum(Fqdy) * (-0.5f * dx);
-            f[kAccConic + 2] = -0.5f * hsum(Fqdy2);
+            // (the wave-uniform factors W/2, H/2 and -1/2 applied after the reduction: post_scale)
+            f[kAccMean2D + 0] = hsum(Fmx);
+            f[kAccMean2D + 1] = hsum(Fmy);
+            f[kAccConic + 0] = hsum(Fq) * (dx * dx);
+            f[kAccConic + 1] = hsum(Fqdy) * dx;
+            f[kAccConic + 2] = hsum(Fqdy2);
             f[kAccConic + 3] = hsum(Fp);
             if constexpr (GEOM) {
                 f[kAccNormal + 0] = hsum(Fn0);
@@ -446,7 +454,7 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
 #pragma unroll
                 for (int q = kAccNormal; q < kAccFields; q++) f[q] = 0.f;
             }
-            const float red = wave_transpose_reduce16(f);
+            const float red = wave_transpose_reduce16(f) * post_scale;
             const float abs_red = wave_sum_dpp(fabs_sum);
             const uint32_t g = s_id[j];
             // one atomic instruction: lanes 0, 4, .., 60 add the 16 fields of
