@@ -346,6 +346,9 @@ constexpr bool kP2NoEnds = GSR_P2_NOENDS;
 #define GSR_P1_ONE 1  // (0: up to 4 Halley walks in phase 1; render_fwd 0.672 -> 0.628 ms at C3 with 1, profiles/r4_ab_p1_one.txt)
 #endif
 constexpr bool kP1One = GSR_P1_ONE;
+#ifndef GSR_LEFT_STATS
+#define GSR_LEFT_STATS 0  // (development: render stats slots 12..15 count why pixels are left to the passes)
+#endif
 // Phase 2b group size: the largest (at most 16 lanes) that runs every straggler in one round, down to
 // GSR_P2B_ONE_ROUND - 1 as log2 (0: 16 / 8 / 4 lanes by count, more rounds above 64 stragglers)
 #ifndef GSR_P2B_ONE_ROUND
@@ -711,8 +714,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     if ((tid & 63) == __builtin_ctzll(m)) {
                         st[0] += 1;
                         st[1] += __popcll(m);
-                        st[8 + 2 * st_phase] += 1;
-                        st[9 + 2 * st_phase] += __popcll(m);
+                        if (!GSR_LEFT_STATS || st_phase < 2) {
+                            st[8 + 2 * st_phase] += 1;
+                            st[9 + 2 * st_phase] += __popcll(m);
+                        }
                     }
                 }
                 const float4 a0 = c_w0[j1], b0 = c_w0[j2];
@@ -840,7 +845,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         // window ends e0, e8 and sets in_range.  A lane still live on return continues from
         // (t, lo, hi).
         struct Refine {
-            bool refined, ill, in_range, live;
+            bool refined, ill, in_range, live, newton_done;
             float t_ref, ref_t, ref_D, ref_E;
             float t, lo, hi;
         };
@@ -877,6 +882,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 r.refined = D * tol_cond >= kHNoise && smooth;
                 // (an ill-conditioned root only where T itself is at 1/2: converged by the Newton step)
                 r.ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
+                r.newton_done = newton;
                 live = false;
                 r.ref_t = t;
                 r.ref_D = D;
@@ -886,7 +892,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         };
         auto halley = [&](auto&& src, int grouped, bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
                           int walks, float scale) {
-            Refine r{false, false, in_range0, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            Refine r{false, false, in_range0, false, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             const f32x2 TSE[1] = {f32x2{e0, e8}};
             for (int k = 0; k < walks && a.passes > 1; k++) {
                 if (__ballot(live) == 0ull) break;
@@ -1023,6 +1029,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         if (r.refined && mb != 0.f)
                             dt = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(r.ref_E, mb - r.ref_t, -r.ref_D);
                     }
+                    if (GSR_LEFT_STATS && r.in_range && !r.refined && !r.ill) flags = r.live ? 16u : r.newton_done ? 32u : 64u;
 #ifdef GSR_DBG_DT
                     if ((flags & kPubRefined) && !(dt < -1e-4f))
                         printf("dbgdt publish (%d,%d) t_ref %.7f ref_t %.7f D %g E %g dt %g\n", x0 + (p & 15), y0 + (p >> 4),
@@ -1118,7 +1125,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     } else if (cnt > 0 || !qin) {
                         publish(p, r);
                     } else {
-                        s_pub_last[p] = 0u;  // no guess: the owner runs the passes
+                        s_pub_last[p] = GSR_LEFT_STATS ? 8u : 0u;  // no guess: the owner runs the passes
                     }
                 }
                 // The pixels not converged after one walk (~30% at C3), compacted and continued by
@@ -1213,6 +1220,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 }
                 const uint32_t n_left = n_pass + n_ill;
                 if constexpr (STATS) st[7] += left3p ? 1 : 0;
+#if GSR_LEFT_STATS
+                // (development) why a pixel is left to the passes: no guess / still live after its walks /
+                // converged by the Newton test but not well conditioned (the rest: the bracket closed
+                // without it, or a root near a window end); ill roots
+                if constexpr (STATS) {
+                    const bool ng = left3p && (s_pub_last[me] & 8u) != 0u;
+                    const bool mr = left3p && !ng && (s_pub_last[me] & 16u) != 0u;
+                    const bool cn = left3p && !ng && (s_pub_last[me] & 32u) != 0u;  // converged by the Newton test, conditioning
+                    const unsigned long long b0 = __ballot(ng), b1 = __ballot(mr), b2 = __ballot(cn),
+                                             b3 = __ballot(left3 && ill);
+                    if ((tid & 63) == 0) {
+                        st[12] += __popcll(b0);
+                        st[13] += __popcll(b1);
+                        st[14] += __popcll(b2);
+                        st[15] += __popcll(b3);
+                    }
+                }
+#endif
                 if (n_left > 0) {  // (block-uniform)
                     if (left3) {
                         const unsigned long long lower = (1ull << (tid & 63)) - 1ull;

@@ -35,5 +35,9 @@ if os.environ.get("GSR_PHASE_CLOCK"):  # a -DGSR_PHASE_CLOCK=1 build: per-wave c
         print(f"clock {name}: {st[8 + k]:.4g} wave-cycles ({st[8 + k] / tot:.3f})")
     print(f"clock total to phase-3 end: {st[15]:.4g}")
     sys.exit(0)
+if os.environ.get("GSR_LEFT_STATS"):  # a -DGSR_LEFT_STATS=1 build: why pixels are left to the passes
+    print("left to the passes: no guess", st[12], "still live after its walks", st[13], "converged (Newton), conditioning", st[14],
+          "| ill roots", st[15], "| the rest (bracket closed, conditioning):", st[7] - st[12] - st[13] - st[14])
+    sys.exit(0)
 for f, name in enumerate(("1 grid", "2 first walk", "2b grouped", "3 passes/dT")):
     print(f"phase {name}: walk wave-steps {st[8 + 2 * f]} active lanes/step {st[9 + 2 * f] / max(st[8 + 2 * f], 1):.2f}")
