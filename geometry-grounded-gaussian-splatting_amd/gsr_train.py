@@ -168,11 +168,13 @@ LAMBDA_DSSIM, LAMBDA_DEPTH_NORMAL, LAMBDA_NCC, LAMBDA_GEO = 0.2, 0.05, 0.6, 0.02
 PATCH_SIZE, PIXEL_NOISE_TH = 3, 1.0
 
 
-def patchmatch(gaussians, render_pkg, view, nearest, depth_normal, kernel_size, pipe):
+def patchmatch_terms(gaussians, render_pkg, view, nearest, kernel_size, pipe) -> dict:
     """PatchMatch.__call__ (utils/loss_utils.py:140-267) without its debug
-    image dumps: the median-depth points of `view` re-observed from `nearest`
-    (sample_depth), the pixel-reprojection geometric loss, and the multi-view
-    NCC of 7x7 half-step patches (warp_patch_ncc) at the consistent pixels."""
+    image dumps, up to its two masked means: the median-depth points of `view`
+    re-observed from `nearest` (sample_depth), the per-pixel reprojection error
+    and weights of the geometric loss with its mask, and the multi-view NCC of
+    7x7 half-step patches (warp_patch_ncc) at the consistent pixels with its
+    weights and mask."""
     H, W = view.image_height, view.image_width
     dev = render_pkg["median_depth"].device
     with torch.no_grad():
@@ -196,9 +198,7 @@ def patchmatch(gaussians, render_pkg, view, nearest, depth_normal, kernel_size, 
     with torch.no_grad():
         d_mask = (sampled["inside"] & (pts_in_nearest[..., -1] > 0.2) & (pts_in_view[..., -1] > 0.2)
                   & (pixel_noise < PIXEL_NOISE_TH) & (render_pkg["median_depth"].squeeze() > 0))
-        weights = torch.exp(-pixel_noise)
-        weights[~d_mask] = 0
-    geo_loss = ((weights * pixel_noise)[d_mask]).mean()
+        weights = torch.exp(-pixel_noise).masked_fill_(~d_mask, 0.0)
     with torch.no_grad():
         d_flat = torch.flatten(d_mask)
         valid = torch.argwhere(d_flat).squeeze(1)
@@ -213,9 +213,30 @@ def patchmatch(gaussians, render_pkg, view, nearest, depth_normal, kernel_size, 
         view.Fx, view.Fy, view.Cx, view.Cy, nearest.Fx, nearest.Fy, nearest.Cx, nearest.Cy, False)
     ncc = torch.clamp(1 - cc, 0.0, 2.0)
     ncc_mask = (ncc < 0.9) & valid_mask
-    ncc = (ncc.squeeze() * w_sel)[ncc_mask.squeeze()]
+    return {"pixel_noise": pixel_noise, "weights": weights, "d_mask": d_mask, "ncc": ncc.squeeze(), "w_sel": w_sel,
+            "ncc_mask": ncc_mask.squeeze()}
+
+
+def masked_mean(x: torch.Tensor, mask: torch.Tensor, empty: float | None = None) -> torch.Tensor:
+    """x[mask].mean() without the boolean gather's device-to-host sync: the
+    masked sum over the mask's count (NaN for an empty mask as the gather's
+    mean, or `empty` when given).  Same value up to summation order, same
+    gradient (mask / count on the selected entries)."""
+    cnt = mask.sum()
+    mean = torch.where(mask, x, torch.zeros((), device=x.device, dtype=x.dtype)).sum() / cnt
+    return mean if empty is None else torch.where(cnt > 0, mean, torch.full_like(mean, empty))
+
+
+def patchmatch(gaussians, render_pkg, view, nearest, depth_normal, kernel_size, pipe):
+    """PatchMatch.__call__ (utils/loss_utils.py:140-267): (ncc_loss, geo_loss).
+    The reference's means over boolean gathers ((weights * pixel_noise)[d_mask],
+    (ncc * weights)[ncc_mask]) are taken as masked sums (`masked_mean`), so the
+    only host synchronisation left is the valid-pixel count warp_patch_ncc
+    needs (tests/test_gpu_train.py checks both forms agree)."""
+    t = patchmatch_terms(gaussians, render_pkg, view, nearest, kernel_size, pipe)
+    geo_loss = masked_mean(t["weights"] * t["pixel_noise"], t["d_mask"])
     # (the reference returns 0 when no pixel qualifies; the mean of an empty set is NaN)
-    ncc_loss = ncc.mean() if ncc.numel() else ncc.new_zeros(())
+    ncc_loss = masked_mean(t["ncc"] * t["w_sel"], t["ncc_mask"], empty=0.0)
     return ncc_loss, geo_loss
 
 

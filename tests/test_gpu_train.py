@@ -1,0 +1,59 @@
+"""The training iteration's PatchMatch losses (gsr_train.patchmatch): the
+sync-free masked means against the reference's boolean-gather means
+(utils/loss_utils.py:140-267: ((weights * pixel_noise)[d_mask]).mean() and
+(ncc * weights)[ncc_mask].mean()), values and gradients, on one small
+synthetic scene; and one whole TrainStep runs with finite losses."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def setup():
+    import gsr_train
+    step, view, nearest = gsr_train.synthetic_training_setup(20_000, 320, 240, device="cuda", seed=3)
+    return gsr_train, step, view, nearest
+
+
+def _grads(loss, params):
+    return torch.autograd.grad(loss, params, retain_graph=True, allow_unused=True)
+
+
+def test_patchmatch_masked_means_match_gathers(setup):
+    gsr_train, step, view, nearest = setup
+    from gaussian_renderer import render
+    g = step.g
+    pkg = render(view, g, step.pipe, step.bg, step.kernel_size, require_depth=True)
+    t = gsr_train.patchmatch_terms(g, pkg, view, nearest, step.kernel_size, step.pipe)
+    assert int(t["d_mask"].sum()) > 100 and int(t["ncc_mask"].sum()) > 100, "scene too sparse to test"
+    geo_ref = ((t["weights"] * t["pixel_noise"])[t["d_mask"]]).mean()
+    ncc_ref = (t["ncc"] * t["w_sel"])[t["ncc_mask"]].mean()
+    geo = gsr_train.masked_mean(t["weights"] * t["pixel_noise"], t["d_mask"])
+    ncc = gsr_train.masked_mean(t["ncc"] * t["w_sel"], t["ncc_mask"], empty=0.0)
+    torch.testing.assert_close(geo, geo_ref, rtol=1e-5, atol=0.0)
+    torch.testing.assert_close(ncc, ncc_ref, rtol=1e-5, atol=0.0)
+    params = [g._xyz, g._opacity, g._scaling, g._rotation]
+    for a, b in ((geo, geo_ref), (ncc, ncc_ref)):
+        for ga, gb in zip(_grads(a, params), _grads(b, params)):
+            assert (ga is None) == (gb is None)
+            if ga is not None:
+                assert torch.isfinite(ga).all()
+                assert float((ga - gb).norm()) <= 1e-5 * float(gb.norm()) + 1e-12
+
+
+def test_masked_mean_empty_mask():
+    import gsr_train
+    x = torch.randn(64, device="cuda", requires_grad=True)
+    m = torch.zeros(64, dtype=torch.bool, device="cuda")
+    assert torch.isnan(gsr_train.masked_mean(x, m))
+    z = gsr_train.masked_mean(x, m, empty=0.0)
+    assert float(z) == 0.0
+    (gx,) = torch.autograd.grad(z, x)
+    assert torch.equal(gx, torch.zeros_like(gx))
+
+
+def test_train_step_runs(setup):
+    _, step, view, nearest = setup
+    losses = [float(step.step(view, nearest)) for _ in range(2)]
+    assert all(torch.isfinite(torch.tensor(losses)))
