@@ -168,6 +168,33 @@ LAMBDA_DSSIM, LAMBDA_DEPTH_NORMAL, LAMBDA_NCC, LAMBDA_GEO = 0.2, 0.05, 0.6, 0.02
 PATCH_SIZE, PIXEL_NOISE_TH = 3, 1.0
 
 
+_GRIDS: dict = {}
+
+
+def _pixel_grids(view, dev):
+    """Per camera (cached): the rays (ix, iy, 1) of the reference's pixel
+    grid (loss_utils.py:148-152), and its (H, W, 2) int32 / float pixel
+    coordinates."""
+    key = (view.image_width, view.image_height, view.Fx, view.Fy, view.Cx, view.Cy, str(dev))
+    if key not in _GRIDS:
+        W, H = view.image_width, view.image_height
+        ix = (torch.arange(W, device=dev, dtype=torch.float32) - view.Cx) / view.Fx
+        iy = (torch.arange(H, device=dev, dtype=torch.float32) - view.Cy) / view.Fy
+        rays = torch.stack([ix[None, :].expand(H, W), iy[:, None].expand(H, W), torch.ones(H, W, device=dev)], -1)
+        gx, gy = torch.meshgrid(torch.arange(W, device=dev, dtype=torch.int32),
+                                torch.arange(H, device=dev, dtype=torch.int32), indexing="xy")
+        pixels = torch.stack([gx, gy], dim=-1)
+        if len(_GRIDS) > 8:
+            _GRIDS.clear()
+        _GRIDS[key] = (rays.contiguous(), pixels, pixels.float())
+    return _GRIDS[key]
+
+
+def _mat3(x: torch.Tensor, M: torch.Tensor) -> torch.Tensor:
+    """x @ M for x [..., 3] and a 3x3 M, as three broadcast multiply-adds."""
+    return torch.addcmul(torch.addcmul(x[..., 0:1] * M[0], x[..., 1:2], M[1]), x[..., 2:3], M[2])
+
+
 def patchmatch_terms(gaussians, render_pkg, view, nearest, kernel_size, pipe) -> dict:
     """PatchMatch.__call__ (utils/loss_utils.py:140-267) without its debug
     image dumps, up to its two masked means: the median-depth points of `view`
@@ -175,26 +202,22 @@ def patchmatch_terms(gaussians, render_pkg, view, nearest, kernel_size, pipe) ->
     and weights of the geometric loss with its mask, and the multi-view NCC of
     7x7 half-step patches (warp_patch_ncc) at the consistent pixels with its
     weights and mask."""
-    H, W = view.image_height, view.image_width
     dev = render_pkg["median_depth"].device
+    rays, pixels, pixels_f = _pixel_grids(view, dev)
     with torch.no_grad():
-        ix = (torch.arange(W, device=dev, dtype=torch.float32) - view.Cx) / view.Fx
-        iy = (torch.arange(H, device=dev, dtype=torch.float32) - view.Cy) / view.Fy
         view_to_nearest_T = (-view.world_view_transform[:3, :3].T @ nearest.R @ nearest.T
                              + view.world_view_transform[3, :3])
         nearest_to_view_R = nearest.R.transpose(1, 0) @ view.world_view_transform[:3, :3]
     depth_reshape = render_pkg["median_depth"].squeeze().unsqueeze(-1)
-    pts = torch.cat([depth_reshape * ix[None, :, None], depth_reshape * iy[:, None, None], depth_reshape], dim=-1)
-    pts = (pts - view.T) @ view.R.T
+    # (the reference's cat of depth * (ix, iy, 1) and its two (H, W, 3) @ (3, 3) products; as broadcast
+    # multiply-adds — a K = 3 matmul took a 130-us library GEMM each way)
+    pts = _mat3(depth_reshape * rays - view.T, view.R.T)
     sampled = sample_depth(pts, nearest, gaussians, pipe, kernel_size)
     pts_in_nearest = sampled["sampled_depth"]
-    pts_in_view = view_to_nearest_T + pts_in_nearest @ nearest_to_view_R
+    pts_in_view = view_to_nearest_T + _mat3(pts_in_nearest, nearest_to_view_R)
     proj = pts_in_view[..., :2] / torch.clamp_min(pts_in_view[..., 2:], 1e-7)
     proj = torch.addcmul(proj.new_tensor([view.Cx, view.Cy]), proj.new_tensor([view.Fx, view.Fy]), proj)
-    gx, gy = torch.meshgrid(torch.arange(W, device=dev, dtype=torch.int32),
-                            torch.arange(H, device=dev, dtype=torch.int32), indexing="xy")
-    pixels = torch.stack([gx, gy], dim=-1)
-    pixel_noise = torch.pairwise_distance(proj, pixels.float())
+    pixel_noise = torch.pairwise_distance(proj, pixels_f)
     with torch.no_grad():
         d_mask = (sampled["inside"] & (pts_in_nearest[..., -1] > 0.2) & (pts_in_view[..., -1] > 0.2)
                   & (pixel_noise < PIXEL_NOISE_TH) & (render_pkg["median_depth"].squeeze() > 0))

@@ -57,3 +57,23 @@ def test_train_step_runs(setup):
     _, step, view, nearest = setup
     losses = [float(step.step(view, nearest)) for _ in range(2)]
     assert all(torch.isfinite(torch.tensor(losses)))
+
+
+def test_mat3_and_rays_match_the_reference_products():
+    """The broadcast forms of the PatchMatch glue equal the reference's cat and
+    (H, W, 3) @ (3, 3) products (loss_utils.py:148-156) to fp32 rounding."""
+    import gsr_train
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(48, 64, 3, generator=gen).cuda()
+    M = torch.randn(3, 3, generator=gen).cuda()
+    torch.testing.assert_close(gsr_train._mat3(x, M), x @ M, rtol=1e-6, atol=1e-6)
+    from types import SimpleNamespace
+    view = SimpleNamespace(image_width=64, image_height=48, Fx=50.0, Fy=52.0, Cx=31.5, Cy=23.5)
+    rays, pixels, pixels_f = gsr_train._pixel_grids(view, torch.device("cuda"))
+    depth = torch.rand(48, 64, 1, generator=gen).cuda()
+    ix = (torch.arange(64, device="cuda", dtype=torch.float32) - view.Cx) / view.Fx
+    iy = (torch.arange(48, device="cuda", dtype=torch.float32) - view.Cy) / view.Fy
+    ref = torch.cat([depth * ix[None, :, None], depth * iy[:, None, None], depth], dim=-1)
+    assert torch.equal(depth * rays, ref)
+    assert pixels.dtype == torch.int32 and torch.equal(pixels[..., 0][0], torch.arange(64, device="cuda", dtype=torch.int32))
+    assert torch.equal(pixels_f, pixels.float())
