@@ -346,6 +346,9 @@ constexpr bool kP2NoEnds = GSR_P2_NOENDS;
 #define GSR_P1_ONE 1  // (0: up to 4 Halley walks in phase 1; render_fwd 0.672 -> 0.628 ms at C3 with 1, profiles/r4_ab_p1_one.txt)
 #endif
 constexpr bool kP1One = GSR_P1_ONE;
+#ifndef GSR_P3_ILL_SHIFT
+#define GSR_P3_ILL_SHIFT 3  // phase 3: an ill-conditioned root's group is at least G_p >> this (2 and 4: the same within noise, profiles/r4_ab_p3_ill_floor.txt)
+#endif
 #ifndef GSR_LEFT_STATS
 #define GSR_LEFT_STATS 0  // (development: render stats slots 12..15 count why pixels are left to the passes)
 #endif
@@ -1254,7 +1257,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     // largest powers of two with n_pass G_p + n_ill G_i <= 256 and G_i >= G_p / 8; a
                     // pixel's group is aligned (the pass groups first), so its DPP combine stays inside it
                     int lgp = kAdaptGroups ? 4 : 0;
-                    while (lgp > 0 && (n_pass << lgp) + n_ill * (uint32_t)max(1, (1 << lgp) >> 3) > (uint32_t)kTilePixels)
+                    while (lgp > 0 && (n_pass << lgp) + n_ill * (uint32_t)max(1, (1 << lgp) >> GSR_P3_ILL_SHIFT) > (uint32_t)kTilePixels)
                         lgp--;
                     int lgi = lgp;
                     while (lgi > 0 && (n_pass << lgp) + (n_ill << lgi) > (uint32_t)kTilePixels) lgi--;
