@@ -346,6 +346,12 @@ constexpr bool kP2NoEnds = GSR_P2_NOENDS;
 #define GSR_P1_ONE 1  // (0: up to 4 Halley walks in phase 1; render_fwd 0.672 -> 0.628 ms at C3 with 1, profiles/r4_ab_p1_one.txt)
 #endif
 constexpr bool kP1One = GSR_P1_ONE;
+// Phase 2b: Halley walks of a straggler before it is left to the passes (3: C2 render_fwd 0.500 -> 0.490 ms,
+// C3 unchanged, profiles/r4_ab_p2b_walks.txt; the sample path keeps kRefineWalks)
+#ifndef GSR_P2B_WALKS
+#define GSR_P2B_WALKS 2
+#endif
+constexpr int kP2bWalks = GSR_P2B_WALKS;
 #ifndef GSR_P3_ILL_SHIFT
 #define GSR_P3_ILL_SHIFT 3  // phase 3: an ill-conditioned root's group is at least G_p >> this (2 and 4: the same within noise, profiles/r4_ab_p3_ill_floor.txt)
 #endif
@@ -1165,7 +1171,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                                       gfilter(G2b, opaque_int(tid) & (G2b - 1))};
                     };
                     const Refine r = halley(src, G2b, true, t, s_pub_m0[p], s_pub_hi[p], false, 0.f, 0.f, true,
-                                            kRefineWalks - 1, fmaxf(t, 1.f));
+                                            kP2bWalks, fmaxf(t, 1.f));
                     if ((tid & (G2b - 1)) == 0)
                         GSR_DBG(p, "p2b: from %.7f -> live %d in %d ref %d ill %d t_ref %.7f t %.7f [%.7f %.7f] D %g\n", t,
                                 (int)r.live, (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.t, r.lo, r.hi, r.ref_D);
