@@ -56,14 +56,12 @@ CLOCK_HZ = 2.4e9  # max clock (MI355X_MICROARCH.md chip table)
 SIMDS = 256 * 4  # 256 CUs x 4 SIMD-32
 # VALU issue peak (MI355X_MICROARCH.md, per-instruction cycle constants): a wave64 VALU instruction
 # occupies its SIMD-32 for 2 cycles when waves interleave (one wave alone: 4); a transcendental
-# (v_exp / v_rsq / v_rcp / v_sqrt / v_log) twice that (one wave alone: 8)
+# (v_exp / v_rsq / v_rcp / v_sqrt / v_log) twice that (one wave alone: 8).  The box's plain-fp32 code
+# does not reach it (tools/probe/valu_rate.hip, profiles/r4_valu_rate_probe.txt: 4.41 cycles per
+# instruction at best), so `roofline.bound` is decided by the measured VALU pipe occupancy
+# (SQ_ACTIVE_INST_VALU, in 4-cycle units, over the launch's SIMD-cycles), not by this peak.
 VALU_PEAK_CYCLES = 2
 TRANS_PEAK_CYCLES = 4
-# The plain-VALU issue rate measured on the box (tools/probe/valu_rate.hip, profiles/r4_valu_rate_probe.txt):
-# 16 independent v_fma_f32 chains per wave at 8 waves per SIMD sustain 4.41 cycles per wave64 instruction
-# per SIMD (2.4 GHz assumed, like the rates above) — the datasheet's 2 is not reached by plain fp32 code;
-# v_pk_fma_f32 (two fmas per lane) issues at about the same rate.
-VALU_MEASURED_CYCLES = 4.41
 
 
 def log(*a):
@@ -113,14 +111,21 @@ def launch_ranks(cmd, args) -> int:
     output; rank 0 prints the JSON line."""
     import subprocess
 
-    if args.dist_backend == "nccl":
-        ndev = torch.cuda.device_count()  # (does not initialise the GPU on this image)
-        if ndev < args.gpus:
-            raise SystemExit(f"bench.py: --gpus {args.gpus} with RCCL needs {args.gpus} devices, {ndev} visible "
-                             "(RCCL refuses two ranks on one device; --dist-backend gloo rehearses N ranks on one GPU)")
+    # (no GPU API here: the device check runs in the ranks, check_devices)
     log("[bench] launching", " ".join(cmd))
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.call(cmd, env=env)
+
+
+def check_devices(args, world: int) -> None:
+    """In each rank, before it touches the GPU: RCCL refuses two ranks on one
+    device, so an N-rank RCCL bench needs N visible devices (device_count()
+    does not initialise the GPU on this image)."""
+    if world > 1 and args.dist_backend == "nccl":
+        ndev = torch.cuda.device_count()
+        if ndev < world:
+            raise SystemExit(f"bench.py: --gpus {world} with RCCL needs {world} devices, {ndev} visible "
+                             "(RCCL refuses two ranks on one device; --dist-backend gloo rehearses N ranks on one GPU)")
 
 
 def parse():
@@ -198,7 +203,9 @@ def stage_bytes(P, K, K_live, HW, shm, sgm, geom, K_contrib=None):
         "render_fwd": K_r * (4 + G) + HW * Opx,
         "bwd_clear": P * A,
         "render_bwd": HW * Ipx + K_r * (4 + G),
-        "preprocess_bwd": P * (A + Bp + 8 + Bp),
+        # accumulators, geometry rows (44 B), the forward-saved colour -> direction Jacobian (36 B, in place
+        # of the SH row) and the SG lobe rows, radii + clamped; every gradient row written
+        "preprocess_bwd": P * (A + 44 + 36 + 28 * sgm + 8 + Bp),
     }
 
 
@@ -212,9 +219,10 @@ def load_pmc(workload_key, kernel_stage):
         with open(os.path.join(ROOT, "profiles", name)) as f:
             st = json.load(f)["stages"][kernel_stage]
         sq = st.get("sq_per_call", {})
-        return st["hbm_bytes_per_launch"], sq.get("SQ_INSTS_VALU"), sq.get("SQ_INSTS_VALU_TRANS_F32"), name
+        return (st["hbm_bytes_per_launch"], sq.get("SQ_INSTS_VALU"), sq.get("SQ_INSTS_VALU_TRANS_F32"),
+                sq.get("SQ_ACTIVE_INST_VALU"), name)
     except Exception:  # noqa: BLE001 - absent summary -> null
-        return None, None, None, None
+        return None, None, None, None, None
 
 
 def host_cores():
@@ -397,6 +405,7 @@ def main():
         if rank == 0:
             print(json.dumps({"n_gpus": world, "rank_sum": ranks}), flush=True)
         return
+    check_devices(args, world)
     # (a rehearsal with more ranks than GPUs shares the devices; device_count() does not initialise the GPU)
     dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     if args.e2e:
@@ -569,18 +578,23 @@ def main():
     if not args.all_stage_events:  # the other stages from the untimed table
         per_launch = {k: (per_launch[k] if k == dom else v) for k, v in table_ms.items()}
     achieved = algo[dom] / (per_launch[dom] * 1e-3) / 1e9
-    traffic, valu_insts, trans_insts, pmc_file = (load_pmc(args.workload_key, dom) if args.preset_workload
-                                                  else (None, None, None, None))
+    traffic, valu_insts, trans_insts, valu_active, pmc_file = (
+        load_pmc(args.workload_key, dom) if args.preset_workload else (None, None, None, None, None))
     hbm_frac = achieved / HBM_PEAK_GBPS
     # VALU-issue fraction of the same launch: the PMC pass's VALU instruction counts for this kernel
     # (per-launch constants of the workload) at their peak issue cost — 2 SIMD cycles per wave64
     # instruction, 4 per transcendental — over the SIMD-cycles of the launch duration measured live here
     simd_cycles = per_launch[dom] * 1e-3 * CLOCK_HZ * SIMDS
-    valu_frac = None
+    valu_frac = pipe_busy = None
     if valu_insts:
         tr = trans_insts or 0
         valu_frac = (valu_insts * VALU_PEAK_CYCLES + tr * (TRANS_PEAK_CYCLES - VALU_PEAK_CYCLES)) / simd_cycles
-    bound = "valu" if valu_frac is not None and valu_frac > hbm_frac else "hbm"
+    if valu_active:  # cycles the SIMDs' arbiters spent on VALU instructions (4-cycle units), measured
+        pipe_busy = valu_active * 4 / simd_cycles
+    # the bound is the measured pipe occupancy against the HBM fraction (the datasheet-rate fraction
+    # understates what binds: the box issues plain fp32 at ~4.4 cycles, not 2)
+    busy = pipe_busy if pipe_busy is not None else valu_frac
+    bound = "valu" if busy is not None and busy > hbm_frac else "hbm"
     roofline = {"bound": bound, "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(hbm_frac, 5),
                 "traffic": traffic, "algorithmic_bytes_per_launch": int(algo[dom]),
@@ -595,9 +609,9 @@ def main():
                     "trans_insts_per_launch": None if trans_insts is None else int(trans_insts),
                     "peak_cycles_per_inst": VALU_PEAK_CYCLES, "peak_cycles_per_trans": TRANS_PEAK_CYCLES,
                     "clock_hz": CLOCK_HZ, "simds": SIMDS,
-                    "frac_of_measured_issue_rate": round(valu_insts * VALU_MEASURED_CYCLES / simd_cycles, 4),
-                    "measured_cycles_per_inst": VALU_MEASURED_CYCLES,
-                    "measured_source": "profiles/r4_valu_rate_probe.txt"},
+                    "pipe_busy": None if pipe_busy is None else round(pipe_busy, 4),
+                    "pipe_busy_source": "SQ_ACTIVE_INST_VALU x 4 / SIMD-cycles of the live launch time",
+                    "bound_from": "pipe_busy" if pipe_busy is not None else "frac"},
                 "pmc_source": None if pmc_file is None else f"profiles/{pmc_file}",
                 "stage_ms": {k: round(v, 4) for k, v in per_launch.items()}}
     total_algo = sum(v for k, v in algo.items() if per_launch.get(k, 0.0) > 0.0)  # the stages this step ran

@@ -394,8 +394,8 @@ int option(int which) { return (which >= 0 && which < kNumOptions) ? g_options[w
 
 extern "C" {
 
-int gsr_debug_render_stats(unsigned long long* out16, int reset) {
-    hipError_t e = gsr::read_render_stats(out16, reset != 0);
+int gsr_debug_render_stats(unsigned long long* out20, int reset) {
+    hipError_t e = gsr::read_render_stats(out20, reset != 0);
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "render stats", e);
 }
 
@@ -467,7 +467,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 16; }
+int gsr_abi_version(void) { return 17; }
 
 int gsr_backward_chunk_size(int P, int chunks) {
     if (P < 0 || chunks < 1) return -1;

@@ -279,8 +279,10 @@ struct PixSrc {
 // [4] waves running the refinement, [5] waves sending a lane to the
 // reference's passes, [6] refinement lane-walks, [7] lanes left to the passes;
 // [8 + 2 f], [9 + 2 f]: walk wave-steps and their active lanes of render-path
-// phase f = 0 (1: grid pixels), 1 (2: first walk), 2 (2b: grouped), 3 (3: passes / dT walks).
-constexpr int kRenderStats = 16;
+// phase f = 0 (1: grid pixels), 1 (2: first walk), 2 (2b: grouped), 3 (3: passes / dT walks);
+// [16] ill-conditioned roots kept (phase 3 computes their dT/dt_m only), [17] lanes phase 3 gives its
+// listed pixels (render path); [18], [19] reserved.
+constexpr int kRenderStats = 20;
 __device__ unsigned long long g_render_stats[kRenderStats];
 
 // SAMPLE: queries at arbitrary points — lanes hold points of one tile's
@@ -318,16 +320,6 @@ __device__ unsigned long long g_render_stats[kRenderStats];
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
-// Strip culling of the composite (render path): a wave covers a 16 x 4 strip
-// of the tile, and a record whose alpha >= 1/255 region misses the strip (the
-// tile culling's exact ellipse test, tiles.h, on the strip's 4 pixel rows and
-// the tile's 16 columns) fails the power / alpha test at every pixel of it.
-// The staging thread computes the record's 4 strip bits; each wave then walks
-// only its records, the next index found by a scalar find-first-set over two
-// 64-bit ballots of the batch, so a skipped record costs no vector work.
-#ifndef GSR_STRIP_CULL
-#define GSR_STRIP_CULL 0
-#endif
 
 // Median-depth phases 2b and 3 (render path) give each listed pixel as many
 // lanes as one round of the block allows (up to 16), instead of 4 and 1.
@@ -364,27 +356,6 @@ constexpr int kP2bWalks = GSR_P2B_WALKS;
 #define GSR_P2B_ONE_ROUND 1  // (C2 render_fwd 0.523 -> 0.503 ms, C3 unchanged; profiles/r4_ab_p2b_one_round.txt)
 #endif
 
-// Bit s set: the record's alpha >= 1/255 region (margin as tile culling) meets
-// pixel rows [y0 + 4 s, y0 + 4 s + 3] x columns [x0, x0 + 15].
-__device__ __forceinline__ uint32_t strip_bits(const float4& w0, const float4& w1, int x0, int y0) {
-    const Ellipse E = make_ellipse(w0, w1, 0.f);
-    if (E.mode == 2) return 0u;
-    if (E.mode == 1) return 15u;
-    uint32_t bits = 0u;
-#pragma unroll
-    for (int st = 0; st < 4; st++) {
-        const float vlo = fmaxf(E.my - (float)(y0 + 4 * st + 3), -E.vmax);
-        const float vhi = fminf(E.my - (float)(y0 + 4 * st), E.vmax);
-        const float vu = fminf(fmaxf(-E.b * E.kst, vlo), vhi);
-        const float vl = fminf(fmaxf(E.b * E.kst, vlo), vhi);
-        const float umax = (-E.b * vu + sqrtf(fmaxf(E.a * E.tau - E.det * vu * vu, 0.f))) * E.ia;
-        const float umin = (-E.b * vl - sqrtf(fmaxf(E.a * E.tau - E.det * vl * vl, 0.f))) * E.ia;
-        // pixel centres x in [mx - umax, mx - umin] meet [x0, x0 + 15]
-        const bool hit = vlo <= vhi && E.mx - umax <= (float)(x0 + 15) && E.mx - umin >= (float)x0;
-        bits |= hit ? (1u << st) : 0u;
-    }
-    return bits;
-}
 template <bool GEOM, bool STATS = false, bool SAMPLE = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, 8))) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 128 x 16 B = 8 KB) aliased with the
@@ -394,8 +365,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     // blended contributors per pixel, word-major (word w of lane t at w * 256 + t: conflict-free)
     __shared__ uint32_t s_mask[GEOM ? kTilePixels * kMaskWords : 1];
     __shared__ int s_alive[2][4];
-    constexpr bool kStrip = GSR_STRIP_CULL && !SAMPLE;
-    __shared__ uint8_t s_strip[kStrip ? kBatch : 1];
     __shared__ uint32_t s_union[kBlendWords];  // (render path) entries some pixel of the tile blended
     __shared__ uint32_t s_max[4];
     // (render path, GEOM) the median-depth phases: per pixel the composite's last contributor,
@@ -558,46 +527,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             s_w1[tid] = w1;
             s_w2[tid] = sp->w2;
             if constexpr (!SAMPLE) s_w3[tid] = sp->w3;
-            if constexpr (kStrip) s_strip[tid] = (uint8_t)strip_bits(w0, w1, px - (tid & 15), py - (tid >> 4));
         }
         __syncthreads();
         const int n = min(kBatch, toDo);
-        if constexpr (kStrip) {
-            // this wave's records of the batch, walked in list order by find-first-set
-            const int l = tid & 63;
-            unsigned long long m0 = __ballot(l < n && ((s_strip[l] >> wave) & 1u));
-            unsigned long long m1 = __ballot(64 + l < n && ((s_strip[64 + l] >> wave) & 1u));
-            while (!done && (m0 | m1) != 0ull) {
-                int j;
-                if (m0) {
-                    j = __builtin_ctzll(m0);
-                    m0 &= m0 - 1ull;
-                } else {
-                    j = 64 + __builtin_ctzll(m1);
-                    m1 &= m1 - 1ull;
+        if constexpr (!GEOM && !SAMPLE) {
+            // no depth: the batch in 32-entry words, each word's blended bits ORed over the wave
+            // (DPP) and set by one lane (one atomic per blending step: render_fwd 0.214 -> 0.181 ms
+            // without depth at C3; with no mask at all the backward walks every entry: 0.34 -> 0.40 ms)
+            for (int j0 = 0; j0 < n; j0 += 32) {
+                wbits = 0u;
+                const int j1 = min(n, j0 + 32);
+                for (int j = j0; !done && j < j1; j++)
+                    step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
+                const int word = (i * kBatch + j0) >> 5;
+                if (word < kBlendWords) {
+                    const uint32_t v = wave_or_dpp(wbits);
+                    if ((tid & 63) == 0 && v) atomicOr(&s_union[word], v);
                 }
-                step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
             }
         } else {
-            if constexpr (!GEOM && !SAMPLE) {
-                // no depth: the batch in 32-entry words, each word's blended bits ORed over the wave
-                // (DPP) and set by one lane (one atomic per blending step: render_fwd 0.214 -> 0.181 ms
-                // without depth at C3; with no mask at all the backward walks every entry: 0.34 -> 0.40 ms)
-                for (int j0 = 0; j0 < n; j0 += 32) {
-                    wbits = 0u;
-                    const int j1 = min(n, j0 + 32);
-                    for (int j = j0; !done && j < j1; j++)
-                        step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
-                    const int word = (i * kBatch + j0) >> 5;
-                    if (word < kBlendWords) {
-                        const uint32_t v = wave_or_dpp(wbits);
-                        if ((tid & 63) == 0 && v) atomicOr(&s_union[word], v);
-                    }
-                }
-            } else {
-                for (int j = 0; !done && j < n; j++)
-                    step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
-            }
+            for (int j = 0; !done && j < n; j++)
+                step(s_w0[j], s_w1[j], [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j);
         }
     }
 
@@ -1228,7 +1178,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     n_ill += (uint32_t)s_alive[0][w];
                 }
                 const uint32_t n_left = n_pass + n_ill;
-                if constexpr (STATS) st[7] += left3p ? 1 : 0;
+                if constexpr (STATS) {
+                    st[7] += left3p ? 1 : 0;
+                    st[16] += (left3 && ill) ? 1 : 0;
+                }
 #if GSR_LEFT_STATS
                 // (development) why a pixel is left to the passes: no guess / still live after its walks /
                 // converged by the Newton test but not well conditioned (the rest: the bracket closed
@@ -1268,6 +1221,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     int lgi = lgp;
                     while (lgi > 0 && (n_pass << lgp) + (n_ill << lgi) > (uint32_t)kTilePixels) lgi--;
                     const uint32_t np_lanes = n_pass << lgp;
+                    if constexpr (STATS) st[17] += tid == 0 ? np_lanes + (n_ill << lgi) : 0u;
                     auto lane_group = [&](uint32_t t, int& lg) -> uint32_t {  // (listed pixel of lane t, its group log2)
                         const bool is_p = t < np_lanes;
                         lg = is_p ? lgp : lgi;

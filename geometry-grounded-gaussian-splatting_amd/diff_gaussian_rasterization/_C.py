@@ -44,7 +44,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 
 def _load():
@@ -142,7 +142,7 @@ def backward_chunk_size(P: int, chunks: int) -> int:
 
 def debug_render_stats(reset: bool = True) -> list:
     """Counters of forward launches made with OPT_RENDER_STATS (render_fwd.hip)."""
-    out = (ctypes.c_ulonglong * 16)()
+    out = (ctypes.c_ulonglong * 20)()
     _check(_load().gsr_debug_render_stats(out, int(bool(reset))))
     return list(out)
 

@@ -293,6 +293,14 @@ class OverlappedViewGrads:
     the rasterizer hands to autograd are then already summed over the
     ranks' views; autograd carries them through the getters as usual.
 
+    Failure: a rank whose backward fails part-way posts its remaining
+    ranges on NaN rows (no peer blocks) and re-raises.  Every backward ends
+    with one more tiny all-reduce (MAX) of a failure flag on every rank, read
+    back by the host, so the PEERS raise too ("a peer rank's rasterizer
+    backward failed") instead of handing NaN-summed gradients to the
+    optimizer.  That read is the exchange's one host synchronisation per
+    backward, after its last collective.
+
     Semantics: each rasterizer backward exchanges its own gradients, so
     several renders per step and gradient accumulation sum correctly (the
     exchange is linear).  Gradients of other loss terms on the same
@@ -304,6 +312,7 @@ class OverlappedViewGrads:
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, chunks: int = 4, expand=None):
         self.group = group
+        self._status = None  # one float per backward: MAX over the ranks of "this rank's backward failed"
         self.chunks = max(1, int(chunks))
         self.world = dist.get_world_size(group)
         if expand is None:
@@ -447,12 +456,25 @@ class OverlappedViewGrads:
                 self._post(b, e, rows, nan(3 * n) if self._sh else None)
                 b = e
         finally:
-            works, self._works = self._works, []
-            for w in works:
-                try:
-                    w.wait()
-                except Exception:  # noqa: BLE001 - already failing; the original error is what is raised
-                    pass
+            try:
+                self._post_status(True)
+            finally:
+                works, self._works = self._works, []
+                for w in works:
+                    try:
+                        w.wait()
+                    except Exception:  # noqa: BLE001 - already failing; the original error is what is raised
+                        pass
+
+    def _post_status(self, failed: bool) -> None:
+        """The backward's last collective, posted by every rank exactly once
+        per backward (by finish, or by abort on the failing rank): MAX of the
+        ranks' failure flags."""
+        dev = self._campos_local.device if self._campos_local is not None else "cpu"
+        if self._status is None or self._status.device != torch.device(dev):
+            self._status = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._status.fill_(1.0 if failed else 0.0)
+        self._works.append(dist.all_reduce(self._status, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
 
     def finish(self, grads, means3D, sg_axis, sg_sharpness, sg_color, sh_degree: int, sg_degree: int) -> None:
         if self._next != self._P:
@@ -460,9 +482,13 @@ class OverlappedViewGrads:
             self.abort()
             raise RuntimeError(msg)
         self._active = False
+        self._post_status(False)
         for w in self._works:
-            w.wait()  # (RCCL: the backward's stream waits for the collective; no host synchronisation)
+            w.wait()  # (RCCL: the backward's stream waits for the collective)
         self._works = []
+        if float(self._status) > 0.0:  # host read of the flag: every rank learns that one failed
+            raise RuntimeError("OverlappedViewGrads: a peer rank's rasterizer backward failed; this step's summed "
+                               "gradients are invalid (NaN in that rank's ranges)")
         if not self._sh or self._P == 0:
             return
         (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dsg_axis, dsg_sharpness, dsg_color, dscales,

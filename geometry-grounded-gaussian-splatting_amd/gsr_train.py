@@ -257,8 +257,9 @@ def patchmatch(gaussians, render_pkg, view, nearest, depth_normal, kernel_size, 
     only host synchronisation left is the valid-pixel count warp_patch_ncc
     needs (tests/test_gpu_train.py checks both forms agree)."""
     t = patchmatch_terms(gaussians, render_pkg, view, nearest, kernel_size, pipe)
-    geo_loss = masked_mean(t["weights"] * t["pixel_noise"], t["d_mask"])
-    # (the reference returns 0 when no pixel qualifies; the mean of an empty set is NaN)
+    # The reference returns (0, 0) when no pixel passes d_mask (loss_utils.py:223-224) and its NCC mean is
+    # over a non-empty set otherwise; the mean of an empty set would be NaN, so both means take empty=0.
+    geo_loss = masked_mean(t["weights"] * t["pixel_noise"], t["d_mask"], empty=0.0)
     ncc_loss = masked_mean(t["ncc"] * t["w_sel"], t["ncc_mask"], empty=0.0)
     return ncc_loss, geo_loss
 

@@ -457,8 +457,8 @@ enum gsr_option {
     GSR_OPT_PBWD_STAGE = 10
 };
 int gsr_set_option(int opt, int value);
-/* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (16 values, see render_fwd.hip). */
-int gsr_debug_render_stats(unsigned long long* out16, int reset);
+/* Diagnostic counters of GSR_OPT_RENDER_STATS forward launches (20 values, see render_fwd.hip). */
+int gsr_debug_render_stats(unsigned long long* out20, int reset);
 
 /*
  * Introspection of a forward's opaque buffers (test hook, no reference

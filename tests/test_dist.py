@@ -305,7 +305,7 @@ def _error_worker(rank, world, port, outdir):
     try:
         ex.settle(True)
         ex.finish(grads, torch.randn(P, 3), None, None, None, 3, 0)
-    except ValueError as e:
+    except (ValueError, RuntimeError) as e:
         raised = str(e)
     out = {"raised": raised, "works_left": len(ex._works), "active": ex._active,
            "means3D": grads[3], "mine": mine[3]}
@@ -328,13 +328,16 @@ def _error_worker(rank, world, port, outdir):
 def test_overlapped_exchange_failure_keeps_ranks_in_lockstep(tmp_path):
     """A range whose exchange raises on one rank: that rank still
     posts every remaining range's collectives — on NaN rows — waits for all of
-    its works and re-raises; the peer finishes its backward (no deadlock) with
-    the failed rank's ranges visibly NaN, and the next step runs normally."""
+    its works and re-raises; the peer's backward completes its collectives (no
+    deadlock) and then raises too (the failure flag all-reduced at
+    the end of every backward), so no rank hands NaN-summed gradients to its
+    optimizer; the next step runs normally on both."""
     port = _free_port()
     mp.start_processes(_error_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
     e0 = torch.load(tmp_path / "e0.pt", weights_only=True)
     e1 = torch.load(tmp_path / "e1.pt", weights_only=True)
-    assert e0["raised"] == "injected failure in range [8, 16)" and e1["raised"] is None
+    assert e0["raised"] == "injected failure in range [8, 16)"
+    assert e1["raised"] is not None and "a peer rank's rasterizer backward failed" in e1["raised"]
     assert e0["works_left"] == 0 and not e0["active"] and not e1["active"]
     m1 = e1["means3D"]
     torch.testing.assert_close(m1[:8], e0["mine"][:8] + e1["mine"][:8])  # posted before the failure: summed

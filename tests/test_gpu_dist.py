@@ -330,3 +330,157 @@ def test_two_ranks_exchange_sums_views_on_gpu(tmp_path, sg_degree):
             assert bool(torch.isfinite(a).all()), (form, k)
             err = float((a.double() - want).norm() / want.norm().clamp_min(1e-30))
             assert err <= 1e-5, (form, k, err)
+
+
+# ---- C4 / C5 at their full workload: N ranks sharing cuda:0 (gloo) ----
+def _checksum(t: torch.Tensor) -> int:
+    """A position-weighted checksum of a float32 tensor's bit patterns (equal
+    checksums on every rank: the replicas are bit-identical, up to a hash
+    collision)."""
+    bits = t.detach().contiguous().view(-1).view(torch.int32).to(torch.int64)
+    n = bits.numel()
+    w = (torch.arange(n, device=bits.device, dtype=torch.int64) * 2654435761 + 97) % 1000003 + 1
+    return int((bits * w).sum())
+
+
+def _full_rank_worker(rank, world, port, outdir, P, sg_degree, views, forms, chunks):
+    """One rank of the view-parallel step at full workload (bench.py's N > 1
+    step): its own 1080p orbit view of the shared scene, forward
+    + backward through the HIP rasterizer, then each exchange form on fresh
+    parameters; the float64 sum over the ranks of the plain per-view
+    gradients is the yardstick, formed in float64 by an all-reduce."""
+    import json
+    import math
+    import sys
+    import time
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [root, os.path.join(root, "geometry-grounded-gaussian-splatting_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gsr_scene as S
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gsr_dist import FactoredViewGrads, OverlappedViewGrads, ViewParallelGrads
+
+    t_start = time.time()
+    torch.set_num_threads(max(1, 16 // world))  # (the ranks share the box's 16-core CPU share)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    W, H = 1920, 1080
+    raw = S.make_gaussians(P, sh_degree=3, sg_degree=sg_degree, aspect=H / W)  # bench.py's scene (seed 0)
+    inp = {k: v.detach().contiguous().to(dev) for k, v in S.activated_inputs(raw).items()}
+    del raw
+    cam = S.orbit_cameras(views, W, H)[rank].to(dev)
+    settings = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2),
+        kernel_size=0.0, bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam.world_view_transform,
+        projmatrix=cam.full_proj_transform, sh_degree=3, sg_degree=sg_degree, campos=cam.camera_center,
+        prefiltered=False, require_depth=True, debug=False)
+    g = {k: v.to(dev) for k, v in S.upstream_grads(H, W, seed=11 + rank).items()}
+    keys = ["means3D", "opacities", "scales", "rotations", "shs", "sg_axis", "sg_sharpness", "sg_color"]
+
+    def fresh():
+        return {k: inp[k].clone().requires_grad_(True) for k in keys}
+
+    def step(ps):
+        color, radii, mdepth, alpha, normal = GaussianRasterizer(settings)(
+            means3D=ps["means3D"], means2D=torch.zeros(P, 3, device=dev, requires_grad=True),
+            opacities=ps["opacities"], shs=ps["shs"], sg_axis=ps["sg_axis"], sg_sharpness=ps["sg_sharpness"],
+            sg_color=ps["sg_color"], scales=ps["scales"], rotations=ps["rotations"])
+        torch.autograd.backward([color, mdepth, normal], [g["color"], g["mdepth"], g["normal"]])
+        torch.cuda.synchronize()
+        n_vis = int((radii > 0).sum())
+        return {k: (t.grad if t.grad is not None else torch.zeros_like(t)) for k, t in ps.items()}, n_vis
+
+    plain, n_vis = step(fresh())
+    want = {}
+    for k in keys:  # the yardstick: sum over the views in float64
+        w = plain[k].double()
+        if w.numel():
+            dist.all_reduce(w)
+        want[k] = w
+    del plain
+    res = {"rank": rank, "visible": n_vis, "forms": {}}
+    for form in forms:
+        ps = fresh()
+        if form == "overlap":
+            with OverlappedViewGrads(chunks=chunks):
+                got, _ = step(ps)
+        elif form == "factored":
+            ex = FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"],
+                                   ps["sg_axis"], ps["sg_sharpness"], ps["sg_color"])
+            step(ps)
+            ex.exchange(cam.camera_center, 3, sg_degree)
+            torch.cuda.synchronize()
+            got = {k: t.grad for k, t in ps.items()}
+        else:
+            step(ps)
+            ViewParallelGrads([ps[k] for k in keys]).all_reduce()
+            torch.cuda.synchronize()
+            got = {k: t.grad for k, t in ps.items()}
+        out = {}
+        for k in keys:
+            if want[k].numel() == 0:
+                continue
+            a = got[k]
+            err = float((a.double() - want[k]).norm() / want[k].norm().clamp_min(1e-30))
+            cs = torch.tensor([_checksum(a), -_checksum(a)], dtype=torch.int64)
+            dist.all_reduce(cs, op=dist.ReduceOp.MAX)  # max and -min over the ranks
+            out[k] = {"rel_l2": err, "finite": bool(torch.isfinite(a).all()),
+                      "replicas_identical": int(cs[0]) == -int(cs[1])}
+        res["forms"][form] = out
+        del got, ps
+    res["seconds"] = round(time.time() - t_start, 1)
+    with open(os.path.join(outdir, f"full{rank}.json"), "w") as f:
+        json.dump(res, f)
+    print(f"[rank {rank}] done in {res['seconds']} s", flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_full_ranks(tmp_path, world, P, sg_degree, views, forms, chunks=4):
+    import json
+    import socket
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_full_rank_worker, args=(world, port, str(tmp_path), P, sg_degree, views, forms, chunks),
+                       nprocs=world, join=True, start_method="spawn")
+    rs = [json.load(open(tmp_path / f"full{r}.json")) for r in range(world)]
+    for r in rs:
+        print(f"rank {r['rank']}: {r['visible']} visible Gaussians, {r['seconds']} s, "
+              + ", ".join(f"{f}: max rel L2 {max(v['rel_l2'] for v in d.values()):.2e}" for f, d in r["forms"].items()))
+        assert r["visible"] > 0.3 * P, r["visible"]  # every view sees a large part of the scene
+        for form, d in r["forms"].items():
+            for k, v in d.items():
+                assert v["finite"], (r["rank"], form, k)
+                assert v["replicas_identical"], (r["rank"], form, k)  # bit-identical on every rank
+                assert v["rel_l2"] <= 1e-5, (r["rank"], form, k, v["rel_l2"])
+    return rs
+
+
+@pytest.mark.timeout(600)
+def test_c4_eight_ranks_full_workload(tmp_path):
+    """C4 (BASELINE.json configs[3]) at its workload: 8 ranks — 8 processes
+    sharing cuda:0 over gloo, since RCCL refuses two ranks on one device —
+    each rendering its own 1920x1080 orbit view of the same 1M Gaussians (SH
+    3) forward + backward through the HIP rasterizer.  For the overlapped
+    (inside the backward, 4 Gaussian ranges), factored and all-reduce
+    exchanges: every rank's gradients are bit-identical and within 1e-5
+    relative L2 of the float64 sum over the 8 views of each view's plain
+    gradients (train.py:142-262 sharded per SURVEY §8(e)).  The RCCL/xGMI
+    timing itself is the driver's 8-GPU run."""
+    _run_full_ranks(tmp_path, 8, 1_000_000, 0, 8, ["overlap", "factored", "allreduce"])
+
+
+@pytest.mark.timeout(600)
+def test_c5_two_ranks_full_workload(tmp_path):
+    """C5's multi-GPU leg at its workload, on two ranks sharing cuda:0 (gloo):
+    5M Gaussians with SH 3 + SG 7 at 1920x1080, two orbit views; the
+    overlapped (7 ranges) and factored exchanges against the float64 sum of
+    the two views' plain gradients (bit-identical replicas, rel. L2 <= 1e-5)."""
+    _run_full_ranks(tmp_path, 2, 5_000_000, 7, 8, ["overlap", "factored"], chunks=7)

@@ -53,6 +53,22 @@ def test_masked_mean_empty_mask():
     assert torch.equal(gx, torch.zeros_like(gx))
 
 
+def test_patchmatch_empty_mask_returns_zero(setup):
+    """No pixel passes d_mask (every median depth 0): the reference returns
+    (0, 0) (utils/loss_utils.py:223-224); here both losses are 0, not NaN, and
+    their gradients are zero."""
+    gsr_train, step, view, nearest = setup
+    from gaussian_renderer import render
+    g = step.g
+    pkg = render(view, g, step.pipe, step.bg, step.kernel_size, require_depth=True)
+    pkg = dict(pkg, median_depth=pkg["median_depth"] * 0.0)
+    ncc, geo = gsr_train.patchmatch(g, pkg, view, nearest, None, step.kernel_size, step.pipe)
+    assert float(ncc) == 0.0 and float(geo) == 0.0
+    params = [g._xyz, g._opacity, g._scaling, g._rotation]
+    for ga in _grads(geo + ncc, params):
+        assert ga is None or (torch.isfinite(ga).all() and float(ga.abs().max()) == 0.0)
+
+
 def test_train_step_runs(setup):
     _, step, view, nearest = setup
     losses = [float(step.step(view, nearest)) for _ in range(2)]
