@@ -176,7 +176,19 @@ def parse():
     return a
 
 
-def stage_bytes(P, K, K_live, HW, shm, sgm, geom, K_contrib=None):
+def row_entries(plist, ranges, grid_x):
+    """The tile lists' row entries (one (Gaussian, column span) entry per Gaussian and tile
+    row it has a live tile in), counted from the final lists: the distinct (Gaussian, tile row) pairs."""
+    import numpy as np
+
+    n = ranges[:, 1].astype(np.int64) - ranges[:, 0].astype(np.int64)
+    rows = np.repeat(np.arange(len(ranges), dtype=np.int64) // grid_x, n)
+    live = np.concatenate([plist[a:b] for a, b in ranges.astype(np.int64) if b > a]) if n.sum() else np.zeros(0, np.uint32)
+    key = live.astype(np.int64) * (int(rows.max()) + 1 if len(rows) else 1) + rows
+    return int(np.unique(key).size)
+
+
+def stage_bytes(P, K, K_live, HW, shm, sgm, geom, K_contrib=None, E_rows=None):
     """Algorithmic (compulsory) HBM bytes per launch of each stage, from the
     per-unit figures of SURVEY.md §8(d).  K is the reference's instance count
     (rect tiles); the binning stages produce the K_live instances that survive
@@ -184,7 +196,12 @@ def stage_bytes(P, K, K_live, HW, shm, sgm, geom, K_contrib=None):
     only up to its max contributor (the last position any pixel blended: the
     backward's loop bound, the forward's saturation point), so their gather
     unit count is K_contrib = sum over tiles of max_contrib (None: K_live,
-    the upper bound of SURVEY §8(d)'s formula)."""
+    the upper bound of SURVEY §8(d)'s formula).  tile_lists counts the two
+    counting passes' own traffic: per Gaussian the q-order index
+    (4 B), the 32-B footprint gathered by the rows pass and its 32-B row
+    record written and read back; per row entry (E_rows: Gaussian, column
+    span, 8 B) one write and two reads (tiles count, tiles emit); per live
+    instance the 4-B point-list write."""
     K_r = K_live if K_contrib is None else K_contrib
     Bp = 44 + 12 * shm + 28 * sgm
     G = 64 if geom else 36
@@ -199,7 +216,7 @@ def stage_bytes(P, K, K_live, HW, shm, sgm, geom, K_contrib=None):
         "sort": K_live * 12,
         "tile_ranges": K_live * 2,
         # q-ordered Gaussians (index + splat rect/conic + radius) in, per-tile lists out
-        "tile_lists": P * 40 + K_live * 4,
+        "tile_lists": P * (4 + 32 + 32 + 32) + (E_rows or 0) * 24 + K_live * 4,
         "render_fwd": K_r * (4 + G) + HW * Opx,
         "bwd_clear": P * A,
         "render_bwd": HW * Ipx + K_r * (4 + G),
@@ -567,13 +584,16 @@ def main():
                                     params["sg_axis"], params["sg_sharpness"], params["sg_color"], args.sh_degree,
                                     args.sg_degree, 1.0, cam.world_view_transform, cam.full_proj_transform, tanx,
                                     tany, 0.0, H, W, cam.camera_center, False, geom, False)
-        K_live = int(_C.debug_binning(fo[7], fo[9], fo[0], H, W, with_list=False)[1][:, 1].max())
+        plist_, ranges_ = _C.debug_binning(fo[7], fo[9], fo[0], H, W, with_list=True)
+        K_live = int(ranges_[:, 1].max())
+        E_rows = row_entries(plist_, ranges_, (W + 15) // 16)
+        del plist_, ranges_
         K_contrib = int(_C.debug_max_contrib(fo[9], H, W).astype("int64").sum())
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.steps / elapsed
     shm = (args.sh_degree + 1) ** 2
-    algo = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom, K_contrib)
-    algo_upper = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom)
+    algo = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom, K_contrib, E_rows)
+    algo_upper = stage_bytes(P, K, K_live, W * H, shm, args.sg_degree, geom, None, E_rows)
     per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in stages.items()}
     if not args.all_stage_events:  # the other stages from the untimed table
         per_launch = {k: (per_launch[k] if k == dom else v) for k, v in table_ms.items()}
@@ -613,7 +633,9 @@ def main():
                     "pipe_busy_source": "SQ_ACTIVE_INST_VALU x 4 / SIMD-cycles of the live launch time",
                     "bound_from": "pipe_busy" if pipe_busy is not None else "frac"},
                 "pmc_source": None if pmc_file is None else f"profiles/{pmc_file}",
-                "stage_ms": {k: round(v, 4) for k, v in per_launch.items()}}
+                "stage_ms": {k: round(v, 4) for k, v in per_launch.items()},
+                "stage_algorithmic_bytes": {k: int(v) for k, v in algo.items() if per_launch.get(k, 0.0) > 0.0},
+                "tile_list_row_entries": E_rows}
     total_algo = sum(v for k, v in algo.items() if per_launch.get(k, 0.0) > 0.0)  # the stages this step ran
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -336,17 +336,22 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
             for (int k = 0; k < NP; k++) {
                 dy[k] = splat2(w0.y) - pp[k].pixy;
                 const f2 power = splat_power2(w0, w1, dx, dy[k]);
-                G[k] = f2{__expf(power.x), __expf(power.y)};
-                alpha_raw[k] = f2{fminf(0.99f, w1.y * G[k].x), fminf(0.99f, w1.y * G[k].y)};
-                va[k] = pp[k].ina && !(contributor >= pp[k].last_a || power.x > 0.0f || alpha_raw[k].x < 1.0f / 255.0f);
-                vb[k] = pp[k].inb && !(contributor >= pp[k].last_b || power.y > 0.0f || alpha_raw[k].y < 1.0f / 255.0f);
-                any = any || va[k] || vb[k];
+                // __expf(x) = v_exp_f32(x log2 e) (the forward's rounding), the products packed
+                const f2 pe = power * splat2(1.44269504088896340736f);
+                G[k] = f2{__builtin_amdgcn_exp2f(pe.x), __builtin_amdgcn_exp2f(pe.y)};
+                const f2 og = splat2(w1.y) * G[k];
+                alpha_raw[k] = f2{fminf(0.99f, og.x), fminf(0.99f, og.y)};
+                // (bitwise, not short-circuit: straight-line compares the ballot below reads directly)
+                va[k] = pp[k].ina & (contributor < pp[k].last_a) & !(power.x > 0.0f) & !(alpha_raw[k].x < 1.0f / 255.0f);
+                vb[k] = pp[k].inb & (contributor < pp[k].last_b) & !(power.y > 0.0f) & !(alpha_raw[k].y < 1.0f / 255.0f);
+                any = any | va[k] | vb[k];
             }
             if (__ballot(any) == 0ull) continue;  // wave-uniform skip (warp.any)
 
             const float4 w2 = s_w2[j];
             const float4 w3 = s_w3[j];
-            const float rsig = w2.y;
+            // (wave-uniform: in a scalar register, so the test is a scalar compare)
+            const float rsig = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, w2.y)));
             const float ks = rsig > 0.f ? 0.5f : 0.f;  // 0.25 kappa = 0.5 kh; non-ball splat: no plane terms
             // field sums over the lane's pixels (the conic / plane terms keep
             // their per-lane factors dx out of the sums)
@@ -456,14 +461,13 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
             }
             const float red = wave_transpose_reduce16(f) * post_scale;
             const float abs_red = wave_sum_dpp(fabs_sum);
-            const uint32_t g = s_id[j];
-            // one atomic instruction: lanes 0, 4, .., 60 add the 16 fields of
-            // the record (one 64-B line), lane 1 adds |dmean2D|
+            // (wave-uniform: the record's address in scalar registers, each lane's field an offset)
+            const uint32_t g = __builtin_amdgcn_readfirstlane(s_id[j]);
+            // lanes 0, 4, .., 60 add the 16 fields of the record (one 64-B line, one atomic
+            // instruction), lane 1 adds |dmean2D|
             const bool field_lane = (lane & 3) == 0 && (GEOM || (lane >> 2) < kAccNormal);
-            if (field_lane || lane == 1) {
-                float* dst = field_lane ? a.acc + (size_t)g * kAccFields + (lane >> 2) : a.acc_abs + g;
-                atomicAdd(dst, field_lane ? red : abs_red);
-            }
+            if (field_lane) atomicAdd(a.acc + (size_t)g * kAccFields + (lane >> 2), red);
+            if (lane == 1) atomicAdd(a.acc_abs + g, abs_red);
         }
     }
 }

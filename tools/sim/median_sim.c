@@ -872,3 +872,258 @@ void sim_s4(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint3
     }
     free(buf);
 }
+
+/* ---- round 5: the first guess of the median depth from the composite's crossing contributor ----
+ * Single-splat model: contributors before the crossing one (the last with T_before > 1/2) are taken as
+ * fully passed (factor 1 - a), those after as not reached (factor 1): T(t) = T_b f_k(t), f_k = sqrt(1 - a g)
+ * in front of the peak and (1 - a) / sqrt(1 - a g) behind it, g = exp(-((t - tp) rs)^2 / 2), solved for
+ * T(t) = 1/2 in closed form.  Reports how often ONE walk from the guess passes the kernel's acceptance
+ * (Newton step <= tol max(t, 1), or <= loose max(t, 1) with |step| F <= curv |h'|), against the mean of
+ * the grid neighbours' exact roots (the current phase-2 guess). */
+static float guess_single(float Tb, float a, float tp, float rs) {
+    if (!(rs > 0.f)) return tp;
+    const float s = sqrtf(1.f - a);
+    float g;
+    int behind;
+    if (Tb * s > 0.5f) {  /* root behind the peak */
+        const float q = 2.f * Tb * (1.f - a);
+        if (q >= 1.f) return tp;  /* never crosses */
+        g = (1.f - q * q) / a;
+        behind = 1;
+    } else {
+        g = (1.f - 0.25f / (Tb * Tb)) / a;
+        behind = 0;
+    }
+    if (!(g > 0.f)) return tp;
+    if (g > 1.f) g = 1.f;
+    const float d = sqrtf(-2.f * logf(g)) / rs;
+    return behind ? tp + d : tp - d;
+}
+static int composite_x(const uint32_t* list, int cnt, const float* xy, const float* co, const float* rp, float px,
+                       float py, contrib_t* out, float* Tfin, float* m0, float* Tb_out, int* kx) {
+    float T = 1.f, mi = 0.f, Tb = 1.f;
+    int n = 0, kk = -1;
+    for (int k = 0; k < cnt; k++) {
+        const uint32_t g = list[k];
+        const float dx = xy[2 * g] - px, dy = xy[2 * g + 1] - py;
+        const float* c4 = co + 4 * g;
+        const float power = -0.5f * (c4[0] * dx * dx + c4[2] * dy * dy) - c4[1] * dx * dy;
+        if (power > 0.f) continue;
+        const float alpha = fminf(0.99f, c4[3] * expf(power));
+        if (alpha < 1.f / 255.f) continue;
+        const float tT = T * (1.f - alpha);
+        if (tT < 1e-4f) break;
+        const float* r = rp + 4 * g;
+        const float t = r[0] * dx + r[1] * dy + r[2];
+        if (T > 0.5f) { mi = t; kk = n; Tb = T; }
+        out[n].a = alpha;
+        out[n].tp = t;
+        out[n].rs = r[3];
+        n++;
+        T = tT;
+    }
+    *Tfin = T;
+    *m0 = mi;
+    *Tb_out = Tb;
+    *kx = kk;
+    return n;
+}
+/* exact root by bisection in double over [lo, hi] (T non-increasing) */
+static double root_exact(const contrib_t* c, int n, double lo, double hi) {
+    for (int it = 0; it < 60; it++) {
+        const double mid = 0.5 * (lo + hi);
+        double T = 1.0;
+        for (int i = 0; i < n; i++) {
+            const double d = (mid - c[i].tp) * c[i].rs;
+            const double g = c[i].rs > 0 ? exp(-0.5 * d * d) : 0.0;
+            const double omg = 1.0 - c[i].a * g;
+            T *= (mid > c[i].tp ? 1.0 - c[i].a : omg) / sqrt(omg);
+        }
+        if (T >= 0.5) lo = mid; else hi = mid;
+    }
+    return 0.5 * (lo + hi);
+}
+static int accept_from(const contrib_t* c, int n, float t, float tol, float loose, float curv) {
+    float h, d1, d2;
+    vac_d2(c, n, t, &h, &d1, &d2);
+    const float D = -d1, F = g_lastF, scale = fmaxf(t, 1.f);
+    if (!(D > 0.f)) return 0;
+    const float step = fabsf(h) / D;
+    return step <= tol * scale || (step <= loose * scale && step * F <= curv * D);
+}
+/* out: [0] pixels in range, [1] single-guess accepted after one walk, [2] neighbour-mean accepted,
+ * [3..10] hist of log10(|guess - root| / max(root, 1)) for the single guess (bins <-7, -7..-6, .., >=-1),
+ * [11..18] the same for the neighbour mean, [19] either accepted, [20] single-guess within the window */
+void sim_guess(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+               const uint32_t* plist, const float* xy, const float* co, const float* rp, float tol, float loose,
+               float curv, double* out) {
+    static contrib_t cc[256][4096];
+    static int nn[256], inr[256];
+    static float gs[256];
+    static double rt[256];
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const int tx = tile % gx, ty = tile / gx;
+        const uint32_t b = ranges[2 * tile], e = ranges[2 * tile + 1];
+        for (int p = 0; p < 256; p++) {
+            const int px = tx * 16 + (p & 15), py = ty * 16 + (p >> 4);
+            inr[p] = 0;
+            if (px >= W || py >= H) continue;
+            float Tf, m0, Tb;
+            int kx;
+            nn[p] = composite_x(plist + b, (int)(e - b), xy, co, rp, (float)px, (float)py, cc[p], &Tf, &m0, &Tb, &kx);
+            if (Tf > 0.45f || kx < 0) continue;
+            const double lo = fmax(m0 - RANGE, 0.f), hi = fmax(m0 + RANGE, 0.f);
+            /* in range as the reference decides it (window ends) */
+            if (!(vac(cc[p], nn[p], (float)lo) >= 0.5f && vac(cc[p], nn[p], (float)hi) <= 0.5f)) continue;
+            inr[p] = 1;
+            rt[p] = root_exact(cc[p], nn[p], lo, hi);
+            const contrib_t* k = &cc[p][kx];
+            gs[p] = guess_single(Tb, k->a, k->tp, k->rs);
+        }
+        for (int p = 0; p < 256; p++) {
+            if (!inr[p]) continue;
+            const int lx = p & 15, ly = p >> 4;
+            double sum = 0;
+            int cnt = 0;
+            for (int dy = -1; dy <= 1; dy++)
+                for (int dx = -1; dx <= 1; dx++) {
+                    const int use = ((lx & 1) ? dx != 0 : dx == 0) && ((ly & 1) ? dy != 0 : dy == 0);
+                    const int nx = lx + dx, ny = ly + dy;
+                    if (use && nx >= 0 && nx < 16 && ny >= 0 && ny < 16 && inr[ny * 16 + nx] && !((nx | ny) & 1) &&
+                        !(nx == lx && ny == ly)) {
+                        sum += rt[ny * 16 + nx];
+                        cnt++;
+                    }
+                }
+            const double scale = fmax(rt[p], 1.0);
+            {   /* higher-order guess: tensor-product Lagrange interpolation of the grid roots */
+                double wxv[4], wyv[4];
+                int xs[4], ys[4], nx_ = 0, ny_ = 0;
+                for (int ax = 0; ax < 2; ax++) {
+                    const int l = ax ? ly : lx;
+                    double* wv = ax ? wyv : wxv;
+                    int* cs = ax ? ys : xs;
+                    int* nc = ax ? &ny_ : &nx_;
+                    if (!(l & 1)) { cs[0] = l; wv[0] = 1; *nc = 1; continue; }
+                    if (l >= 3 && l <= 11) { int o[4] = {-3, -1, 1, 3}; double w[4] = {-1/16., 9/16., 9/16., -1/16.};
+                        for (int q = 0; q < 4; q++) { cs[q] = l + o[q]; wv[q] = w[q]; } *nc = 4; }
+                    else if (l == 1) { int o[3] = {-1, 1, 3}; double w[3] = {3/8., 3/4., -1/8.};
+                        for (int q = 0; q < 3; q++) { cs[q] = l + o[q]; wv[q] = w[q]; } *nc = 3; }
+                    else if (l == 13) { int o[3] = {-3, -1, 1}; double w[3] = {-1/8., 3/4., 3/8.};
+                        for (int q = 0; q < 3; q++) { cs[q] = l + o[q]; wv[q] = w[q]; } *nc = 3; }
+                    else { int o[2] = {-3, -1}; double w[2] = {-0.5, 1.5};  /* l = 15: linear extrapolation */
+                        for (int q = 0; q < 2; q++) { cs[q] = l + o[q]; wv[q] = w[q]; } *nc = 2; }
+                }
+                double gsum = 0; int ok = 1;
+                for (int i = 0; i < nx_; i++) for (int j = 0; j < ny_; j++) {
+                    const int q = ys[j] * 16 + xs[i];
+                    if (!inr[q]) ok = 0; else gsum += wxv[i] * wyv[j] * rt[q];
+                }
+                if (ok && !(!(lx & 1) && !(ly & 1))) {
+                    const float gh = (float)gsum;
+                    out[21] += 1;
+                    out[22] += accept_from(cc[p], nn[p], gh, tol, loose, curv);
+                    double e3 = fabs(gh - rt[p]) / scale;
+                    int b3 = e3 <= 0 ? 0 : (int)floor(log10(e3)) + 8;
+                    b3 = b3 < 0 ? 0 : b3 > 7 ? 7 : b3;
+                    out[23 + b3] += 1;
+                }
+            }
+            out[0] += 1;
+            const int a1 = accept_from(cc[p], nn[p], gs[p], tol, loose, curv);
+            out[1] += a1;
+            double e1 = fabs(gs[p] - rt[p]) / scale;
+            int b1 = e1 <= 0 ? 0 : (int)floor(log10(e1)) + 8;
+            b1 = b1 < 0 ? 0 : b1 > 7 ? 7 : b1;
+            out[3 + b1] += 1;
+            out[20] += fabs(gs[p] - rt[p]) < 0.4;
+            if (cnt) {
+                const float gm = (float)(sum / cnt);
+                const int a2 = accept_from(cc[p], nn[p], gm, tol, loose, curv);
+                out[2] += a2;
+                out[19] += a1 || a2;
+                double e2 = fabs(gm - rt[p]) / scale;
+                int b2 = e2 <= 0 ? 0 : (int)floor(log10(e2)) + 8;
+                b2 = b2 < 0 ? 0 : b2 > 7 ? 7 : b2;
+                out[11 + b2] += 1;
+            }
+        }
+    }
+}
+
+/* round 5: blended contributors a median-depth walk must visit when the list is cut after the last one
+ * that is not "far behind" the reference's whole first window (t_peak - K / rsigma > m0 + 0.4 for
+ * contributors after the T = 1/2 crossing, whose factor is then exactly 1 at every depth of the window).
+ * out: [0] in-range pixels, [1] blended contributors, [2] blended up to the cut, [3] blended before the
+ * crossing, [4] far-behind contributors before the cut (still walked) */
+void sim_cut(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges, const uint32_t* plist,
+             const float* xy, const float* co, const float* rp, float K, double* out) {
+    static contrib_t cc[4096];
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const int tx = tile % gx, ty = tile / gx;
+        const uint32_t b = ranges[2 * tile], e = ranges[2 * tile + 1];
+        for (int p = 0; p < 256; p++) {
+            const int px = tx * 16 + (p & 15), py = ty * 16 + (p >> 4);
+            if (px >= W || py >= H) continue;
+            float Tf, m0, Tb;
+            int kx;
+            const int n = composite_x(plist + b, (int)(e - b), xy, co, rp, (float)px, (float)py, cc, &Tf, &m0, &Tb, &kx);
+            if (Tf > 0.45f || kx < 0) continue;
+            int cut = kx, farb = 0;
+            for (int i = kx + 1; i < n; i++) {
+                const int far = cc[i].rs > 0 && cc[i].tp - K / cc[i].rs > m0 + RANGE;
+                if (!far) cut = i;
+            }
+            for (int i = kx + 1; i <= cut; i++) farb += cc[i].rs > 0 && cc[i].tp - K / cc[i].rs > m0 + RANGE;
+            out[0] += 1;
+            out[1] += n;
+            out[2] += cut + 1;
+            out[3] += kx + 1;
+            out[4] += farb;
+        }
+    }
+}
+
+/* round 5: the backward's walked (tile, entry) steps: entries before the tile's max contributor that some
+ * pixel blended (TileState::blend_mask; entries past the first 256 are all walked).
+ * out: [0] tiles, [1] sum max_contrib, [2] walked steps, [3] sum over walked steps of blending pixels */
+void sim_bwd_steps(int W, int H, int gx, int ntiles, const uint32_t* tiles, const uint32_t* ranges,
+                   const uint32_t* plist, const float* xy, const float* co, double* out) {
+    static int cnt[65536];
+    for (int ti = 0; ti < ntiles; ti++) {
+        const uint32_t tile = tiles[ti];
+        const int tx = tile % gx, ty = tile / gx;
+        const uint32_t b = ranges[2 * tile], e = ranges[2 * tile + 1];
+        const int n = (int)(e - b);
+        for (int k = 0; k < n && k < 65536; k++) cnt[k] = 0;
+        int maxc = 0;
+        for (int p = 0; p < 256; p++) {
+            const int px = tx * 16 + (p & 15), py = ty * 16 + (p >> 4);
+            if (px >= W || py >= H) continue;
+            float T = 1.f;
+            int last = 0;
+            for (int k = 0; k < n; k++) {
+                const uint32_t g = plist[b + k];
+                const float dx = xy[2 * g] - px, dy = xy[2 * g + 1] - py;
+                const float* c4 = co + 4 * g;
+                const float power = -0.5f * (c4[0] * dx * dx + c4[2] * dy * dy) - c4[1] * dx * dy;
+                if (power > 0.f) continue;
+                const float alpha = fminf(0.99f, c4[3] * expf(power));
+                if (alpha < 1.f / 255.f) continue;
+                const float tT = T * (1.f - alpha);
+                if (tT < 1e-4f) break;
+                cnt[k]++;
+                T = tT;
+                last = k + 1;
+            }
+            if (last > maxc) maxc = last;
+        }
+        out[0] += 1;
+        out[1] += maxc;
+        for (int k = 0; k < maxc; k++) {
+            if (k >= 256 || cnt[k] > 0) { out[2] += 1; out[3] += cnt[k]; }
+        }
+    }
+}
