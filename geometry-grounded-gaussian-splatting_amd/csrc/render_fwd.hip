@@ -207,6 +207,8 @@ __constant__ constexpr float kProbeOffsets[kProbes] = {0.f,    -0.5f,   -0.25f, 
 #endif
 constexpr uint32_t kPubRefined = 1u, kPubOut = 2u, kPubIll = 4u;  // phase results: root found / not in range /
                                                                    // root found, ill-conditioned (below)
+constexpr uint32_t kPubBracket = 128u;  // left to the passes with an evaluated bracket [lo, hi] of the root
+constexpr uint32_t kLastMask = 0x3fffffffu, kLoEv = 1u << 30, kHiEv = 1u << 31;  // (s_pub_last of a phase-2b pixel)
 #ifndef GSR_REFINE_WALKS
 #define GSR_REFINE_WALKS 4
 #endif
@@ -320,7 +322,8 @@ struct PixSrc {
 // [8 + 2 f], [9 + 2 f]: walk wave-steps and their active lanes of render-path
 // phase f = 0 (1: grid pixels), 1 (2: first walk), 2 (2b: grouped), 3 (3: passes / dT walks);
 // [16] ill-conditioned roots kept (phase 3 computes their dT/dt_m only), [17] lanes phase 3 gives its
-// listed pixels (render path); [18], [19] reserved.
+// listed pixels (render path); [18] reference passes skipped by phase-3 pixels' brackets, [19] pixels that
+// skipped at least one.
 constexpr int kRenderStats = 20;
 __device__ unsigned long long g_render_stats[kRenderStats];
 
@@ -385,6 +388,9 @@ constexpr bool kP1One = GSR_P1_ONE;
 constexpr int kP2bWalks = GSR_P2B_WALKS;
 #ifndef GSR_P3_ILL_SHIFT
 #define GSR_P3_ILL_SHIFT 3  // phase 3: an ill-conditioned root's group is at least G_p >> this (2 and 4: the same within noise, profiles/r4_ab_p3_ill_floor.txt)
+#endif
+#ifndef GSR_PASS_SKIP
+#define GSR_PASS_SKIP 1  // phase 3 skips the reference passes a pixel's evaluated bracket decides
 #endif
 #ifndef GSR_LEFT_STATS
 #define GSR_LEFT_STATS 0  // (development: render stats slots 12..15 count why pixels are left to the passes)
@@ -816,7 +822,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             return G == 1 ? ~0u : G == 2 ? 0x55555555u << q : G == 4 ? 0x11111111u << q
                  : G == 8 ? 0x01010101u << q : 0x00010001u << q;
         };
-        auto pass = [&](auto first_c, auto&& src, int G) {
+        auto pass = [&](auto first_c, auto&& src, int G, bool on) {
             constexpr bool FIRST = decltype(first_c)::value;
             constexpr int START = FIRST ? 0 : 1;
             constexpr int END = FIRST ? kSplit + 1 : kSplit;
@@ -837,12 +843,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             const float T1 = ts[END - 1];
             if (resident) {
                 const PixSrc ps = src();
-                walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, in_range && !refined,
+                walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, in_range && !refined && on,
                      each([&](float alpha, float t_peak, float rs, float sc, float bm) {
                          bisect_step<NP, HAS1>(A, B, TS, A1, B1, T1, alpha, t_peak, rs, sc, bm);
                      }));
             } else {
-                bool bdone = !in_range;
+                bool bdone = !in_range || !on;
                 uint32_t c = 0;
                 for (int ch = 0; ch < chunks; ch++) {
                     __syncthreads();
@@ -864,6 +870,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     }
                 }
             }
+            if (!on) return;  // (a lane whose passes are done keeps its cell; a group shares `on`)
 #pragma unroll
             for (int k = 0; k < NP; k++) {
                 Tp[START + 2 * k] = gprod(A[k].x, G) * __builtin_amdgcn_rsqf(gprod(B[k].x, G));
@@ -897,6 +904,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             bool refined, ill, in_range, live, newton_done;
             float t_ref, ref_t, ref_D, ref_E;
             float t, lo, hi;
+            bool lo_ev, hi_ev;  // lo / hi set by an evaluation of T (not the window's unevaluated ends)
         };
         // One walk's update of a live pixel: log2 T, its derivatives -D, E and the curvature bound F at t
         // (the products and sums of the walk), the bracket, the Halley iterate, and acceptance.
@@ -905,8 +913,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             const float tol = kRefineTol * scale, tol_cond = kCondTol * scale, tol_loose = kLooseTol * scale;
             if constexpr (STATS) st[6] += 1;
             const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
-            if (H >= 0.f) lo = t;
-            else hi = t;
+            if (H >= 0.f) {
+                lo = t;
+                r.lo_ev = true;
+            } else {
+                hi = t;
+                r.hi_ev = true;
+            }
             // Halley step t - 2 H H' / (2 H'^2 - H H''), H' = -D, H'' = E; bisection if it leaves the bracket
             const float th = t + fast_div(2.f * H * D, __builtin_fmaf(2.f * D, D, -H * E));
             const bool halley_in = th >= lo && th <= hi;
@@ -940,8 +953,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             t = tn;
         };
         auto halley = [&](auto&& src, int grouped, bool live, float t, float lo, float hi, bool ends, float e0, float e8, bool in_range0,
-                          int walks, float scale) {
-            Refine r{false, false, in_range0, false, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                          int walks, float scale, bool lo_ev, bool hi_ev) {
+            Refine r{false, false, in_range0, false, false, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, lo_ev, hi_ev};
             const f32x2 TSE[1] = {f32x2{e0, e8}};
             for (int k = 0; k < walks && a.passes > 1; k++) {
                 if (__ballot(live) == 0ull) break;
@@ -1051,7 +1064,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             float wsec = Hlo / (Hlo - Hhi);
             wsec = wsec != wsec ? 0.5f : fminf(fmaxf(wsec, 0.f), 1.f);
             const float t = __builtin_fmaf(wsec, hi - lo, lo);
-            return halley(src, grouped, pin && bracketed, t, lo, hi, false, 0.f, 0.f, pin, walks, fmaxf(t, 1.f));
+            return halley(src, grouped, pin && bracketed, t, lo, hi, false, 0.f, 0.f, pin, walks, fmaxf(t, 1.f), bracketed,
+                          bracketed);
         };
         bool have_out = false;  // (render path) md_out and dT/dt_m published by the pixel's worker
         if (a.refine && resident && a.passes > 0) {
@@ -1088,6 +1102,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         if (r.refined && mb != 0.f)
                             dt = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(r.ref_E, mb - r.ref_t, -r.ref_D);
                     }
+                    if (GSR_PASS_SKIP && r.in_range && !r.refined && !r.ill && r.lo_ev && r.hi_ev) {
+                        flags = kPubBracket;  // (the reference's passes whose cell holds the bracket are skipped)
+                        mo = r.lo;
+                        s_pub_hi[p] = r.hi;
+                    }
                     if (GSR_LEFT_STATS && r.in_range && !r.refined && !r.ill) flags = r.live ? 16u : r.newton_done ? 32u : 64u;
 #ifdef GSR_DBG_DT
                     if ((flags & kPubRefined) && !(dt < -1e-4f))
@@ -1098,7 +1117,140 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     s_pub_T[p] = mo;
                     s_pub_m0[p] = dt;
                 };
-                {  // phase 1
+                // Two-level phase 1 (round 5): the 16 pixels of the 4-spaced grid run the probe walk and a Halley
+                // walk on 16 lanes each (1a); the other 48 even-grid pixels start a Halley walk from the
+                // 4-grid roots interpolated (1b, 4 lanes each) instead of running the probe walk
+                // themselves.  tools/sim/guess_sim.py (C3 contributor sets): 89% of them are accepted after
+                // that one walk, 99.9% within two; the probe walk (7 samples per contributor) they skip
+                // cost about 1.75 Halley walks.  A pixel with no root among its taps starts from its own
+                // m0.  Those not converged continue in phase 2 on their own lane (as the grid pixels do).
+#ifndef GSR_P1_TWO_LEVEL
+#define GSR_P1_TWO_LEVEL 1
+#endif
+#ifndef GSR_INTERP_SPREAD
+#define GSR_INTERP_SPREAD 0.05f
+#endif
+                constexpr float kInterpSpread = GSR_INTERP_SPREAD;
+                // (block-uniform) the two-level scheme needs a smooth root field: every 4-grid pixel in range
+                // (T <= MIN_TRANSMITTANCE) and their composite m0 within kInterpSpread of their mean (m0, the
+                // crossing contributor's depth, is known before phase 1; the roots follow it within ~0.05).
+                // tools/sim/guess_sim.py: C3 tiles under 5e-2 hold 97% of the pixels (82-93% of the 1b pixels
+                // accepted after one walk); the sparse C2 scene's median depth is rough (17% of its tiles, 25%
+                // accepted), and there a tile takes phase 1 as before: its 64 grid pixels probe-walked at once
+                // (a two-level tile that falls back after 1a leaves a wave idle in 1b: C2 0.48 -> 0.505 ms).
+                bool two_level = GSR_P1_TWO_LEVEL;
+                if (two_level) {
+                    float g_min = 3.4e38f, g_max = -3.4e38f, g_sum = 0.f;
+                    bool all_in = true;
+#pragma unroll
+                    for (int i = 0; i < 16; i++) {
+                        const int q = (i >> 2) * 64 + (i & 3) * 4;
+                        const float gm = s_pub_m0[q];
+                        all_in = all_in && s_pub_T[q] <= kMinTransmittance;
+                        g_min = fminf(g_min, gm);
+                        g_max = fmaxf(g_max, gm);
+                        g_sum += gm;
+                    }
+                    two_level = all_in && g_max - g_min <= kInterpSpread * fmaxf(g_sum * (1.f / 16.f), 1.f);
+                }
+                if (two_level) {
+                    {  // phase 1a: (4 (g / 4), 4 (g % 4)), g = lane / 16
+                        auto grid4_pixel = [&](int lane) { return ((lane >> 4) >> 2) * 64 + ((lane >> 4) & 3) * 4; };
+                        const int gp = grid4_pixel(tid), q = tid & 15;
+                        const float gm0 = s_pub_m0[gp], gT = s_pub_T[gp];
+                        auto src = [&] {
+                            const int lane = opaque_int(tid), gq = grid4_pixel(lane);
+                            return PixSrc{s_mask + gq, s_pub_last[gq], (float)(x0 + (gq & 15)), (float)(y0 + (gq >> 4)),
+                                          0x00010001u << (lane & 15)};
+                        };
+                        const Refine r = probe_refine(src, gm0, gT, 16, 1);
+                        if (q == 0) {
+                            const int lane = opaque_int(tid), g4 = grid4_pixel(lane);
+                            const bool cont = r.live;
+                            const int gi = (g4 >> 5) * 8 + ((g4 & 15) >> 1);  // s_groot index (y / 2) 8 + x / 2
+                            s_groot[gi] = (r.in_range && r.refined) ? r.t_ref : cont ? r.t : -1.f;
+                            s_glive[gi] = cont ? 1 : 0;
+                            if (!cont) publish(g4, r);
+                        }
+                    }
+                    __syncthreads();
+                    stamp(3);
+                    {  // phase 1b: the 48 even-grid pixels off the 4-grid, 4 lanes each (waves 0-2)
+                        // k = lane / 4: rows of the half-resolution grid in pairs (2 r, 2 r + 1): 4 pixels (odd
+                        // half-res x) then 8
+                        auto half_xy = [](int k, int& hx, int& hy) {
+                            const int r = k / 12, m = k - 12 * (k / 12);
+                            hx = m < 4 ? 2 * m + 1 : m - 4;
+                            hy = m < 4 ? 2 * r : 2 * r + 1;
+                        };
+                        const int k = tid >> 2;
+                        // (block-uniform) a 4-grid pixel without a root (1a did not find it in range): these 48
+                        // run the probe walk instead
+                        const bool v16 = s_groot[((tid & 15) >> 2) * 16 + (tid & 3) * 2] >= 0.f;
+                        const bool interp_tile = (__ballot(v16) & 0xFFFFull) == 0xFFFFull;
+                        if (k < 48) {
+                            int hx, hy;
+                            half_xy(k, hx, hy);
+                            const int p = (2 * hy) * 16 + 2 * hx;
+                            // the 4-grid roots interpolated on the half-resolution lattice (the phase-2 rules)
+                            auto rule = [](int l, int* o, float* w, int& n) {
+                                if (!(l & 1)) {
+                                    o[0] = l; w[0] = 1.f; n = 1;
+                                } else if (l == 1) {
+                                    o[0] = 0; o[1] = 2; o[2] = 4; w[0] = 0.375f; w[1] = 0.75f; w[2] = -0.125f; n = 3;
+                                } else if (l == 5) {
+                                    o[0] = 2; o[1] = 4; o[2] = 6; w[0] = -0.125f; w[1] = 0.75f; w[2] = 0.375f; n = 3;
+                                } else if (l == 7) {
+                                    o[0] = 4; o[1] = 6; w[0] = -0.5f; w[1] = 1.5f; n = 2;
+                                } else {
+                                    o[0] = 0; o[1] = 2; o[2] = 4; o[3] = 6;
+                                    w[0] = -0.0625f; w[1] = 0.5625f; w[2] = 0.5625f; w[3] = -0.0625f; n = 4;
+                                }
+                            };
+                            int ox[4], oy[4], nx, ny;
+                            float wx[4], wy[4];
+                            rule(hx, ox, wx, nx);
+                            rule(hy, oy, wy, ny);
+                            float acc = 0.f;
+                            bool ok = true;
+#pragma unroll
+                            for (int j = 0; j < 4; j++) {
+                                if (j >= ny) break;
+                                float row = 0.f;
+#pragma unroll
+                                for (int i = 0; i < 4; i++) {
+                                    if (i >= nx) break;
+                                    const float gr = s_groot[oy[j] * 8 + ox[i]];
+                                    ok = ok && gr >= 0.f;
+                                    row = __builtin_fmaf(wx[i], gr, row);
+                                }
+                                acc = __builtin_fmaf(wy[j], row, acc);
+                            }
+                            const float qm0 = s_pub_m0[p], qT = s_pub_T[p];
+                            const bool qin = qT <= kMinTransmittance;
+                            const float lo_w = fmaxf(qm0 - a.sample_range, 0.f), hi_w = fmaxf(qm0 + a.sample_range, 0.f);
+                            const float e0 = lo_w, e8 = __builtin_fmaf((hi_w - lo_w) * (1.f / (float)kSplit), (float)kSplit, lo_w);
+                            const float t0 = fminf(fmaxf(ok ? acc : qm0, e0), e8);
+                            auto src = [&] {
+                                int hx2, hy2;
+                                half_xy(opaque_int(tid) >> 2, hx2, hy2);
+                                const int pp = (2 * hy2) * 16 + 2 * hx2;
+                                return PixSrc{s_mask + pp, s_pub_last[pp], (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
+                                              0x11111111u << (opaque_int(tid) & 3)};
+                            };
+                            const Refine r = interp_tile
+                                                 ? halley(src, 4, qin, t0, e0, e8, false, 0.f, 0.f, qin, 1, fmaxf(t0, 1.f),
+                                                          false, false)
+                                                 : probe_refine(src, qm0, qT, 4, 1);
+                            if ((tid & 3) == 0) {
+                                const bool cont = r.live;
+                                s_groot[hy * 8 + hx] = (r.in_range && r.refined) ? r.t_ref : cont ? r.t : -1.f;
+                                s_glive[hy * 8 + hx] = cont ? 1 : 0;
+                                if (!cont) publish(p, r);
+                            }
+                        }
+                    }
+                } else {  // phase 1
                     // (2 (g / 8), 2 (g % 8)) in the tile, g = lane / 4; recomputed for the publish
                     auto grid_pixel = [&](int lane) { return ((lane >> 2) >> 3) * 32 + ((lane >> 2) & 7) * 2; };
                     const int gp = grid_pixel(tid), q = tid & 3;
@@ -1221,13 +1373,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     const bool interp = GSR_P2_INTERP && !on_grid && guess_interp(lx, ly, ti);
                     const float t0 = cnt ? fminf(fmaxf(interp ? ti : sum / (float)cnt, e0), e8) : e0;
                     auto src = [&] { return PixSrc{s_mask + p, ql, qx, qy, ~0u}; };  // (one walk)
-                    const Refine r = halley(src, 1, qin && cnt > 0, t0, e0, e8, !kP2NoEnds, e0, e8, qin, 1, fmaxf(t0, 1.f));
+                    const Refine r = halley(src, 1, qin && cnt > 0, t0, e0, e8, !kP2NoEnds, e0, e8, qin, 1, fmaxf(t0, 1.f),
+                                            false, false);
                     GSR_DBG(p, "p2: m0 %.7f cnt %d t0 %.7f -> live %d in %d ref %d ill %d t_ref %.7f t %.7f [%.7f %.7f] D %g\n",
                             qm0, cnt, t0, (int)r.live, (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.t, r.lo,
                             r.hi, r.ref_D);
                     live2 = r.live;
-                    if (live2) {  // continued by a lane group below
-                        s_pub_last[p] = ql;
+                    if (live2) {  // continued by a lane group below (which ends of its bracket are evaluated: high bits)
+                        s_pub_last[p] = ql | (r.lo_ev ? kLoEv : 0u) | (r.hi_ev ? kHiEv : 0u);
                         s_pub_T[p] = r.t;
                         s_pub_m0[p] = r.lo;
                         s_pub_hi[p] = r.hi;
@@ -1265,13 +1418,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 for (uint32_t e = (uint32_t)(tid >> lg2b); e < n_live; e += (uint32_t)(kTilePixels >> lg2b)) {
                     const int p = s_list[e];
                     const float t = s_pub_T[p];
+                    const uint32_t sl = s_pub_last[p];
                     auto src = [&] {
                         const int pp = s_list[opaque_int((int)e)];
-                        return PixSrc{s_mask + pp, s_pub_last[pp], (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
+                        return PixSrc{s_mask + pp, s_pub_last[pp] & kLastMask, (float)(x0 + (pp & 15)), (float)(y0 + (pp >> 4)),
                                       gfilter(G2b, opaque_int(tid) & (G2b - 1))};
                     };
                     const Refine r = halley(src, G2b, true, t, s_pub_m0[p], s_pub_hi[p], false, 0.f, 0.f, true,
-                                            kP2bWalks, fmaxf(t, 1.f));
+                                            kP2bWalks, fmaxf(t, 1.f), (sl & kLoEv) != 0u, (sl & kHiEv) != 0u);
                     if ((tid & (G2b - 1)) == 0)
                         GSR_DBG(p, "p2b: from %.7f -> live %d in %d ref %d ill %d t_ref %.7f t %.7f [%.7f %.7f] D %g\n", t,
                                 (int)r.live, (int)r.in_range, (int)r.refined, (int)r.ill, r.t_ref, r.t, r.lo, r.hi, r.ref_D);
@@ -1357,7 +1511,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                                                   : before3 + __popcll(bl3 & lower);
                         s_list[slot] = (uint8_t)me;
                         s_pub_last[me] = last;
-                        s_pub_m0[me] = m_init;  // (an ill root stays in s_pub_T[me])
+                        s_pub_m0[me] = m_init;  // (an ill root stays in s_pub_T[me]; a bracket's lo too, its hi in s_pub_hi)
+                        if (!ill && !(flags & kPubBracket)) s_pub_hi[me] = -1.f;
                     }
                     __syncthreads();
                     const bool own_in = in_range, own_refined = refined;  // (the worker role reuses them)
@@ -1400,9 +1555,48 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                             }
                             dmin = fmaxf(wm0 - a.sample_range, 0.f);
                             dmax = fmaxf(wm0 + a.sample_range, 0.f);
-                            pass(std::true_type{}, wsrc, G3);
+                            const int npass = max(a.passes, kSplitIterations);
+                            // Passes decided by the bracket (round 5): where the pixel's walks left an evaluated
+                            // bracket lo < root < hi (T(lo) >= 1/2 > T(hi)) that lies inside one cell of a pass,
+                            // T being non-increasing that pass picks exactly that cell, so it is not evaluated:
+                            // the first evaluated pass starts in the deepest such cell (all 9 of its samples, as
+                            // the reference's first pass; the same depths bit for bit, so the same values as if
+                            // the skipped passes had run).  A decision within rounding of the bracket's ends is a
+                            // float64 near-tie either way (tests/flip_audit.py).
+                            int skip = 0;
+                            const float bhi = work_pass ? s_pub_hi[pw] : -1.f;
+                            if (GSR_PASS_SKIP && bhi >= 0.f) {
+                                const float blo = s_pub_T[pw];
+                                const float mg = 1e-6f * fmaxf(bhi, 1.f);
 #pragma unroll 1
-                            for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, wsrc, G3);
+                                for (int lv = 0; lv < npass - 1; lv++) {
+                                    const float iv = (dmax - dmin) * (1.f / (float)kSplit);
+                                    int kc = -1;
+#pragma unroll
+                                    for (int c = 0; c < kSplit; c++) {
+                                        const float c0 = __builtin_fmaf(iv, (float)c, dmin);
+                                        const float c1 = __builtin_fmaf(iv, (float)(c + 1), dmin);
+                                        kc = (c0 <= blo - mg && c1 >= bhi + mg) ? c : kc;
+                                    }
+                                    if (kc < 0) break;
+                                    dmax = __builtin_fmaf((float)(kc + 1), iv, dmin);
+                                    dmin = __builtin_fmaf((float)kc, iv, dmin);
+                                    skip++;
+                                }
+                            }
+                            if constexpr (STATS) {
+                                if (work_pass && (tid & (G3 - 1)) == 0) {
+                                    st[18] += (unsigned long long)skip;
+                                    st[19] += skip > 0 ? 1ull : 0ull;
+                                }
+                            }
+                            pass(std::true_type{}, wsrc, G3, true);
+#pragma unroll 1
+                            for (int it = 1; it < npass; it++) {
+                                const bool on = it < npass - skip;
+                                if (__ballot(on) == 0ull) break;
+                                pass(std::false_type{}, wsrc, G3, on);
+                            }
                         }
                         // the median depth and dT/dt_m as the owner path below computes them
                         float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
@@ -1462,16 +1656,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 }
                 dmin = win_lo();
                 dmax = win_hi();
-                pass(std::true_type{}, own_src, 1);
+                pass(std::true_type{}, own_src, 1, true);
 #pragma unroll 1
-                for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, own_src, 1);
+                for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, own_src, 1, true);
             }
         } else {
             dmin = win_lo();
             dmax = win_hi();
-            if (a.passes > 0) pass(std::true_type{}, own_src, 1);
+            if (a.passes > 0) pass(std::true_type{}, own_src, 1, true);
 #pragma unroll 1
-            for (int it = 1; it < a.passes; it++) pass(std::false_type{}, own_src, 1);
+            for (int it = 1; it < a.passes; it++) pass(std::false_type{}, own_src, 1, true);
         }
         if constexpr (STATS) {
             stamp(7);

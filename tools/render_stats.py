@@ -41,3 +41,5 @@ if os.environ.get("GSR_LEFT_STATS"):  # a -DGSR_LEFT_STATS=1 build: why pixels a
     sys.exit(0)
 for f, name in enumerate(("1 grid", "2 first walk", "2b grouped", "3 passes/dT")):
     print(f"phase {name}: walk wave-steps {st[8 + 2 * f]} active lanes/step {st[9 + 2 * f] / max(st[8 + 2 * f], 1):.2f}")
+print("ill-conditioned roots kept", st[16], "phase-3 lanes", st[17], "passes skipped by brackets", st[18],
+      "pixels skipping", st[19])

@@ -959,7 +959,7 @@ void sim_guess(int W, int H, int gx, int ntiles, const uint32_t* tiles, const ui
                float curv, double* out) {
     static contrib_t cc[256][4096];
     static int nn[256], inr[256];
-    static float gs[256];
+    static float gs[256], m0s[256], tfs[256];
     static double rt[256];
     for (int ti = 0; ti < ntiles; ti++) {
         const uint32_t tile = tiles[ti];
@@ -972,6 +972,8 @@ void sim_guess(int W, int H, int gx, int ntiles, const uint32_t* tiles, const ui
             float Tf, m0, Tb;
             int kx;
             nn[p] = composite_x(plist + b, (int)(e - b), xy, co, rp, (float)px, (float)py, cc[p], &Tf, &m0, &Tb, &kx);
+            m0s[p] = m0;
+            tfs[p] = Tf;
             if (Tf > 0.45f || kx < 0) continue;
             const double lo = fmax(m0 - RANGE, 0.f), hi = fmax(m0 + RANGE, 0.f);
             /* in range as the reference decides it (window ends) */
@@ -1028,6 +1030,67 @@ void sim_guess(int W, int H, int gx, int ntiles, const uint32_t* tiles, const ui
                     int b3 = e3 <= 0 ? 0 : (int)floor(log10(e3)) + 8;
                     b3 = b3 < 0 ? 0 : b3 > 7 ? 7 : b3;
                     out[23 + b3] += 1;
+                }
+            }
+            {   /* two-level grid: an even-grid pixel not on the 4-grid, guessed from the 4-grid roots
+                 * (coordinates / 2 on the 4-grid's half-resolution lattice: the same 1-D rules, h = 4) */
+                if (!(lx & 1) && !(ly & 1) && ((lx | ly) & 2)) {
+                    const int hx = lx >> 1, hy = ly >> 1;  /* 0..7, 4-grid at even h */
+                    double wxv[4], wyv[4];
+                    int xs[4], ys[4], nx_ = 0, ny_ = 0;
+                    for (int ax = 0; ax < 2; ax++) {
+                        const int l = ax ? hy : hx;
+                        double* wv = ax ? wyv : wxv;
+                        int* cs = ax ? ys : xs;
+                        int* nc = ax ? &ny_ : &nx_;
+                        if (!(l & 1)) { cs[0] = l; wv[0] = 1; *nc = 1; continue; }
+                        if (l == 3) { int o[4] = {-3, -1, 1, 3}; double w[4] = {-1/16., 9/16., 9/16., -1/16.};
+                            for (int q = 0; q < 4; q++) { cs[q] = l + o[q]; wv[q] = w[q]; } *nc = 4; }
+                        else if (l == 1) { int o[3] = {-1, 1, 3}; double w[3] = {3/8., 3/4., -1/8.};
+                            for (int q = 0; q < 3; q++) { cs[q] = l + o[q]; wv[q] = w[q]; } *nc = 3; }
+                        else if (l == 5) { int o[3] = {-3, -1, 1}; double w[3] = {-1/8., 3/4., 3/8.};
+                            for (int q = 0; q < 3; q++) { cs[q] = l + o[q]; wv[q] = w[q]; } *nc = 3; }
+                        else { int o[2] = {-3, -1}; double w[2] = {-0.5, 1.5};
+                            for (int q = 0; q < 2; q++) { cs[q] = l + o[q]; wv[q] = w[q]; } *nc = 2; }
+                    }
+                    double g4 = 0; int ok4 = 1;
+                    for (int i = 0; i < nx_; i++) for (int j = 0; j < ny_; j++) {
+                        const int q = (2 * ys[j]) * 16 + 2 * xs[i];
+                        if (!inr[q]) ok4 = 0; else g4 += wxv[i] * wyv[j] * rt[q];
+                    }
+                    if (ok4) {
+                        const float gh = (float)g4;
+                        out[31] += 1;
+                        const int acc = accept_from(cc[p], nn[p], gh, tol, loose, curv);
+                        out[32] += acc;
+                        {   /* by the tile's 4-grid root spread (max - min) / max(mean, 1): bins <1e-3, <1e-2, <3e-2, <0.1, >= */
+                            double mn = 1e30, mx = -1e30, sm = 0; int nv = 0;
+                            for (int q4 = 0; q4 < 16; q4++) {
+                                const int qq = (4 * (q4 >> 2)) * 16 + 4 * (q4 & 3);
+                                if (inr[qq]) { mn = fmin(mn, rt[qq]); mx = fmax(mx, rt[qq]); sm += rt[qq]; nv++; }
+                            }
+                            const double sp = nv ? (mx - mn) / fmax(sm / nv, 1.0) : 1.0;
+                            const int sb = nv < 16 ? 5 : sp < 1e-3 ? 0 : sp < 1e-2 ? 1 : sp < 3e-2 ? 2 : sp < 0.1 ? 3 : 4;
+                            out[34 + 2 * sb] += 1;
+                            out[35 + 2 * sb] += acc;
+                            /* the same by the spread of the 4-grid pixels' composite m0 (known before phase 1) */
+                            double mn2 = 1e30, mx2 = -1e30, sm2 = 0; int nv2 = 0;
+                            for (int q4 = 0; q4 < 16; q4++) {
+                                const int qq = (4 * (q4 >> 2)) * 16 + 4 * (q4 & 3);
+                                if (tfs[qq] <= 0.45f) { mn2 = fmin(mn2, m0s[qq]); mx2 = fmax(mx2, m0s[qq]); sm2 += m0s[qq]; nv2++; }
+                            }
+                            const double sp2 = nv2 ? (mx2 - mn2) / fmax(sm2 / nv2, 1.0) : 1.0;
+                            const int sb2 = nv2 < 16 ? 5 : sp2 < 1e-2 ? 0 : sp2 < 2e-2 ? 1 : sp2 < 5e-2 ? 2 : sp2 < 0.1 ? 3 : 4;
+                            out[46 + 2 * sb2] += 1;
+                            out[47 + 2 * sb2] += acc;
+                        }
+                        if (!acc) {  /* a second walk from the Halley iterate */
+                            float h, d1, d2;
+                            vac_d2(cc[p], nn[p], gh, &h, &d1, &d2);
+                            const float tn = gh - 2.f * h * d1 / (2.f * d1 * d1 - h * d2);
+                            out[33] += accept_from(cc[p], nn[p], tn, tol, loose, curv);
+                        }
+                    }
                 }
             }
             out[0] += 1;
