@@ -467,7 +467,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 17; }
+int gsr_abi_version(void) { return 18; }
 
 int gsr_backward_chunk_size(int P, int chunks) {
     if (P < 0 || chunks < 1) return -1;
@@ -1181,6 +1181,80 @@ int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const i
                 image_height_r, image_width_r, image_height_n, image_width_n, ncc, grad_depths, grad_normals, valid};
     hipError_t e = launch_ncc(q, (hipStream_t)stream_ptr);
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "warp_patch_ncc", e);
+}
+
+int gsr_patchmatch_lift(int H, int W, float Fx, float Fy, float Cx, float Cy, const float* T, const float* M,
+                        const float* median_depth, float* points, void* stream_ptr) {
+    if (H < 0 || W < 0 || (H * W > 0 && (!T || !M || !median_depth || !points)))
+        return fail(GSR_ERR_ARGS, "patchmatch lift: invalid arguments");
+    hipError_t e = launch_patchmatch_lift(false, H, W, Fx, Fy, Cx, Cy, T, M, median_depth, nullptr, points,
+                                          (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "patchmatch lift", e);
+}
+
+int gsr_patchmatch_lift_backward(int H, int W, float Fx, float Fy, float Cx, float Cy, const float* M,
+                                 const float* dL_dpoints, float* dL_dmedian_depth, void* stream_ptr) {
+    if (H < 0 || W < 0 || (H * W > 0 && (!M || !dL_dpoints || !dL_dmedian_depth)))
+        return fail(GSR_ERR_ARGS, "patchmatch lift backward: invalid arguments");
+    hipError_t e = launch_patchmatch_lift(true, H, W, Fx, Fy, Cx, Cy, nullptr, M, nullptr, dL_dpoints,
+                                          dL_dmedian_depth, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "patchmatch lift backward", e);
+}
+
+static const char* pm_check(int H, int W, const float* md, const float* normal, const float* pin,
+                            const uint8_t* inside, const float* Mv, const float* tv, const float* R, const float* T,
+                            const float* image_r, const float* image_n, int Hn, int Wn, const float* saved_w,
+                            const uint8_t* saved_flags, const float* saved_gd, const float* saved_gn) {
+    if (H <= 0 || W <= 0 || Hn <= 0 || Wn <= 0) return "patchmatch: invalid sizes";
+    if (!md || !normal || !pin || !inside || !Mv || !tv || !R || !T || !image_r || !image_n || !saved_w ||
+        !saved_flags || !saved_gd || !saved_gn)
+        return "patchmatch: missing buffer";
+    return nullptr;
+}
+
+int gsr_patchmatch_terms_forward(gsr_alloc_fn scratch_alloc, void* scratch_ctx, int H, int W,
+                                 const float* median_depth, const float* normal, const float* points_nearest,
+                                 const uint8_t* inside, const float* Mv, const float* tv, float Fx, float Fy, float Cx,
+                                 float Cy, float noise_th, const float* R, const float* T, const float* image_r,
+                                 const float* image_n, float fx_r, float fy_r, float cx_r, float cy_r, float fx_n,
+                                 float fy_n, float cx_n, float cy_n, int image_height_n, int image_width_n,
+                                 float* saved_w, uint8_t* saved_flags, float* saved_gd, float* saved_gn,
+                                 float* out4, void* stream_ptr) {
+    if (const char* m = pm_check(H, W, median_depth, normal, points_nearest, inside, Mv, tv, R, T, image_r, image_n,
+                                 image_height_n, image_width_n, saved_w, saved_flags, saved_gd, saved_gn))
+        return fail(GSR_ERR_ARGS, m);
+    if (!out4 || !scratch_alloc) return fail(GSR_ERR_ARGS, "patchmatch: missing buffer");
+    void* buf = scratch_alloc(scratch_ctx, patchmatch_partials(H, W) * sizeof(float) + 256);
+    if (!buf) return fail(GSR_ERR_ALLOC, "patchmatch: scratch allocation failed");
+    PatchMatchParams q{H, W, median_depth, normal, points_nearest, inside, Mv, tv, Fx, Fy, Cx, Cy, noise_th, R, T,
+                       image_r, image_n, fx_r, fy_r, cx_r, cy_r, fx_n, fy_n, cx_n, cy_n, image_height_n,
+                       image_width_n, saved_w, saved_flags, saved_gd, saved_gn};
+    hipError_t e = launch_patchmatch_terms(q, reinterpret_cast<float*>(aligned_base(buf)), out4,
+                                           (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "patchmatch terms", e);
+}
+
+int gsr_patchmatch_terms_backward(int H, int W, const float* median_depth, const float* normal,
+                                  const float* points_nearest, const uint8_t* inside, const float* Mv, const float* tv,
+                                  float Fx, float Fy, float Cx, float Cy, float noise_th, const float* R,
+                                  const float* T, const float* image_r, const float* image_n, float fx_r, float fy_r,
+                                  float cx_r, float cy_r, float fx_n, float fy_n, float cx_n, float cy_n,
+                                  int image_height_n, int image_width_n, const float* saved_w,
+                                  const uint8_t* saved_flags, const float* saved_gd, const float* saved_gn,
+                                  const float* out4, const float* dL_dloss2, float* dL_dpoints_nearest,
+                                  float* dL_dmedian_depth, float* dL_dnormal, void* stream_ptr) {
+    if (const char* m = pm_check(H, W, median_depth, normal, points_nearest, inside, Mv, tv, R, T, image_r, image_n,
+                                 image_height_n, image_width_n, saved_w, saved_flags, saved_gd, saved_gn))
+        return fail(GSR_ERR_ARGS, m);
+    if (!out4 || !dL_dloss2 || !dL_dpoints_nearest || !dL_dmedian_depth || !dL_dnormal)
+        return fail(GSR_ERR_ARGS, "patchmatch backward: missing buffer");
+    PatchMatchParams q{H, W, median_depth, normal, points_nearest, inside, Mv, tv, Fx, Fy, Cx, Cy, noise_th, R, T,
+                       image_r, image_n, fx_r, fy_r, cx_r, cy_r, fx_n, fy_n, cx_n, cy_n, image_height_n,
+                       image_width_n, const_cast<float*>(saved_w), const_cast<uint8_t*>(saved_flags),
+                       const_cast<float*>(saved_gd), const_cast<float*>(saved_gn)};
+    hipError_t e = launch_patchmatch_terms_bwd(q, out4, dL_dloss2, dL_dpoints_nearest, dL_dmedian_depth, dL_dnormal,
+                                               (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "patchmatch terms backward", e);
 }
 
 int gsr_fused_ssim_forward(gsr_alloc_fn scratch_alloc, void* scratch_ctx, int NC, int H, int W, int valid,

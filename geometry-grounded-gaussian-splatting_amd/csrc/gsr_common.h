@@ -275,6 +275,28 @@ __device__ inline uint32_t xcd_remap(uint32_t b, uint32_t n) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
+// The tile of a 256-point chunk: the last t in [0, n) with off[t] <= chunk
+// (off non-decreasing, off[0] = 0), searched 64-wide — each lane tests one of
+// 64 evenly spaced candidates and the ballot narrows the span 64-fold — so
+// 8160 tiles take 3 dependent loads, against 13 for a binary search (the
+// chain sat in front of every SAMPLE workgroup's first batch).  Call with
+// every lane of the wave active; the result is wave-uniform.
+__device__ inline uint32_t wave_find_chunk_tile(const uint32_t* __restrict__ off, uint32_t n, uint32_t chunk) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t lo = 0, span = n;
+    while (span > 1) {
+        const uint32_t step = (span + 63u) >> 6;
+        const uint32_t t = lo + lane * step;
+        const bool ok = lane == 0u || (t < lo + span && off[t] <= chunk);
+        const unsigned long long b = __ballot(ok);
+        const uint32_t L = 63u - (uint32_t)__builtin_clzll(b);
+        const uint32_t end = lo + span;
+        lo += L * step;
+        span = min(step, end - lo);
+    }
+    return __builtin_amdgcn_readfirstlane(lo);
+}
+
 // Division as the reference compiles it: CR is built with --use_fast_math
 // (DGR/setup.py), where a / b is the approximate div.approx.f32, i.e.
 // a * rcp(b).  Here: v_rcp_f32 (1 ulp) and one multiply, instead of the

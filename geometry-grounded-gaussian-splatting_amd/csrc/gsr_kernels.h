@@ -176,6 +176,35 @@ struct NccParams {
 };
 hipError_t launch_ncc(const NccParams& q, hipStream_t stream);
 
+// ncc.hip: the fused PatchMatch terms of training (gsr_patchmatch_*)
+struct PatchMatchParams {
+    int H, W;               // the view (reference image of the NCC)
+    const float* md;        // [H*W]
+    const float* normal;    // [3, H*W]
+    const float* pin;       // [H*W, 3]
+    const uint8_t* inside;  // [H*W]
+    const float* Mv;        // [9] row-major
+    const float* tv;        // [3]
+    float Fx, Fy, Cx, Cy;
+    float noise_th;
+    const float* R;  // [9] NCC rotation (the reference's column-major float33), T [3]
+    const float* T;
+    const float* image_r;
+    const float* image_n;
+    float fx_r, fy_r, cx_r, cy_r, fx_n, fy_n, cx_n, cy_n;
+    int Hn, Wn;
+    float* w;
+    uint8_t* flags;
+    float* gd;
+    float* gn;
+};
+size_t patchmatch_partials(int H, int W);
+hipError_t launch_patchmatch_terms(const PatchMatchParams& q, float* partial, float* out, hipStream_t stream);
+hipError_t launch_patchmatch_terms_bwd(const PatchMatchParams& q, const float* out, const float* dL_dloss,
+                                       float* dL_dpin, float* dL_dmd, float* dL_dnormal, hipStream_t stream);
+hipError_t launch_patchmatch_lift(bool backward, int H, int W, float Fx, float Fy, float Cx, float Cy, const float* T,
+                                  const float* M, const float* md, const float* gpts, float* out, hipStream_t stream);
+
 // ssim.hip: fused SSIM forward / backward
 size_t ssim_partials(int NC, int H, int W);
 hipError_t launch_ssim_fwd(int NC, int H, int W, int valid, const float* img1, const float* img2, float* fA,

@@ -47,12 +47,15 @@ __device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y
 constexpr int kNccRadius = 3;          // RADIUS of the reference's <3, true> instance
 constexpr float kNccHalfExtent = 1.5f;  // RADIUS * 0.5 (half-pixel steps)
 
-__global__ void __launch_bounds__(256) ncc_kernel(NccArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
-    const int ux = a.uvs[2 * idx], uy = a.uvs[2 * idx + 1];
-    const float depth = a.depths[idx];
-    const f3 normal = {a.normals[3 * idx], a.normals[3 * idx + 1], a.normals[3 * idx + 2]};
+struct NccPix {
+    bool ok;
+    float ncc, gd;
+    f3 gn;
+};
+
+// One reference pixel (ux, uy) with its depth and (unit) normal: the NCC of
+// its patch against the warp and d(NCC)/d(depth, normal) (forward mode).
+__device__ __forceinline__ NccPix ncc_pixel(const NccArgs& a, int ux, int uy, float depth, f3 normal) {
     const f3 pnr = {(ux - a.cx_r) / a.fx_r, (uy - a.cy_r) / a.fy_r, 1.f};
     const float distance = -dot3(pnr, normal) * depth;
     float out_ncc = 0.f, out_gd = 0.f;
@@ -144,12 +147,21 @@ __global__ void __launch_bounds__(256) ncc_kernel(NccArgs a) {
         out_ncc = ncc;
         ok = ok && var_r > 5e-6f && var_n > 5e-6f;
     }
-    a.ncc[idx] = ok ? out_ncc : 0.f;
-    a.grad_depths[idx] = ok ? out_gd : 0.f;
-    a.grad_normals[3 * idx] = ok ? out_gn.x : 0.f;
-    a.grad_normals[3 * idx + 1] = ok ? out_gn.y : 0.f;
-    a.grad_normals[3 * idx + 2] = ok ? out_gn.z : 0.f;
-    a.valid[idx] = ok ? 1 : 0;
+    return NccPix{ok, out_ncc, out_gd, out_gn};
+}
+
+__global__ void __launch_bounds__(256) ncc_kernel(NccArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    const int ux = a.uvs[2 * idx], uy = a.uvs[2 * idx + 1];
+    const NccPix r = ncc_pixel(a, ux, uy, a.depths[idx],
+                               f3{a.normals[3 * idx], a.normals[3 * idx + 1], a.normals[3 * idx + 2]});
+    a.ncc[idx] = r.ok ? r.ncc : 0.f;
+    a.grad_depths[idx] = r.ok ? r.gd : 0.f;
+    a.grad_normals[3 * idx] = r.ok ? r.gn.x : 0.f;
+    a.grad_normals[3 * idx + 1] = r.ok ? r.gn.y : 0.f;
+    a.grad_normals[3 * idx + 2] = r.ok ? r.gn.z : 0.f;
+    a.valid[idx] = r.ok ? 1 : 0;
 }
 
 hipError_t launch_ncc(const NccParams& q, hipStream_t stream) {
@@ -180,6 +192,298 @@ hipError_t launch_ncc(const NccParams& q, hipStream_t stream) {
     a.grad_normals = q.grad_normals;
     a.valid = q.valid;
     hipLaunchKernelGGL(ncc_kernel, dim3((q.P + 255) / 256), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ PatchMatch
+// The multi-view loss around sample_depth (PatchMatch.__call__,
+// utils/loss_utils.py:140-267) as three kernels, for the training step
+// (gsr_train.PatchMatchFused): no boolean gather, no host synchronisation
+// (the reference's argwhere of the valid pixels), no chain of broadcast
+// elementwise ops and their autograd mirror images.
+//  * lift: the view's median-depth points in world space (:147-153),
+//  * terms: per pixel the reprojection of the point sample_depth returned
+//    from the nearest view (:160-170), the geometric mask and weight
+//    (:206-221), and at the masked pixels the NCC of the normalised rendered
+//    normal's homography warp (ncc_pixel, :239-256 with warp_patch_ncc), with
+//    per-block sums of both masked means (:222-226, :258-262);
+//  * finish: the two losses from the block sums in a fixed order.
+// Their backwards: d(loss)/d(point in the nearest view, median depth,
+// rendered normal), the two masked means' gradients through the same chain.
+constexpr uint8_t kPmGeo = 1u, kPmNcc = 2u, kPmNccGrad = 4u;  // d_mask, ncc_mask, clamp passes the gradient
+
+struct PmArgs {
+    int H, W;
+    const float* md;        // [H*W] median depth of the view
+    const float* normal;    // [3, H*W] rendered normal (not normalised)
+    const float* pin;       // [H*W, 3] sampled points in the nearest camera
+    const uint8_t* inside;  // [H*W]
+    const float* Mv;        // [3][3] row-major: point in view = tv + pin @ Mv
+    const float* tv;        // [3]
+    float Fx, Fy, Cx, Cy;   // view intrinsics (the reprojection)
+    float noise_th;         // multi-view pixel noise threshold
+    NccArgs nc;             // the NCC's poses, images and intrinsics
+    float* w;               // [H*W] geometric weight exp(-noise) on d_mask, else 0
+    uint8_t* flags;         // [H*W] kPm*
+    float* gd;              // [H*W] d(NCC)/d(depth) at ncc_mask pixels
+    float* gn;              // [H*W, 3] d(NCC)/d(unit normal)
+    float* partial;         // [blocks][4] sums: w * noise, d_mask, ncc * w, ncc_mask
+};
+
+struct PmReproj {
+    f3 piv;
+    float z, dx, dy, noise;
+};
+
+// pts_in_view = tv + pin @ Mv, proj = (Cx, Cy) + (Fx, Fy) * xy / max(z, 1e-7),
+// noise = |proj - pixel + 1e-6| (torch.pairwise_distance, eps 1e-6)
+__device__ __forceinline__ PmReproj pm_reproject(const PmArgs& a, f3 pin, int x, int y) {
+#pragma clang fp contract(off)  // (one rounding per torch op of the reference's formulation)
+    PmReproj r;
+    float v[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) v[j] = a.tv[j] + ((pin.x * a.Mv[j] + pin.y * a.Mv[3 + j]) + pin.z * a.Mv[6 + j]);
+    r.piv = f3{v[0], v[1], v[2]};
+    r.z = fmaxf(v[2], 1e-7f);
+    const float px = a.Cx + a.Fx * (v[0] / r.z), py = a.Cy + a.Fy * (v[1] / r.z);
+    r.dx = px - (float)x + 1e-6f;
+    r.dy = py - (float)y + 1e-6f;
+    r.noise = sqrtf(r.dx * r.dx + r.dy * r.dy);
+    return r;
+}
+
+__device__ __forceinline__ f3 pm_normal(const PmArgs& a, int p, int n, float& len) {
+#pragma clang fp contract(off)
+    const f3 q = {a.normal[p], a.normal[n + p], a.normal[2 * n + p]};
+    len = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
+    const float m = fmaxf(len, 1e-12f);  // F.normalize (eps 1e-12)
+    return f3{q.x / m, q.y / m, q.z / m};
+}
+
+// four per-lane sums -> one row of the block's partials (fixed order)
+__device__ __forceinline__ void pm_block_sums(float (&v)[4], float* out) {
+    __shared__ float s[4][4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = wave_sum_f(v[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) s[wave][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) out[threadIdx.x] = (s[0][threadIdx.x] + s[1][threadIdx.x]) + (s[2][threadIdx.x] + s[3][threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) pm_terms_kernel(PmArgs a) {
+    const int n = a.H * a.W;
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    float sums[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p < n) {
+        const int y = p / a.W, x = p - y * a.W;
+        const f3 pin = {a.pin[3 * p], a.pin[3 * p + 1], a.pin[3 * p + 2]};
+        const PmReproj r = pm_reproject(a, pin, x, y);
+        const float depth = a.md[p];
+        const bool dm = a.inside[p] != 0 && pin.z > 0.2f && r.piv.z > 0.2f && r.noise < a.noise_th && depth > 0.f;
+        const float w = dm ? expf(-r.noise) : 0.f;
+        uint8_t fl = dm ? kPmGeo : 0u;
+        float gd = 0.f;
+        f3 gn = {0.f, 0.f, 0.f};
+        if (dm) {
+            sums[0] = w * r.noise;
+            sums[1] = 1.f;
+            float len;
+            const NccPix c = ncc_pixel(a.nc, x, y, depth, pm_normal(a, p, n, len));
+            const float one_m = 1.f - (c.ok ? c.ncc : 0.f);
+            const float ncc = fminf(fmaxf(one_m, 0.f), 2.f);  // torch.clamp(1 - cc, 0, 2)
+            if (c.ok && ncc < 0.9f) {
+                fl |= kPmNcc | ((one_m >= 0.f && one_m <= 2.f) ? kPmNccGrad : 0u);
+                sums[2] = ncc * w;
+                sums[3] = 1.f;
+                gd = c.gd;
+                gn = c.gn;
+            }
+        }
+        a.w[p] = w;
+        a.flags[p] = fl;
+        a.gd[p] = gd;
+        a.gn[3 * p] = gn.x;
+        a.gn[3 * p + 1] = gn.y;
+        a.gn[3 * p + 2] = gn.z;
+    }
+    pm_block_sums(sums, a.partial + 4 * blockIdx.x);
+}
+
+// out = {geo_loss, ncc_loss, d_mask count, ncc_mask count}; an empty mask gives 0 (loss_utils.py:223-224)
+__global__ void __launch_bounds__(1024) pm_finish_kernel(const float* __restrict__ partial, int nb,
+                                                         float* __restrict__ out) {
+    __shared__ float s[16][4];
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = threadIdx.x; b < nb; b += 1024) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] += partial[4 * b + k];
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = wave_sum_f(v[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) s[wave][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int w = 0; w < 16; w++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) t[k] += s[w][k];
+        out[0] = t[1] > 0.f ? t[0] / t[1] : 0.f;
+        out[1] = t[3] > 0.f ? t[2] / t[3] : 0.f;
+        out[2] = t[1];
+        out[3] = t[3];
+    }
+}
+
+// dL/d(pin, md, normal) for dL/d(geo_loss, ncc_loss) = g[0], g[1] (device scalars)
+__global__ void __launch_bounds__(256) pm_terms_bwd_kernel(PmArgs a, const float* __restrict__ out,
+                                                           const float* __restrict__ g, float* __restrict__ dpin,
+                                                           float* __restrict__ dmd, float* __restrict__ dnormal) {
+    const int n = a.H * a.W;
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    const float cg = out[2] > 0.f ? g[0] / out[2] : 0.f;
+    const float cn = out[3] > 0.f ? g[1] / out[3] : 0.f;
+    const uint8_t fl = a.flags[p];
+    f3 gp = {0.f, 0.f, 0.f}, gnrm = {0.f, 0.f, 0.f};
+    float gmd = 0.f;
+    if (fl & kPmGeo) {
+        const int y = p / a.W, x = p - y * a.W;
+        const f3 pin = {a.pin[3 * p], a.pin[3 * p + 1], a.pin[3 * p + 2]};
+        const PmReproj r = pm_reproject(a, pin, x, y);
+        const float gnoise = cg * a.w[p];  // d(masked mean of w * noise)/d noise, w under no_grad
+        const float s = r.noise > 0.f ? gnoise / r.noise : 0.f;
+        const float gx = s * r.dx * a.Fx, gy = s * r.dy * a.Fy;  // d/d(xy / z) of the projection
+        const float iz = 1.f / r.z;
+        const float gz = r.piv.z >= 1e-7f ? -(gx * r.piv.x + gy * r.piv.y) * iz * iz : 0.f;
+        const float gv[3] = {gx * iz, gy * iz, gz};
+        gp.x = (gv[0] * a.Mv[0] + gv[1] * a.Mv[1]) + gv[2] * a.Mv[2];
+        gp.y = (gv[0] * a.Mv[3] + gv[1] * a.Mv[4]) + gv[2] * a.Mv[5];
+        gp.z = (gv[0] * a.Mv[6] + gv[1] * a.Mv[7]) + gv[2] * a.Mv[8];
+        if (fl & kPmNccGrad) {
+            const float gcc = -cn * a.w[p];  // ncc = clamp(1 - cc): d/dcc = -1
+            gmd = gcc * a.gd[p];
+            const f3 gu = f3{a.gn[3 * p], a.gn[3 * p + 1], a.gn[3 * p + 2]} * gcc;
+            float len;
+            const f3 u = pm_normal(a, p, n, len);
+            // F.normalize backward: (g - u (u . g)) / |n| (|n| clamped to eps: g / eps)
+            gnrm = len > 1e-12f ? (gu - u * dot3(u, gu)) * (1.f / len) : gu * 1e12f;
+        }
+    }
+    dpin[3 * p] = gp.x;
+    dpin[3 * p + 1] = gp.y;
+    dpin[3 * p + 2] = gp.z;
+    dmd[p] = gmd;
+    dnormal[p] = gnrm.x;
+    dnormal[n + p] = gnrm.y;
+    dnormal[2 * n + p] = gnrm.z;
+}
+
+// the median-depth points in world space (loss_utils.py:147-153):
+// ((md * ray - T) @ M), ray = ((x - Cx) / Fx, (y - Cy) / Fy, 1); backward: dL/dmd
+__global__ void __launch_bounds__(256) pm_lift_kernel(bool backward, int H, int W, float Fx, float Fy, float Cx,
+                                                      float Cy, const float* __restrict__ T,
+                                                      const float* __restrict__ M, const float* __restrict__ md,
+                                                      const float* __restrict__ gpts, float* __restrict__ out) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= H * W) return;
+    const int y = p / W, x = p - y * W;
+    const float ray[3] = {((float)x - Cx) / Fx, ((float)y - Cy) / Fy, 1.f};
+    if (!backward) {
+        const float d = md[p];
+        const float v[3] = {d * ray[0] - T[0], d * ray[1] - T[1], d * ray[2] - T[2]};
+#pragma unroll
+        for (int j = 0; j < 3; j++) out[3 * p + j] = (v[0] * M[j] + v[1] * M[3 + j]) + v[2] * M[6 + j];
+    } else {
+        const float g[3] = {gpts[3 * p], gpts[3 * p + 1], gpts[3 * p + 2]};
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; k++) acc += ((g[0] * M[3 * k] + g[1] * M[3 * k + 1]) + g[2] * M[3 * k + 2]) * ray[k];
+        out[p] = acc;
+    }
+}
+
+static NccArgs pm_ncc_args(const PatchMatchParams& q) {
+    NccArgs a{};
+    a.R = q.R;
+    a.T = q.T;
+    a.image_r = q.image_r;
+    a.image_n = q.image_n;
+    a.fx_r = q.fx_r;
+    a.fy_r = q.fy_r;
+    a.cx_r = q.cx_r;
+    a.cy_r = q.cy_r;
+    a.fx_n = q.fx_n;
+    a.fy_n = q.fy_n;
+    a.cx_n = q.cx_n;
+    a.cy_n = q.cy_n;
+    a.Hr = q.H;
+    a.Wr = q.W;
+    a.Hn = q.Hn;
+    a.Wn = q.Wn;
+    return a;
+}
+
+static PmArgs pm_args(const PatchMatchParams& q) {
+    PmArgs a{};
+    a.H = q.H;
+    a.W = q.W;
+    a.md = q.md;
+    a.normal = q.normal;
+    a.pin = q.pin;
+    a.inside = q.inside;
+    a.Mv = q.Mv;
+    a.tv = q.tv;
+    a.Fx = q.Fx;
+    a.Fy = q.Fy;
+    a.Cx = q.Cx;
+    a.Cy = q.Cy;
+    a.noise_th = q.noise_th;
+    a.nc = pm_ncc_args(q);
+    a.w = q.w;
+    a.flags = q.flags;
+    a.gd = q.gd;
+    a.gn = q.gn;
+    return a;
+}
+
+size_t patchmatch_partials(int H, int W) { return (size_t)4 * (((size_t)H * W + 255) / 256); }
+
+hipError_t launch_patchmatch_terms(const PatchMatchParams& q, float* partial, float* out, hipStream_t stream) {
+    const int n = q.H * q.W;
+    const int nb = (n + 255) / 256;
+    if (n <= 0) return hipErrorInvalidValue;
+    PmArgs a = pm_args(q);
+    a.partial = partial;
+    hipLaunchKernelGGL(pm_terms_kernel, dim3(nb), dim3(256), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(pm_finish_kernel, dim3(1), dim3(1024), 0, stream, (const float*)partial, nb, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_patchmatch_terms_bwd(const PatchMatchParams& q, const float* out, const float* dL_dloss,
+                                       float* dL_dpin, float* dL_dmd, float* dL_dnormal, hipStream_t stream) {
+    const int n = q.H * q.W;
+    if (n <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pm_terms_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, pm_args(q), out, dL_dloss,
+                       dL_dpin, dL_dmd, dL_dnormal);
+    return hipGetLastError();
+}
+
+hipError_t launch_patchmatch_lift(bool backward, int H, int W, float Fx, float Fy, float Cx, float Cy, const float* T,
+                                  const float* M, const float* md, const float* gpts, float* out, hipStream_t stream) {
+    const int n = H * W;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pm_lift_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, backward, H, W, Fx, Fy, Cx, Cy, T,
+                       M, md, gpts, out);
     return hipGetLastError();
 }
 

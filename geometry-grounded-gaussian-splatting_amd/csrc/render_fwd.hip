@@ -213,6 +213,14 @@ constexpr uint32_t kLastMask = 0x3fffffffu, kLoEv = 1u << 30, kHiEv = 1u << 31; 
 #define GSR_REFINE_WALKS 4
 #endif
 constexpr int kRefineWalks = GSR_REFINE_WALKS;
+// SAMPLE mode: Halley walks from the query point's own distance (GSR_SAMPLE_GUESS, in the kernel)
+#ifndef GSR_SAMPLE_GUESS
+#define GSR_SAMPLE_GUESS 1
+#endif
+#ifndef GSR_SAMPLE_WALKS
+#define GSR_SAMPLE_WALKS 5
+#endif
+constexpr int kSampleWalks = GSR_SAMPLE_WALKS;
 #ifndef GSR_REFINE_TOL
 #define GSR_REFINE_TOL 3e-5f
 #endif
@@ -428,7 +436,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
 #ifndef GSR_PHASE_CLOCK
 #define GSR_PHASE_CLOCK 0
 #endif
-    constexpr bool kClock = GSR_PHASE_CLOCK && STATS && !SAMPLE;
+    constexpr bool kClock = GSR_PHASE_CLOCK && STATS;
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     auto stamp = [&](int k) {
         if constexpr (kClock) ph[k] = clock64();
@@ -441,13 +449,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     if constexpr (SAMPLE) {
         // chunks of one tile are consecutive: XCD-contiguous runs of chunks share Gaussian lists
         chunk = xcd_remap(blockIdx.x, a.num_chunks);
-        uint32_t lo = 0, hi = a.num_tiles;  // last tile with chunk_off[t] <= chunk
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.chunk_off[mid] <= chunk) lo = mid;
-            else hi = mid;
-        }
-        tile = lo;
+        tile = wave_find_chunk_tile(a.chunk_off, a.num_tiles, chunk);
         const uint2 pr = a.pt_ranges[tile];
         const uint32_t slot = pr.x + (chunk - a.chunk_off[tile]) * kTilePixels + tid;
         inside = slot < pr.y;
@@ -455,7 +457,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         const float2 xy = inside ? a.pt_xy[pid] : make_float2(0.f, 0.f);
         pixx = xy.x;
         pixy = xy.y;
-        if constexpr (!GEOM) pt_t = inside ? a.pt_t[pid] : 0.f;
+        pt_t = inside ? a.pt_t[pid] : 0.f;  // (GEOM: the refinement's start, GSR_SAMPLE_GUESS)
     } else {
         tile = a.tile_order ? a.tile_order[blockIdx.x] : xcd_remap(blockIdx.x, a.num_tiles);
         const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
@@ -467,6 +469,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     }
 
     const uint2 range = a.ranges[tile];
+    unsigned long long t_pro = 0, n_rounds = 0, n_idle = 0;  // (phase-clock builds, SAMPLE) prologue end, batches
+#if GSR_SAMPLE_PROLOGUE_ONLY  // (timing build: the SAMPLE raster's prologue alone; its outputs are wrong)
+    if constexpr (SAMPLE) {
+        if (inside && pixx == -1234.f && range.y == 7u) a.out_inside[pid] = 7;
+        if (tid == 0) a.chunk_max[chunk] = 0u;
+        return;
+    }
+#endif
+    if constexpr (kClock && SAMPLE) t_pro = clock64() + (unsigned long long)(range.x & 0u);
     const int total = (int)(range.y - range.x);
     const int rounds = (total + kBatch - 1) / kBatch;
 
@@ -564,6 +575,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         if ((tid & 63) == 0) s_alive[i & 1][wave] = wave_alive;
         __syncthreads();  // also: everyone finished reading the previous batch
         if (!(s_alive[i & 1][0] | s_alive[i & 1][1] | s_alive[i & 1][2] | s_alive[i & 1][3])) break;
+        if constexpr (kClock && SAMPLE) {
+            n_rounds++;
+            n_idle += wave_alive ? 0ull : 1ull;
+        }
         const int k = i * kBatch + tid;
         if (tid < kBatch && k < total) {
             const Splat* sp = a.splats + a.point_list[range.x + k];
@@ -662,7 +677,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
 #ifndef GSR_TIME_COMPOSITE_ONLY
 #define GSR_TIME_COMPOSITE_ONLY 0  // (timing builds only: skip the median depth, its outputs are then wrong)
 #endif
-    if constexpr (GEOM && !(GSR_TIME_COMPOSITE_ONLY && !SAMPLE)) {
+#ifndef GSR_TIME_SAMPLE_COMPOSITE_ONLY
+#define GSR_TIME_SAMPLE_COMPOSITE_ONLY 0  // (timing builds only: the SAMPLE raster without its median depth)
+#endif
+    if constexpr (GEOM && !(GSR_TIME_COMPOSITE_ONLY && !SAMPLE) && !(GSR_TIME_SAMPLE_COMPOSITE_ONLY && SAMPLE)) {
         unsigned long long st[kRenderStats] = {0, 0, cst[0], cst[1]};
         int st_phase = 0;  // (STATS) render-path phase of the walks below
         float Tp[kSplit + 1];
@@ -1638,7 +1656,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                         in_range = s_pub_last[me] != 0u;
                     }
                 }
+            } else if (GSR_SAMPLE_GUESS) {
+                stamp(2);
+                // SAMPLE (round 5): the query point lies on the other view's median-depth surface, so where
+                // that surface is seen from this view the root is near the point's own distance |p_view|
+                // (pt_t).  The Halley walks start there — the first one also samples the window ends for
+                // the reference's in_range test, as phase 2 of the render path — instead of behind a
+                // 7-probe walk; the bisection fallback of root_update keeps an occluded point's far-off
+                // start inside the window's bracket.
+                const bool pin = T <= kMinTransmittance;
+                const float lo_w = win_lo(), hi_w = win_hi();
+                const float e0 = lo_w, e8 = __builtin_fmaf((hi_w - lo_w) * (1.f / (float)kSplit), (float)kSplit, lo_w);
+                const float t0 = fminf(fmaxf(pt_t, e0), e8);
+                const Refine r = halley(own_src, 1, pin, t0, e0, e8, true, e0, e8, pin, kSampleWalks, fmaxf(t0, 1.f),
+                                        false, false);
+                in_range = r.in_range;
+                refined = r.refined;
+                t_ref = r.t_ref;
+                ref_t = r.ref_t;
+                ref_D = r.ref_D;
+                ref_E = r.ref_E;
+                stamp(4);
             } else {
+                stamp(2);
                 const Refine r = probe_refine(own_src, m_init, T, 1, kRefineWalks);
                 in_range = r.in_range;
                 refined = r.refined;
@@ -1646,6 +1686,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 ref_t = r.ref_t;
                 ref_D = r.ref_D;
                 ref_E = r.ref_E;
+                stamp(4);
             }
             // lanes left: the reference's passes from its first window (render path: phase 3 above)
             const bool left = SAMPLE && in_range && !refined;
@@ -1660,6 +1701,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
 #pragma unroll 1
                 for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, own_src, 1, true);
             }
+            if constexpr (SAMPLE) stamp(5);
         } else {
             dmin = win_lo();
             dmax = win_hi();
@@ -1671,7 +1713,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             stamp(7);
             if constexpr (kClock) {
 #pragma unroll
+                for (int k = 1; k < 8; k++) ph[k] = ph[k] ? ph[k] : ph[k - 1];  // (SAMPLE: stamps 3, 6 unset)
+#pragma unroll
                 for (int k = 0; k < 7; k++) st[8 + k] = (tid & 63) == 0 ? ph[k + 1] - ph[k] : 0ull;
+                if constexpr (SAMPLE) {  // prologue clocks, batches, batches with the wave's lanes all done
+                    st[16] = (tid & 63) == 0 ? t_pro - ph[0] : 0ull;
+                    st[17] = (tid & 63) == 0 ? n_rounds : 0ull;
+                    st[18] = (tid & 63) == 0 ? n_idle : 0ull;
+                }
                 st[15] = (tid & 63) == 0 ? ph[7] - ph[0] : 0ull;
             }
             for (int q = 0; q < kRenderStats; q++)
@@ -1853,6 +1902,9 @@ hipError_t launch_point_fwd(int query, const FwdParams& p, const GeomState& gs, 
     if (num_chunks == 0) return hipSuccess;
     if (query == kQueryIntegrate)
         hipLaunchKernelGGL((render_fwd_kernel<false, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,
+                           stream, a);
+    else if (option(kOptRenderStats))
+        hipLaunchKernelGGL((render_fwd_kernel<true, true, true>), dim3(num_chunks), dim3(kTilePixels), 0,
                            stream, a);
     else
         hipLaunchKernelGGL((render_fwd_kernel<true, false, true>), dim3(num_chunks), dim3(kTilePixels), 0,

@@ -219,13 +219,7 @@ __global__ void __launch_bounds__(256) sample_bwd_kernel(SampleBwdArgs a) {
     if (blockIdx.x >= a.totals[2]) return;  // uniform over the block
     const uint32_t chunk = a.chunk_order ? a.chunk_order[blockIdx.x] : xcd_remap(blockIdx.x, a.totals[2]);
     const int tid = threadIdx.x, lane = tid & 63;
-    uint32_t lo = 0, hi = a.num_tiles;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.chunk_off[mid] <= chunk) lo = mid;
-        else hi = mid;
-    }
-    const uint32_t tile = lo;
+    const uint32_t tile = wave_find_chunk_tile(a.chunk_off, a.num_tiles, chunk);
     const uint2 range = a.ranges[tile];
     const int max_contrib = (int)a.chunk_max[chunk];
     const uint2 pr = a.pt_ranges[tile];

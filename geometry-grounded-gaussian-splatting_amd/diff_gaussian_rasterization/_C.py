@@ -44,7 +44,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 
 def _load():

@@ -35,6 +35,7 @@ from fused_ssim import fused_ssim
 from gaussian_renderer import render, sample_depth
 from gsr_geometry import depth_to_normal
 from gsr_optim import FusedAdam, add_densification_stats
+from gsr_patchmatch import patchmatch_fused
 import warp_patch_ncc
 
 
@@ -250,7 +251,7 @@ def masked_mean(x: torch.Tensor, mask: torch.Tensor, empty: float | None = None)
     return mean if empty is None else torch.where(cnt > 0, mean, torch.full_like(mean, empty))
 
 
-def patchmatch(gaussians, render_pkg, view, nearest, depth_normal, kernel_size, pipe):
+def patchmatch(gaussians, render_pkg, view, nearest, kernel_size, pipe):
     """PatchMatch.__call__ (utils/loss_utils.py:140-267): (ncc_loss, geo_loss).
     The reference's means over boolean gathers ((weights * pixel_noise)[d_mask],
     (ncc * weights)[ncc_mask]) are taken as masked sums (`masked_mean`), so the
@@ -270,8 +271,11 @@ class TrainStep:
 
     COMPONENTS = ("render", "depth_normal", "patchmatch", "rgb_loss", "backward", "densify_stats", "adam")
 
-    def __init__(self, gaussians: TrainGaussians, kernel_size: float = 0.0, bg=None, densify: bool = True):
+    def __init__(self, gaussians: TrainGaussians, kernel_size: float = 0.0, bg=None, densify: bool = True,
+                 fused_patchmatch: bool = True):
         self.g = gaussians
+        # PatchMatch on the fused kernels (gsr_patchmatch), or the reference's torch formulation (patchmatch)
+        self.patchmatch = patchmatch_fused if fused_patchmatch else patchmatch
         self.kernel_size = kernel_size
         dev = gaussians._xyz.device
         self.bg = torch.zeros(3, device=dev) if bg is None else bg
@@ -297,7 +301,7 @@ class TrainStep:
         err = 1 - torch.linalg.vecdot(pkg["normal"], depth_normal, dim=0)
         normal_loss = torch.where(valid_points.squeeze(), err, torch.zeros_like(err)).mean()
         self._mark()
-        ncc_loss, geo_loss = patchmatch(g, pkg, view, nearest, depth_normal, self.kernel_size, self.pipe)
+        ncc_loss, geo_loss = self.patchmatch(g, pkg, view, nearest, self.kernel_size, self.pipe)
         self._mark()
         gt = view.original_image
         l1 = torch.abs(image - gt).mean()

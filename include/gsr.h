@@ -356,6 +356,51 @@ int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const i
                        float* grad_normals, uint8_t* valid, void* stream);
 
 /*
+ * PatchMatch multi-view loss, fused (the training
+ * step's caller of sample_depth and warp_patch_ncc): replaces the torch body
+ * of PatchMatch.__call__ (utils/loss_utils.py:140-267) around its two
+ * extension calls, for one view of H x W pixels and its nearest view.
+ *  - lift: points [H*W,3] = (median_depth * ray - T) @ M, ray = ((x - Cx) / Fx,
+ *    (y - Cy) / Fy, 1) (:147-153; T = view.T, M = view.R^T, row-major);
+ *    backward: dL/dmedian_depth [H*W] for dL/dpoints.
+ *  - terms forward: from points_nearest [H*W,3] (sample_depth of the lifted
+ *    points in the nearest view) and inside [H*W] (uint8): the reprojection
+ *    into the view (point in view = tv + p @ Mv, Mv row-major), the pixel
+ *    noise, the geometric mask (inside, both depths > 0.2, noise < noise_th,
+ *    median depth > 0) and weight exp(-noise) (:160-221), and at the masked
+ *    pixels the NCC (as gsr_warp_patch_ncc, R/T/intrinsics/images likewise) of
+ *    the normalised normal [3,H*W] (:228-256).  out4 (device) = {geo_loss,
+ *    ncc_loss, d_mask count, ncc_mask count}; a loss over an empty mask is 0
+ *    (:223-224).  saved_* ([H*W] w, flags, gd; [H*W,3] gn) are for the
+ *    backward.  One scratch allocation (16 B per 256 pixels); no host
+ *    synchronisation.
+ *  - terms backward: dL/d(points_nearest, median_depth, normal) for
+ *    dL/d(geo_loss, ncc_loss) = dL_dloss2 (device, 2 floats).  Every output
+ *    element is written.
+ */
+int gsr_patchmatch_lift(int H, int W, float Fx, float Fy, float Cx, float Cy, const float* T, const float* M,
+                        const float* median_depth, float* points, void* stream);
+int gsr_patchmatch_lift_backward(int H, int W, float Fx, float Fy, float Cx, float Cy, const float* M,
+                                 const float* dL_dpoints, float* dL_dmedian_depth, void* stream);
+int gsr_patchmatch_terms_forward(gsr_alloc_fn scratch_alloc, void* scratch_ctx, int H, int W,
+                                 const float* median_depth, const float* normal, const float* points_nearest,
+                                 const uint8_t* inside, const float* Mv, const float* tv, float Fx, float Fy, float Cx,
+                                 float Cy, float noise_th, const float* R, const float* T, const float* image_r,
+                                 const float* image_n, float fx_r, float fy_r, float cx_r, float cy_r, float fx_n,
+                                 float fy_n, float cx_n, float cy_n, int image_height_n, int image_width_n,
+                                 float* saved_w, uint8_t* saved_flags, float* saved_gd, float* saved_gn,
+                                 float* out4, void* stream);
+int gsr_patchmatch_terms_backward(int H, int W, const float* median_depth, const float* normal,
+                                  const float* points_nearest, const uint8_t* inside, const float* Mv, const float* tv,
+                                  float Fx, float Fy, float Cx, float Cy, float noise_th, const float* R,
+                                  const float* T, const float* image_r, const float* image_n, float fx_r, float fy_r,
+                                  float cx_r, float cy_r, float fx_n, float fy_n, float cx_n, float cy_n,
+                                  int image_height_n, int image_width_n, const float* saved_w,
+                                  const uint8_t* saved_flags, const float* saved_gd, const float* saved_gn,
+                                  const float* out4, const float* dL_dloss2, float* dL_dpoints_nearest,
+                                  float* dL_dmedian_depth, float* dL_dnormal, void* stream);
+
+/*
  * D-SSIM term: replaces the external fused_ssim(img1,
  * img2, padding) that utils/loss_utils.py:48-49 calls (padding "valid") with
  * the SSIM of the reference's own _ssim (loss_utils.py:36-72): 11 x 11

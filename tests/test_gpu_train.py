@@ -62,11 +62,131 @@ def test_patchmatch_empty_mask_returns_zero(setup):
     g = step.g
     pkg = render(view, g, step.pipe, step.bg, step.kernel_size, require_depth=True)
     pkg = dict(pkg, median_depth=pkg["median_depth"] * 0.0)
-    ncc, geo = gsr_train.patchmatch(g, pkg, view, nearest, None, step.kernel_size, step.pipe)
-    assert float(ncc) == 0.0 and float(geo) == 0.0
+    from gsr_patchmatch import patchmatch_fused
     params = [g._xyz, g._opacity, g._scaling, g._rotation]
-    for ga in _grads(geo + ncc, params):
-        assert ga is None or (torch.isfinite(ga).all() and float(ga.abs().max()) == 0.0)
+    for fn in (gsr_train.patchmatch, patchmatch_fused):
+        ncc, geo = fn(g, pkg, view, nearest, step.kernel_size, step.pipe)
+        assert float(ncc) == 0.0 and float(geo) == 0.0
+        for ga in _grads(geo + ncc, params):
+            assert ga is None or (torch.isfinite(ga).all() and float(ga.abs().max()) == 0.0)
+
+
+def _rel(a, b):
+    return float((a - b).norm()) / max(float(b.norm()), 1e-30)
+
+
+def _close(a, b, name=""):
+    """Gradient agreement for fp32-sensitive terms: relative L2 <= 1e-3 and
+    99% of the entries within 1e-4 of the largest magnitude."""
+    assert _rel(a, b) <= 1e-3, (name, _rel(a, b))
+    tol = 1e-4 * float(b.abs().max())
+    frac = float(((a - b).abs() <= tol).float().mean())
+    assert frac >= 0.99, (name, frac)
+
+
+def _pm_inputs(setup):
+    gsr_train, step, view, nearest = setup
+    from gaussian_renderer import render
+    pkg = render(view, step.g, step.pipe, step.bg, step.kernel_size, require_depth=True)
+    md = pkg["median_depth"].detach().requires_grad_(True)
+    nrm = pkg["normal"].detach().requires_grad_(True)
+    return gsr_train, step, view, nearest, dict(pkg, median_depth=md, normal=nrm), md, nrm
+
+
+def test_fused_patchmatch_lift_matches_torch(setup):
+    """The lift kernel against the reference's (md * ray - T) @ R^T
+    (loss_utils.py:147-153): points and dL/dmd to fp32 rounding."""
+    gsr_train, step, view, nearest, pkg, md, nrm = _pm_inputs(setup)
+    import gsr_patchmatch as PM
+    rays, _, _ = gsr_train._pixel_grids(view, md.device)
+    ref = gsr_train._mat3(md.squeeze().unsqueeze(-1) * rays - view.T, view.R.T)
+    got = PM._Lift.apply(md, view.T, view.R.T.contiguous(), (view.Fx, view.Fy, view.Cx, view.Cy))
+    torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-6 * float(ref.abs().max()))
+    g = torch.randn_like(ref)
+    assert _rel(torch.autograd.grad(got, md, g)[0], torch.autograd.grad(ref, md, g)[0]) <= 1e-6
+
+
+def test_fused_patchmatch_geo_terms_match_torch(setup):
+    """The terms kernel's geometric loss from one set of sampled points
+    against the reference's reprojection, pairwise distance and masked mean
+    (loss_utils.py:160-226): the loss to 1e-5 and dL/d(sampled point) to 1e-3
+    relative L2 (99% of the pixels within 1e-4 of the largest) at the pixels
+    whose reprojection error is >= 0.1 px.  The gradient's direction is that
+    of proj - pixel + 1e-6 over its length: at a point that reprojects onto
+    its own pixel (consistent median depths) that is the pairwise distance's
+    eps plus fp32 rounding of a ~300 px coordinate (ulp 3e-5) in either
+    formulation, and it converges as 1 / error — there only the count of such
+    pixels and finiteness are compared."""
+    gsr_train, step, view, nearest, pkg, md, nrm = _pm_inputs(setup)
+    import gsr_patchmatch as PM
+    from gaussian_renderer import sample_depth
+    rays, pixels, pixels_f = gsr_train._pixel_grids(view, md.device)
+    pts = gsr_train._mat3(md.detach().squeeze().unsqueeze(-1) * rays - view.T, view.R.T)
+    smp = sample_depth(pts, nearest, step.g, step.pipe, step.kernel_size)
+    pin = smp["sampled_depth"].detach().requires_grad_(True)
+    inside = smp["inside"]
+    with torch.no_grad():
+        wv = view.world_view_transform
+        tv = -wv[:3, :3].T @ nearest.R @ nearest.T + wv[3, :3]
+        Mv = nearest.R.transpose(1, 0) @ wv[:3, :3]
+    piv = tv + gsr_train._mat3(pin, Mv)
+    proj = piv[..., :2] / torch.clamp_min(piv[..., 2:], 1e-7)
+    proj = torch.addcmul(proj.new_tensor([view.Cx, view.Cy]), proj.new_tensor([view.Fx, view.Fy]), proj)
+    noise = torch.pairwise_distance(proj, pixels_f)
+    with torch.no_grad():
+        dm = inside & (pin[..., -1] > 0.2) & (piv[..., -1] > 0.2) & (noise < 1.0) & (md.squeeze() > 0)
+        w = torch.exp(-noise).masked_fill_(~dm, 0.0)
+    ref = gsr_train.masked_mean(w * noise, dm, empty=0.0)
+    got, _ = PM._Terms.apply(md, nrm, pin, inside, PM._Consts(view, nearest))
+    assert int(dm.sum()) > 100
+    assert abs(float(got) - float(ref)) <= 1e-5 * float(ref)
+    (ga,) = torch.autograd.grad(got, pin)
+    (gb,) = torch.autograd.grad(ref, pin)
+    good = (noise >= 0.1) & dm
+    assert int(good.sum()) > 100
+    _close(ga[good], gb[good])
+    kink = dm & ~good
+    assert torch.isfinite(ga).all()
+    assert int((ga[kink] != 0).any(-1).sum()) == int((gb[kink] != 0).any(-1).sum())
+    assert not (ga[~dm] != 0).any()
+
+
+def test_fused_patchmatch_ncc_matches_torch(setup):
+    """The NCC loss on the full chain (lift, sample_depth, terms) against the
+    reference's (gather, warp_patch_ncc, clamp, masked mean; loss_utils.py:
+    228-262): the loss to 1e-4 relative and its gradients into the median
+    depth and the rendered normals on the same pixels, 99% of them within 1e-4
+    of the largest and 1e-3 relative L2 overall: the NCC's forward-mode
+    derivatives divide by the plane's distance along the ray (ncc.hip), so the
+    last-bit differences between torch's F.normalize and the kernel's (and
+    between the compacted and the dense kernel's instruction schedules) reach
+    ~3% at a few near-grazing pixels (measured: relative L2 1.9e-4, the top 10
+    pixels 60% of it)."""
+    gsr_train, step, view, nearest, pkg, md, nrm = _pm_inputs(setup)
+    from gsr_patchmatch import patchmatch_fused
+    g = step.g
+    t = gsr_train.patchmatch_terms(g, pkg, view, nearest, step.kernel_size, step.pipe)
+    assert int(t["ncc_mask"].sum()) > 100, "scene too sparse to test"
+    ref = gsr_train.patchmatch(g, pkg, view, nearest, step.kernel_size, step.pipe)[0]
+    got = patchmatch_fused(g, pkg, view, nearest, step.kernel_size, step.pipe)[0]
+    assert float(ref) > 0.0
+    assert abs(float(got) - float(ref)) <= 1e-4 * abs(float(ref)), (float(got), float(ref))
+    for name, ga, gb in zip(["median_depth", "normal"], _grads(got, [md, nrm]), _grads(ref, [md, nrm])):
+        assert torch.isfinite(ga).all(), name
+        assert torch.equal(ga != 0, gb != 0), name
+        _close(ga, gb, name)
+
+
+def test_train_step_fused_and_torch_patchmatch_agree(setup):
+    """One whole iteration's loss with either PatchMatch (fresh copies of the
+    same Gaussians, so both start from the same state)."""
+    import gsr_train
+    out = []
+    for fused in (True, False):
+        step, view, nearest = gsr_train.synthetic_training_setup(20_000, 320, 240, device="cuda", seed=3)
+        step = gsr_train.TrainStep(step.g, fused_patchmatch=fused)
+        out.append(float(step.step(view, nearest)))
+    assert abs(out[0] - out[1]) <= 1e-5 * abs(out[1]), out
 
 
 def test_train_step_runs(setup):

@@ -77,3 +77,21 @@ print(json.dumps({"what": "sample_depth fwd+bwd (autograd), 1M Gaussians, 1920x1
                   "ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1 / dt, 2), "num_rendered": out[0],
                   "num_points": out[1], "inside": int(out[4].sum()),
                   "stage_ms": {k: round(v / n, 4) for k, (v, n) in st.items() if n}}))
+if os.environ.get("SAMPLE_STATS"):  # the SAMPLE raster's counters (and, in a -DGSR_PHASE_CLOCK=1 build, clocks)
+    _C.set_option(_C.OPT_RENDER_STATS, 1)
+    _C.debug_render_stats(reset=True)
+    _C.sample_rasterized_depth(pts.detach(), params["means3D"].detach(), params["opacities"].detach(),
+                               params["scales"].detach(), params["rotations"].detach(), 1.0, torch.Tensor([]),
+                               cam1.world_view_transform, cam1.full_proj_transform, tanx, tany, 0.0, H, W,
+                               cam1.camera_center, False, False)
+    torch.cuda.synchronize()
+    s = _C.debug_render_stats(reset=True)
+    _C.set_option(_C.OPT_RENDER_STATS, 0)
+    print("walk wave-steps", s[0], "active lanes/step", round(s[1] / max(s[0], 1), 2), "composite wave-steps", s[2],
+          "blending lanes/step", round(s[3] / max(s[2], 1), 2), "refine waves", s[4], "pass waves", s[5],
+          "root updates", s[6], "lanes left", s[7])
+    if s[15]:
+        for k, name in enumerate(("composite", "masks/staging", "probe walk", "Halley walks", "passes", "-", "-")):
+            print(f"clock {name}: {s[8 + k]:.4g} ({s[8 + k] / s[15]:.3f})")
+        print(f"clock prologue (in composite): {s[16]:.4g}; batches {s[17]} (per wave {s[17] / max(s[4], 1):.2f}), "
+              f"with the wave's lanes all done {s[18]}")
