@@ -1183,6 +1183,38 @@ int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const i
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "warp_patch_ncc", e);
 }
 
+int gsr_scale_opacity_3d_filter(int P, const float* scaling, const float* opacity, const float* filter_3D,
+                                float* scales, float* opacities, void* stream_ptr) {
+    if (P < 0 || (P > 0 && (!scaling || !opacity || !filter_3D || !scales || !opacities)))
+        return fail(GSR_ERR_ARGS, "scale/opacity getter: invalid arguments");
+    hipError_t e = launch_scale_opacity(P, scaling, opacity, filter_3D, scales, opacities, nullptr, nullptr, nullptr,
+                                        nullptr, false, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "scale/opacity getter", e);
+}
+
+int gsr_scale_opacity_3d_filter_backward(int P, const float* scaling, const float* opacity, const float* filter_3D,
+                                         const float* dL_dscales, const float* dL_dopacities, float* dL_dscaling,
+                                         float* dL_dopacity, void* stream_ptr) {
+    if (P < 0 || (P > 0 && (!scaling || !opacity || !filter_3D || !dL_dscaling || !dL_dopacity)))
+        return fail(GSR_ERR_ARGS, "scale/opacity getter backward: invalid arguments");
+    hipError_t e = launch_scale_opacity(P, scaling, opacity, filter_3D, nullptr, nullptr, dL_dscales, dL_dopacities,
+                                        dL_dscaling, dL_dopacity, true, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "scale/opacity getter backward", e);
+}
+
+int gsr_normalize_rows(int n, int D, const float* x, float* y, void* stream_ptr) {
+    if (n < 0 || D <= 0 || (n > 0 && (!x || !y))) return fail(GSR_ERR_ARGS, "normalize: invalid arguments");
+    hipError_t e = launch_normalize_rows(n, D, x, nullptr, y, false, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "normalize", e);
+}
+
+int gsr_normalize_rows_backward(int n, int D, const float* x, const float* dL_dy, float* dL_dx, void* stream_ptr) {
+    if (n < 0 || D <= 0 || (n > 0 && (!x || !dL_dy || !dL_dx)))
+        return fail(GSR_ERR_ARGS, "normalize backward: invalid arguments");
+    hipError_t e = launch_normalize_rows(n, D, x, dL_dy, dL_dx, true, (hipStream_t)stream_ptr);
+    return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "normalize backward", e);
+}
+
 int gsr_patchmatch_lift(int H, int W, float Fx, float Fy, float Cx, float Cy, const float* T, const float* M,
                         const float* median_depth, float* points, void* stream_ptr) {
     if (H < 0 || W < 0 || (H * W > 0 && (!T || !M || !median_depth || !points)))

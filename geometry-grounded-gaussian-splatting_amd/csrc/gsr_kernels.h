@@ -176,6 +176,13 @@ struct NccParams {
 };
 hipError_t launch_ncc(const NccParams& q, hipStream_t stream);
 
+// optim.hip: the activation getters of training (gsr_scale_opacity_3d_filter*, gsr_normalize_rows*)
+hipError_t launch_scale_opacity(int P, const float* s, const float* o, const float* f, float* scales, float* opac,
+                                const float* gS, const float* gO, float* ds, float* dop, bool backward,
+                                hipStream_t stream);
+hipError_t launch_normalize_rows(int n, int D, const float* x, const float* gy, float* out, bool backward,
+                                 hipStream_t stream);
+
 // ncc.hip: the fused PatchMatch terms of training (gsr_patchmatch_*)
 struct PatchMatchParams {
     int H, W;               // the view (reference image of the NCC)

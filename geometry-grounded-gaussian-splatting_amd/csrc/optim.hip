@@ -124,4 +124,93 @@ hipError_t launch_densify_stats(int P, const float* vgrad, const int* radii, flo
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ getters
+// GaussianModel's activation getters (scene/gaussian_model.py:146-212) that
+// feed every render and sample_depth call of training, as one thread per
+// Gaussian instead of ~10 broadcast torch ops (and ~20 in their autograd
+// backward: prod / sqrt / division / zero checks):
+//   get_scaling_n_opacity_with_3D_filter (and the separate
+//   get_scaling_with_3D_filter / get_opacity_with_3D_filter):
+//     q = exp(s)^2, a = q + f^2, scales = sqrt(a),
+//     opacity = sigmoid(o) sqrt(q0 q1 q2) rsqrt(a0 a1 a2)
+//   backward: dL/ds_k = gS_k q_k / sqrt(a_k) + gO opacity f^2 / a_k,
+//             dL/do = gO opacity (1 - sigmoid(o));
+//   get_rotation (F.normalize, eps 1e-12) and its backward
+//     (g - y (y . g)) / max(|x|, eps) (|x| <= eps: g / eps).
+// Pure HBM streams (20 B in, 16 B out per Gaussian).
+__global__ void __launch_bounds__(256) scale_opacity_kernel(int P, const float* __restrict__ s,
+                                                            const float* __restrict__ o,
+                                                            const float* __restrict__ f, float* __restrict__ scales,
+                                                            float* __restrict__ opac, const float* __restrict__ gS,
+                                                            const float* __restrict__ gO, float* __restrict__ ds,
+                                                            float* __restrict__ dop, bool backward) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    const float f2 = f[i] * f[i];
+    float q[3], a[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float e = expf(s[3 * i + k]);
+        q[k] = e * e;
+        a[k] = q[k] + f2;
+    }
+    const float sig = 1.f / (1.f + expf(-o[i]));
+    const float coef = sqrtf((q[0] * q[1]) * q[2]) * (1.f / sqrtf((a[0] * a[1]) * a[2]));
+    const float op = sig * coef;
+    if (!backward) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) scales[3 * i + k] = sqrtf(a[k]);
+        opac[i] = op;
+        return;
+    }
+    const float go = gO ? gO[i] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float g = gS ? gS[3 * i + k] : 0.f;
+        ds[3 * i + k] = g * (q[k] / sqrtf(a[k])) + go * op * (f2 / a[k]);
+    }
+    dop[i] = go * op * (1.f - sig);
+}
+
+__global__ void __launch_bounds__(256) normalize_rows_kernel(int n, int D, const float* __restrict__ x,
+                                                             const float* __restrict__ gy, float* __restrict__ out,
+                                                             bool backward) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float* r = x + (size_t)i * D;
+    float ss = 0.f;
+    for (int k = 0; k < D; k++) ss += r[k] * r[k];
+    const float len = sqrtf(ss), m = fmaxf(len, 1e-12f);
+    float* o = out + (size_t)i * D;
+    if (!backward) {
+        for (int k = 0; k < D; k++) o[k] = r[k] / m;
+        return;
+    }
+    const float* g = gy + (size_t)i * D;
+    if (len > 1e-12f) {
+        float dot = 0.f;
+        for (int k = 0; k < D; k++) dot += (r[k] / m) * g[k];
+        for (int k = 0; k < D; k++) o[k] = (g[k] - (r[k] / m) * dot) / m;
+    } else {
+        for (int k = 0; k < D; k++) o[k] = g[k] / m;
+    }
+}
+
+hipError_t launch_scale_opacity(int P, const float* s, const float* o, const float* f, float* scales, float* opac,
+                                const float* gS, const float* gO, float* ds, float* dop, bool backward,
+                                hipStream_t stream) {
+    if (P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scale_opacity_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, P, s, o, f, scales, opac,
+                       gS, gO, ds, dop, backward);
+    return hipGetLastError();
+}
+
+hipError_t launch_normalize_rows(int n, int D, const float* x, const float* gy, float* out, bool backward,
+                                 hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(normalize_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n, D, x, gy, out,
+                       backward);
+    return hipGetLastError();
+}
+
 }  // namespace gsr

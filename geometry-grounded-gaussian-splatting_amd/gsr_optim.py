@@ -12,12 +12,112 @@ foreach kernels.
 add_densification_stats — GaussianModel.add_densification_stats plus the
 max_radii2D update (gaussian_model.py:818-821, train.py:236-237) as one
 kernel (gsr_densify_stats).
+
+scaling_n_opacity_with_3D_filter / normalize_rows — the activation getters
+get_scaling_n_opacity_with_3D_filter and get_rotation
+(gaussian_model.py:146-212) as autograd functions over one kernel each way
+(gsr_scale_opacity_3d_filter*, gsr_normalize_rows*).
 """
 from __future__ import annotations
+
+import ctypes
 
 import torch
 
 from diff_gaussian_rasterization import _C
+
+
+def _lib():
+    L = _C._load()
+    if not getattr(L, "_getters_bound", False):
+        vp, i = ctypes.c_void_p, ctypes.c_int
+        L.gsr_scale_opacity_3d_filter.restype = i
+        L.gsr_scale_opacity_3d_filter.argtypes = [i] + [vp] * 6
+        L.gsr_scale_opacity_3d_filter_backward.restype = i
+        L.gsr_scale_opacity_3d_filter_backward.argtypes = [i] + [vp] * 8
+        L.gsr_normalize_rows.restype = i
+        L.gsr_normalize_rows.argtypes = [i, i, vp, vp, vp]
+        L.gsr_normalize_rows_backward.restype = i
+        L.gsr_normalize_rows_backward.argtypes = [i, i, vp, vp, vp, vp]
+        L._getters_bound = True
+    return L
+
+
+def _rc(L, rc):
+    if rc != 0:
+        raise RuntimeError("gsr: " + L.gsr_last_error().decode())
+
+
+def _dev32(t, name):
+    if not t.is_cuda or t.dtype != torch.float32:
+        raise RuntimeError(f"gsr getters: `{name}` must be a float32 HIP tensor")
+    return t.contiguous()
+
+
+class _ScaleOpacity(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, scaling, opacity, filter_3D):
+        L = _lib()
+        s, o, f = _dev32(scaling, "scaling"), _dev32(opacity, "opacity"), _dev32(filter_3D, "filter_3D")
+        P = s.shape[0]
+        if s.shape != (P, 3) or o.numel() != P or f.numel() != P:
+            raise RuntimeError("gsr getters: scaling [P,3], opacity [P,1], filter_3D [P,1] expected")
+        scales = torch.empty_like(s)
+        op = torch.empty_like(o)
+        with torch.cuda.device(s.device):
+            _rc(L, L.gsr_scale_opacity_3d_filter(P, s.data_ptr(), o.data_ptr(), f.data_ptr(), scales.data_ptr(),
+                                                 op.data_ptr(), _C._stream(s.device)))
+        ctx.save_for_backward(s, o, f)
+        return scales, op
+
+    @staticmethod
+    def backward(ctx, g_scales, g_op):
+        L = _lib()
+        s, o, f = ctx.saved_tensors
+        ds, do = torch.empty_like(s), torch.empty_like(o)
+        gs = None if g_scales is None else g_scales.contiguous()
+        go = None if g_op is None else g_op.contiguous()
+        with torch.cuda.device(s.device):
+            _rc(L, L.gsr_scale_opacity_3d_filter_backward(
+                s.shape[0], s.data_ptr(), o.data_ptr(), f.data_ptr(), None if gs is None else gs.data_ptr(),
+                None if go is None else go.data_ptr(), ds.data_ptr(), do.data_ptr(), _C._stream(s.device)))
+        return ds, do, None
+
+
+def scaling_n_opacity_with_3D_filter(scaling, opacity, filter_3D):
+    """(sqrt(exp(s)^2 + f^2), sigmoid(o) sqrt(prod exp(s)^2 / prod(exp(s)^2 + f^2)))
+    of gaussian_model.py's get_scaling_n_opacity_with_3D_filter, one kernel."""
+    return _ScaleOpacity.apply(scaling, opacity, filter_3D)
+
+
+class _NormalizeRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        L = _lib()
+        xc = _dev32(x, "x")
+        y = torch.empty_like(xc)
+        n, D = xc.shape[0], xc[0].numel() if xc.shape[0] else 1
+        with torch.cuda.device(xc.device):
+            _rc(L, L.gsr_normalize_rows(n, D, xc.data_ptr(), y.data_ptr(), _C._stream(xc.device)))
+        ctx.save_for_backward(xc)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        L = _lib()
+        (xc,) = ctx.saved_tensors
+        gc = g.contiguous()
+        dx = torch.empty_like(xc)
+        n, D = xc.shape[0], xc[0].numel() if xc.shape[0] else 1
+        with torch.cuda.device(xc.device):
+            _rc(L, L.gsr_normalize_rows_backward(n, D, xc.data_ptr(), gc.data_ptr(), dx.data_ptr(),
+                                                 _C._stream(xc.device)))
+        return dx
+
+
+def normalize_rows(x):
+    """F.normalize(x) over dim 1 for x [n, D] (get_rotation), one kernel."""
+    return _NormalizeRows.apply(x)
 
 
 class FusedAdam(torch.optim.Optimizer):

@@ -34,7 +34,7 @@ import gsr_scene as S
 from fused_ssim import fused_ssim
 from gaussian_renderer import render, sample_depth
 from gsr_geometry import depth_to_normal
-from gsr_optim import FusedAdam, add_densification_stats
+from gsr_optim import FusedAdam, add_densification_stats, normalize_rows, scaling_n_opacity_with_3D_filter
 from gsr_patchmatch import patchmatch_fused
 import warp_patch_ncc
 
@@ -96,6 +96,7 @@ class TrainGaussians(torch.nn.Module):
         self._sg_axis, self._sg_sharpness, self._sg_color = P(raw.sg_axis), P(raw.sg_sharpness), P(raw.sg_color)
         self.register_buffer("filter_3D", raw.filter_3D.detach().clone())
         self.active_sh_degree, self.active_sg_degree = sh_degree, sg_degree
+        self.torch_getters = False
         n = raw.xyz.shape[0]
         dev = raw.xyz.device
         self.max_radii2D = torch.zeros(n, device=dev)
@@ -121,18 +122,26 @@ class TrainGaussians(torch.nn.Module):
     def get_scaling(self):
         return torch.exp(self._scaling)
 
+    # (the three 3D-filter getters and get_rotation on the fused kernels of gsr_optim; torch_getters=True
+    # keeps the reference's torch expressions, which tests/test_gpu_train.py compares them with)
     @property
     def get_scaling_with_3D_filter(self):
+        if not self.torch_getters:
+            return scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D)[0]
         return torch.sqrt(torch.square(self.get_scaling) + torch.square(self.filter_3D))
 
     @property
     def get_opacity_with_3D_filter(self):
+        if not self.torch_getters:
+            return scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D)[1]
         sq = torch.square(self.get_scaling)
         coef = torch.sqrt(sq.prod(dim=1) / (sq + torch.square(self.filter_3D)).prod(dim=1))
         return torch.sigmoid(self._opacity) * coef[..., None]
 
     @property
     def get_scaling_n_opacity_with_3D_filter(self):
+        if not self.torch_getters:
+            return scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D)
         sq = torch.square(self.get_scaling)
         after = sq + torch.square(self.filter_3D)
         coef = sq.prod(dim=1).sqrt() * after.prod(dim=1).rsqrt()
@@ -140,6 +149,8 @@ class TrainGaussians(torch.nn.Module):
 
     @property
     def get_rotation(self):
+        if not self.torch_getters:
+            return normalize_rows(self._rotation)
         return F.normalize(self._rotation)
 
     @property

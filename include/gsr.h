@@ -356,6 +356,26 @@ int gsr_warp_patch_ncc(int P, const float* depths, const float* normals, const i
                        float* grad_normals, uint8_t* valid, void* stream);
 
 /*
+ * GaussianModel's activation getters (the callers of the
+ * rasterizer in training; scene/gaussian_model.py:146-212), one thread per
+ * Gaussian.  scale/opacity with the 3D filter
+ * (get_scaling_n_opacity_with_3D_filter): scaling [P,3] and opacity [P]
+ * are the raw parameters, filter_3D [P]; scales [P,3] = sqrt(exp(s)^2 +
+ * f^2), opacities [P] = sigmoid(o) * sqrt(prod exp(s)^2 / prod(exp(s)^2 +
+ * f^2)).  The backward writes dL/dscaling, dL/dopacity for dL/dscales,
+ * dL/dopacities (either may be NULL: zero).  normalize_rows: y = x /
+ * max(|x|, 1e-12) per row of D (get_rotation's F.normalize) and its
+ * backward.
+ */
+int gsr_scale_opacity_3d_filter(int P, const float* scaling, const float* opacity, const float* filter_3D,
+                                float* scales, float* opacities, void* stream);
+int gsr_scale_opacity_3d_filter_backward(int P, const float* scaling, const float* opacity, const float* filter_3D,
+                                         const float* dL_dscales, const float* dL_dopacities, float* dL_dscaling,
+                                         float* dL_dopacity, void* stream);
+int gsr_normalize_rows(int n, int D, const float* x, float* y, void* stream);
+int gsr_normalize_rows_backward(int n, int D, const float* x, const float* dL_dy, float* dL_dx, void* stream);
+
+/*
  * PatchMatch multi-view loss, fused (the training
  * step's caller of sample_depth and warp_patch_ncc): replaces the torch body
  * of PatchMatch.__call__ (utils/loss_utils.py:140-267) around its two

@@ -213,3 +213,44 @@ def test_mat3_and_rays_match_the_reference_products():
     assert torch.equal(depth * rays, ref)
     assert pixels.dtype == torch.int32 and torch.equal(pixels[..., 0][0], torch.arange(64, device="cuda", dtype=torch.int32))
     assert torch.equal(pixels_f, pixels.float())
+
+
+def test_fused_getters_match_torch(setup):
+    """The fused activation getters (gsr_optim: scale / opacity with the 3D
+    filter, get_rotation's normalisation) against the reference's torch
+    expressions (gaussian_model.py:146-212): values to 2e-6 relative and
+    their gradients for random upstream gradients to 1e-5 relative L2."""
+    _, step, _, _ = setup
+    g = step.g
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    saved_filter = g.filter_3D.clone()
+    # a filter of the scales' size (the synthetic scene's is zero: the f^2 terms would go unchecked)
+    g.filter_3D.copy_(torch.exp(g._scaling.detach()).mean(1, keepdim=True)
+                      * torch.rand(g.filter_3D.shape, device="cuda", generator=gen))
+    try:
+        _check_getters(g, gen)
+    finally:
+        g.filter_3D.copy_(saved_filter)
+
+
+def _check_getters(g, gen):
+    outs = {}
+    for torch_getters in (True, False):
+        g.torch_getters = torch_getters
+        try:
+            sc, op = g.get_scaling_n_opacity_with_3D_filter
+            vals = [sc, op, g.get_scaling_with_3D_filter, g.get_opacity_with_3D_filter, g.get_rotation]
+        finally:
+            g.torch_getters = False
+        outs[torch_getters] = vals
+    ups = [torch.randn(v.shape, device="cuda", generator=gen) for v in outs[True]]
+    for k, (a, b) in enumerate(zip(outs[False], outs[True])):
+        torch.testing.assert_close(a, b, rtol=2e-6, atol=0.0, msg=f"getter {k}")
+        leaves = [g._scaling, g._opacity, g._rotation]
+        ga = torch.autograd.grad(a, leaves, ups[k], retain_graph=True, allow_unused=True)
+        gb = torch.autograd.grad(b, leaves, ups[k], retain_graph=True, allow_unused=True)
+        ga = [torch.zeros_like(lf) if x is None else x for x, lf in zip(ga, leaves)]  # (unused: None or zeros)
+        gb = [torch.zeros_like(lf) if y is None else y for y, lf in zip(gb, leaves)]
+        scale = max(float(y.norm()) for y in gb)
+        for j, (x, y) in enumerate(zip(ga, gb)):
+            assert float((x - y).norm()) <= 1e-5 * max(float(y.norm()), 1e-2 * scale), (k, j, _rel(x, y))
