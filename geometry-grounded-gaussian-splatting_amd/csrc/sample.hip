@@ -177,6 +177,9 @@ hipError_t launch_sample_setup(int PN, uint32_t tiles, const PointBinState& pb, 
 }
 
 // ------------------------------------------------------------------ backward
+#ifndef GSR_SAMPLE_BWD_PAIRS
+#define GSR_SAMPLE_BWD_PAIRS 1
+#endif
 struct SampleBwdArgs {
     const uint2* ranges;
     const uint32_t* point_list;
@@ -375,6 +378,223 @@ __global__ void __launch_bounds__(256) sample_bwd_kernel(SampleBwdArgs a) {
     }
 }
 
+// The same with two points per lane (GSR_SAMPLE_BWD_PAIRS): a 128-lane
+// workgroup per 256-point chunk, the lane's points p and p + 128 in the
+// halves of packed registers.  Per (wave, Gaussian) step the record reads,
+// the skip ballot, the transpose reduction and the atomic serve 128 points
+// instead of 64, and the per-point arithmetic runs as v_pk_* pairs; every
+// packed operation rounds as the scalar one, so alpha and the contribute
+// decisions stay bit-identical to the forward's.
+typedef float sf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ sf2 ssplat(float v) { return sf2{v, v}; }
+__device__ __forceinline__ sf2 ssel(bool ca, bool cb, sf2 x, sf2 y) { return sf2{ca ? x.x : y.x, cb ? x.y : y.y}; }
+
+constexpr int kSbLanes = kTilePixels / 2;
+
+__global__ void __launch_bounds__(kSbLanes) sample_bwd_pairs_kernel(SampleBwdArgs a) {
+    __shared__ float4 s_w0[kTilePixels], s_w1[kTilePixels], s_w2[kTilePixels];
+    __shared__ uint32_t s_id[kTilePixels];
+
+    if (blockIdx.x >= a.totals[2]) return;  // uniform over the block
+    const uint32_t chunk = a.chunk_order ? a.chunk_order[blockIdx.x] : xcd_remap(blockIdx.x, a.totals[2]);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t tile = wave_find_chunk_tile(a.chunk_off, a.num_tiles, chunk);
+    const uint2 range = a.ranges[tile];
+    const int max_contrib = (int)a.chunk_max[chunk];
+    const uint2 pr = a.pt_ranges[tile];
+    const uint32_t base = pr.x + (chunk - a.chunk_off[tile]) * kTilePixels + tid;
+
+    // per-point seed (sample_backward.cu:138-158), one point per half
+    float px[2] = {0.f, 0.f}, py[2] = {0.f, 0.f}, md[2] = {0.f, 0.f}, dLD[2] = {0.f, 0.f}, dT[2] = {0.f, 0.f};
+    float gpx[2] = {0.f, 0.f}, gpy[2] = {0.f, 0.f};
+    uint32_t last[2] = {0u, 0u}, pid[2] = {0u, 0u};
+    bool in[2] = {false, false}, on[2] = {false, false}, cached[2] = {false, false};
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const uint32_t slot = base + q * kSbLanes;
+        in[q] = slot < pr.y;
+        if (!in[q]) continue;
+        pid[q] = a.pt_list[slot];
+        const uint32_t id = pid[q];
+        const float2 xy = a.pt_xy[id];
+        px[q] = xy.x;
+        py[q] = xy.y;
+        last[q] = a.pt_last[id];
+        md[q] = a.pt_mdepth[id];
+        const bool in_r = a.inside[id] != 0;
+        const float g0 = a.dL_doutput[3 * id], g1 = a.dL_doutput[3 * id + 1], g2 = a.dL_doutput[3 * id + 2];
+        const float pnx = (px[q] - (float)(a.W - 1) / 2.f) / a.focal_x;
+        const float pny = (py[q] - (float)(a.H - 1) / 2.f) / a.focal_y;
+        const float rln = 1.0f / sqrtf(pnx * pnx + pny * pny + 1.f);
+        const float rln2 = 1.f / (pnx * pnx + pny * pny + 1.f);
+        const float depth = md[q] * rln;
+        const float dL_ddepth = g0 * pnx + g1 * pny + g2;
+        dLD[q] = rln * dL_ddepth;
+        const float aux = dL_ddepth * rln2;
+        gpx[q] = (g0 - aux * pnx) * depth / a.focal_x;
+        gpy[q] = (g1 - aux * pny) * depth / a.focal_y;
+        on[q] = last[q] != 0 && in_r;
+        cached[q] = a.pt_cached[id] != 0;
+        dT[q] = cached[q] ? a.pt_dT[id] : 0.f;
+    }
+    const int rounds = (max_contrib + kTilePixels - 1) / kTilePixels;
+    auto stage = [&](int i, bool ids) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int k = tid + h * kSbLanes;
+            const int c = i * kTilePixels + k;
+            if (c < max_contrib) {
+                const uint32_t g = a.point_list[range.x + c];
+                const Splat* sp = a.splats + g;
+                s_w0[k] = sp->w0;
+                s_w1[k] = sp->w1;
+                s_w2[k] = sp->w2;
+                if (ids) s_id[k] = g;
+            }
+        }
+    };
+
+    // pre-pass dT/dt_m (sample_backward.cu:170-215) for points the forward did not cache
+    {
+        const bool need0 = on[0] && !cached[0], need1 = on[1] && !cached[1];
+        const uint32_t wave_last = wave_max_u(max(need0 ? last[0] : 0u, need1 ? last[1] : 0u));
+        const bool block_needs = __syncthreads_or(wave_last != 0u);
+        uint32_t c = 0;
+        int toDo = max_contrib;
+        for (int i = 0; block_needs && i < rounds; i++, toDo -= kTilePixels) {
+            __syncthreads();
+            stage(i, false);
+            __syncthreads();
+            const int n = min(kTilePixels, toDo);
+            for (int j = 0; j < n && c < wave_last; j++) {
+                c++;
+                const float4 w0 = s_w0[j], w1 = s_w1[j], w2 = s_w2[j];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const bool need = q ? need1 : need0;
+                    const float dx = w0.x - px[q], dy = w0.y - py[q];
+                    const float power = splat_power(w0, w1, dx, dy);
+                    const float alpha = fminf(0.99f, w1.y * __expf(power));
+                    if (!(need && c <= last[q] && !(power > 0.f) && !(alpha < 1.0f / 255.0f))) continue;
+                    const float t_peak = splat_tpeak(w1, w2, dx, dy);
+                    const float t_delta = (md[q] - t_peak) * w2.y;
+                    const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
+                    dT[q] += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * w2.y;
+                }
+            }
+        }
+    }
+    const sf2 kappa = {on[0] ? dLD[0] / fmaxf(-dT[0], 1e-7f) : 0.f, on[1] ? dLD[1] / fmaxf(-dT[1], 1e-7f) : 0.f};
+    const uint32_t wave_last = wave_max_u(max(on[0] ? last[0] : 0u, on[1] ? last[1] : 0u));
+    const sf2 pixx = {px[0], px[1]}, pixy = {py[0], py[1]}, mDepth = {md[0], md[1]};
+    sf2 dpx = {gpx[0], gpx[1]}, dpy = {gpy[0], gpy[1]};
+
+    // main pass, front to back (sample_backward.cu:228-354)
+    const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
+    constexpr float kLog2e = 1.44269504088896340736f;
+    uint32_t contributor = 0;
+    int toDo = max_contrib;
+    for (int i = 0; i < rounds; i++, toDo -= kTilePixels) {
+        __syncthreads();
+        stage(i, true);
+        __syncthreads();
+        const int n = min(kTilePixels, toDo);
+        for (int j = 0; j < n && contributor < wave_last; j++) {
+            contributor++;
+            const float4 w0 = s_w0[j], w1 = s_w1[j];
+            sf2 dx = ssplat(w0.x) - pixx, dy = ssplat(w0.y) - pixy;
+            sf2 power;
+            {
+#pragma clang fp contract(off)
+                const sf2 ax = (ssplat(w0.z) * dx) * dx;  // splat_power, per half
+                const sf2 qq = __builtin_elementwise_fma(ssplat(w1.x) * dy, dy, ax);
+                power = __builtin_elementwise_fma(ssplat(-0.5f), qq, -((ssplat(w0.w) * dx) * dy));
+            }
+            const sf2 pe = power * ssplat(kLog2e);  // __expf(x) = v_exp_f32(x log2 e)
+            const sf2 G = {__builtin_amdgcn_exp2f(pe.x), __builtin_amdgcn_exp2f(pe.y)};
+            const sf2 og = ssplat(w1.y) * G;
+            const bool va = on[0] & (contributor <= last[0]) & !(power.x > 0.f) & !(og.x < 1.0f / 255.0f);
+            const bool vb = on[1] & (contributor <= last[1]) & !(power.y > 0.f) & !(og.y < 1.0f / 255.0f);
+            if (__ballot(va | vb) == 0ull) continue;  // wave-uniform skip (warp.any)
+            const float4 w2 = s_w2[j];
+            // (an invalid half: offsets 0 keep its terms finite, its gradient factors are zeroed below)
+            dx = ssel(va, vb, dx, ssplat(0.f));
+            dy = ssel(va, vb, dy, ssplat(0.f));
+            const sf2 alpha = {fminf(0.99f, og.x), fminf(0.99f, og.y)};
+            sf2 t_peak;
+            {
+#pragma clang fp contract(off)
+                t_peak = __builtin_elementwise_fma(ssplat(w1.w), dy, ssplat(w1.z) * dx) + ssplat(w2.x);
+            }
+            const float rsig = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, w2.y)));
+            const sf2 md_tp = mDepth - t_peak;
+            const sf2 t_delta = md_tp * ssplat(rsig);
+            const sf2 ge = ((ssplat(-0.5f) * t_delta) * t_delta) * ssplat(kLog2e);
+            const sf2 G_exp = {__builtin_amdgcn_exp2f(ge.x), __builtin_amdgcn_exp2f(ge.y)};
+            const sf2 Gt = alpha * G_exp;
+            const sf2 omg = ssplat(1.f) - Gt, oma = ssplat(1.f) - alpha;
+            sf2 dL_dGt = (kappa * ssplat(0.25f)) * sf2{fast_rcp(omg.x), fast_rcp(omg.y)};
+            dL_dGt = ssel(md_tp.x > 0.f, md_tp.y > 0.f, dL_dGt, -dL_dGt);
+            dL_dGt = ssel(va && rsig > 0.f, vb && rsig > 0.f, dL_dGt, ssplat(0.f));
+            const sf2 kr = ssel(va && t_delta.x > 0.f, vb && t_delta.y > 0.f,
+                                ssplat(0.5f) * sf2{fast_rcp(oma.x), fast_rcp(oma.y)}, ssplat(0.f));
+            const sf2 dL_dopa = dL_dGt * G_exp - kappa * kr;
+            const sf2 dL_ddelta = -dL_dGt * Gt * t_delta;
+            const sf2 dL_drsig = dL_ddelta * md_tp;
+            const sf2 dL_dt = -dL_ddelta * ssplat(rsig);
+            const sf2 dL_dG = ssplat(w1.y) * dL_dopa;
+            const sf2 Gv = ssel(va, vb, G, ssplat(0.f));  // (power > 0 may have overflowed G)
+            const sf2 gdx = Gv * dx, gdy = Gv * dy;
+            const sf2 dG_ddelx = -gdx * ssplat(w0.z) - gdy * ssplat(w0.w);
+            const sf2 dG_ddely = -gdy * ssplat(w1.x) - gdx * ssplat(w0.w);
+            const sf2 dL_ddelx = dL_dG * dG_ddelx + dL_dt * ssplat(w1.z);
+            const sf2 dL_ddely = dL_dG * dG_ddely + dL_dt * ssplat(w1.w);
+            dpx -= dL_ddelx;
+            dpy -= dL_ddely;
+            const sf2 c0 = ssplat(-0.5f) * gdx * dL_dG, c2 = ssplat(-0.5f) * gdy * dL_dG;
+            const sf2 cx = c0 * dx, cy = c0 * dy, cz = c2 * dy, ops = Gv * dL_dopa;
+            const sf2 tx = dL_dt * dx, ty = dL_dt * dy;
+            float f[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) f[q] = 0.f;
+            f[kAccMean2D + 0] = (dL_ddelx.x + dL_ddelx.y) * ddelx_dx;
+            f[kAccMean2D + 1] = (dL_ddely.x + dL_ddely.y) * ddely_dy;
+            f[kAccConic + 0] = cx.x + cx.y;
+            f[kAccConic + 1] = cy.x + cy.y;
+            f[kAccConic + 2] = cz.x + cz.y;
+            f[kAccConic + 3] = ops.x + ops.y;
+            f[kAccPlane + 0] = tx.x + tx.y;
+            f[kAccPlane + 1] = ty.x + ty.y;
+            f[kAccPlane + 2] = dL_dt.x + dL_dt.y;
+            f[kAccPlane + 3] = dL_drsig.x + dL_drsig.y;
+            const float red = wave_transpose_reduce16(f);
+            // lanes 4k hold field k; colour (0-2) and normal (9-11) are zero here
+            const int field = lane >> 2;
+            const bool field_lane = (lane & 3) == 0 && field >= kAccMean2D &&
+                                    (field < kAccNormal || field >= kAccPlane);
+            const uint32_t g = __builtin_amdgcn_readfirstlane(s_id[j]);
+            if (field_lane) atomicAdd(a.acc + (size_t)g * kAccFields + field, red);
+        }
+    }
+    const float* Pm = a.proj;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        if (!in[q]) continue;
+        // dL/dpoints2D in NDC units, then the projection backward
+        // (preprocessPointsCUDA bwd, sample_backward.cu:42-75)
+        const uint32_t id = pid[q];
+        const float gx2 = (q ? dpx.y : dpx.x) * ddelx_dx, gy2 = (q ? dpy.y : dpy.x) * ddely_dy;
+        const float mx = a.points3D[3 * id], my = a.points3D[3 * id + 1], mz = a.points3D[3 * id + 2];
+        const float hw = Pm[3] * mx + Pm[7] * my + Pm[11] * mz + Pm[15];
+        const float m_w = 1.0f / (hw + 0.0000001f);
+        const float mul1 = (Pm[0] * mx + Pm[4] * my + Pm[8] * mz + Pm[12]) * m_w * m_w;
+        const float mul2 = (Pm[1] * mx + Pm[5] * my + Pm[9] * mz + Pm[13]) * m_w * m_w;
+        a.dL_dpoints3D[3 * id + 0] = (Pm[0] * m_w - Pm[3] * mul1) * gx2 + (Pm[1] * m_w - Pm[3] * mul2) * gy2;
+        a.dL_dpoints3D[3 * id + 1] = (Pm[4] * m_w - Pm[7] * mul1) * gx2 + (Pm[5] * m_w - Pm[7] * mul2) * gy2;
+        a.dL_dpoints3D[3 * id + 2] = (Pm[8] * m_w - Pm[11] * mul1) * gx2 + (Pm[9] * m_w - Pm[11] * mul2) * gy2;
+    }
+}
+
 // chunks <= ceil(points / 256) + tiles holding points
 uint32_t sample_chunk_bound(int PN, uint32_t tiles) {
     return (uint32_t)((PN + kTilePixels - 1) / kTilePixels) + min(tiles, (uint32_t)PN);
@@ -413,7 +633,10 @@ hipError_t launch_sample_bwd(const SampleBwdParams& b, const GeomState& gs, cons
     a.acc = ws.acc;
     a.chunk_order = ws.tile_order;
     const uint32_t bound = sample_chunk_bound(b.PN, tiles);
-    hipLaunchKernelGGL(sample_bwd_kernel, dim3(bound), dim3(kTilePixels), 0, stream, a);
+    if (GSR_SAMPLE_BWD_PAIRS)
+        hipLaunchKernelGGL(sample_bwd_pairs_kernel, dim3(bound), dim3(kSbLanes), 0, stream, a);
+    else
+        hipLaunchKernelGGL(sample_bwd_kernel, dim3(bound), dim3(kTilePixels), 0, stream, a);
     return hipGetLastError();
 }
 
