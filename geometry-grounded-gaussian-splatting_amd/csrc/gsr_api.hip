@@ -467,7 +467,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 18; }
+int gsr_abi_version(void) { return 19; }
 
 int gsr_backward_chunk_size(int P, int chunks) {
     if (P < 0 || chunks < 1) return -1;
@@ -523,7 +523,7 @@ const char* gsr_last_error(void) { return g_last_error.c_str(); }
 // CR/auxiliary.h:146-148 (the reference traps the kernel)
 static const char* kPrefilteredMsg = "Point is filtered although prefiltered is set. This shouldn't happen!";
 
-int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+int gsr_rasterize_forward_ex2(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
                              gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
                              int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
                              int height, const float* means3D, const float* colors_precomp, const float* opacities,
@@ -533,13 +533,15 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
                              const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
                              float* out_color, float* out_mdepth, float* out_alpha, float* out_normal, int* radii,
                              int require_depth, int debug, void* stream_ptr, int* num_rendered,
-                             gsr_alloc_fn scratch_alloc, void* scratch_ctx) {
+                             gsr_alloc_fn scratch_alloc, void* scratch_ctx, const float* shs_rest) {
     hipStream_t stream = (hipStream_t)stream_ptr;
     if (num_rendered) *num_rendered = 0;
     FwdParams p = make_params(P, sh_degree, SHM, sg_degree, SGM, background, width, height, means3D, colors_precomp,
                               opacities, scales, rotations, cov3D_precomp, shs, sg_axis, sg_sharpness, sg_color,
                               scale_modifier, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, kernel_size,
                               require_depth);
+    p.shs_rest = shs_rest;
+    if (shs_rest && (!shs || SHM < 2)) return fail(GSR_ERR_ARGS, "split SH rows need the DC rows and SHM >= 2");
     if (const char* msg = check_params(p)) return fail(GSR_ERR_ARGS, msg);
     if (!out_color || !out_alpha || !out_mdepth || !out_normal) return fail(GSR_ERR_ARGS, "missing output buffer");
     if (!geom_alloc || !binning_alloc || !image_alloc || !tile_alloc) return fail(GSR_ERR_ARGS, "missing allocator");
@@ -661,6 +663,26 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
     return GSR_OK;
 }
 
+int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                             int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
+                             int height, const float* means3D, const float* colors_precomp, const float* opacities,
+                             const float* scales, const float* rotations, const float* cov3D_precomp,
+                             const float* shs, const float* sg_axis, const float* sg_sharpness, const float* sg_color,
+                             float scale_modifier, const float* viewmatrix, const float* projmatrix,
+                             const float* cam_pos, float tan_fovx, float tan_fovy, float kernel_size, int prefiltered,
+                             float* out_color, float* out_mdepth, float* out_alpha, float* out_normal, int* radii,
+                             int require_depth, int debug, void* stream_ptr, int* num_rendered,
+                             gsr_alloc_fn scratch_alloc, void* scratch_ctx) {
+    return gsr_rasterize_forward_ex2(geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx,
+                                     tile_alloc, tile_ctx, P, sh_degree, SHM, sg_degree, SGM, background, width,
+                                     height, means3D, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                                     shs, sg_axis, sg_sharpness, sg_color, scale_modifier, viewmatrix, projmatrix,
+                                     cam_pos, tan_fovx, tan_fovy, kernel_size, prefiltered, out_color, out_mdepth,
+                                     out_alpha, out_normal, radii, require_depth, debug, stream_ptr, num_rendered,
+                                     scratch_alloc, scratch_ctx, nullptr);
+}
+
 int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
                           gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
                           int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background, int width,
@@ -680,7 +702,7 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
                                     nullptr, nullptr);
 }
 
-int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
+int gsr_rasterize_backward_ex2(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
                               int sg_degree, int SGM, int R, const float* background, int width, int height,
                            const float* means3D, const float* colors_precomp, const float* opacities,
                            const float* scales, const float* rotations, const float* cov3D_precomp,
@@ -695,7 +717,7 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
                            float* dL_dscale, float* dL_drot, float* dL_dcov3D, float* dL_dsh, float* dL_dsg_axis,
                            float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
                            int chunks, gsr_chunk_fn on_chunk, void* chunk_ctx, float* dc_rows,
-                              void* stream_ptr) {
+                              void* stream_ptr, const float* shs_rest, float* dL_dsh_rest) {
     hipStream_t stream = (hipStream_t)stream_ptr;
     BwdParams b;
     b.f = make_params(P, sh_degree, SHM, sg_degree, SGM, background, width, height, means3D, colors_precomp,
@@ -716,6 +738,10 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
         return fail(GSR_ERR_ARGS, "missing SG gradients");
     if (chunks < 1) return fail(GSR_ERR_ARGS, "chunks must be >= 1");
     if (dc_rows && !shs) return fail(GSR_ERR_ARGS, "dc_rows needs the SH colour path");
+    if (shs_rest && (!shs || SHM < 2 || !dL_dsh_rest || dc_rows))
+        return fail(GSR_ERR_ARGS, "split SH rows need the DC rows, SHM >= 2, both gradients and no dc_rows");
+    b.f.shs_rest = shs_rest;
+    b.dL_dsh_rest = dL_dsh_rest;
     b.R = R;
     b.radii = radii;
     b.alphas = alphas;
@@ -778,6 +804,25 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
         if (on_chunk) on_chunk(chunk_ctx, b0, b1);
     }
     return GSR_OK;
+}
+
+int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
+                              int sg_degree, int SGM, int R, const float* background, int width, int height,
+                           const float* means3D, const float* colors_precomp, const float* opacities,
+                           const float* scales, const float* rotations, const float* cov3D_precomp,
+                           const float* shs, const float* sg_axis, const float* sg_sharpness,
+                           const float* sg_color, float scale_modifier, const float* viewmatrix,
+                           const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                           float kernel_size, const int* radii, const float* alphas, const float* normalmap,
+                           const float* mdepth, const void* geom_buffer, const void* binning_buffer,
+                           const void* image_buffer, const void* tile_buffer, const float* dL_dpix,
+                           const float* dL_dpix_mdepth, const float* dL_dalphas, const float* dL_dpixel_normals,
+                           float* dL_dmean3D, float* dL_dmean2D, float* dL_dcolor, float* dL_dopacity,
+                           float* dL_dscale, float* dL_drot, float* dL_dcov3D, float* dL_dsh, float* dL_dsg_axis,
+                           float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
+                           int chunks, gsr_chunk_fn on_chunk, void* chunk_ctx, float* dc_rows,
+                              void* stream_ptr) {
+    return gsr_rasterize_backward_ex2(geom_bwd_alloc, geom_bwd_ctx, P, sh_degree, SHM, sg_degree, SGM, R, background, width, height, means3D, colors_precomp, opacities, scales, rotations, cov3D_precomp, shs, sg_axis, sg_sharpness, sg_color, scale_modifier, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, kernel_size, radii, alphas, normalmap, mdepth, geom_buffer, binning_buffer, image_buffer, tile_buffer, dL_dpix, dL_dpix_mdepth, dL_dalphas, dL_dpixel_normals, dL_dmean3D, dL_dmean2D, dL_dcolor, dL_dopacity, dL_dscale, dL_drot, dL_dcov3D, dL_dsh, dL_dsg_axis, dL_dsg_sharpness, dL_dsg_color, require_depth, debug, chunks, on_chunk, chunk_ctx, dc_rows, stream_ptr, nullptr, nullptr);
 }
 
 int gsr_rasterize_backward(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,

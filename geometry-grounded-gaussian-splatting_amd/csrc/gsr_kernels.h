@@ -28,6 +28,7 @@ struct FwdParams {
     const float* sg_axis;
     const float* sg_sharpness;
     const float* sg_color;
+    const float* shs_rest = nullptr;  // split SH rows: shs holds [P][3] DC rows, shs_rest [P][SHM-1][3]
     float scale_modifier;
     const float* view;
     const float* proj;
@@ -61,6 +62,7 @@ struct BwdParams {
     float* dL_dsg_axis;
     float* dL_dsg_sharpness;
     float* dL_dsg_color;
+    float* dL_dsh_rest = nullptr;  // split SH rows (f.shs_rest): dL_dsh [P][3], dL_dsh_rest [P][SHM-1][3]
 };
 
 // preprocess_fwd.hip

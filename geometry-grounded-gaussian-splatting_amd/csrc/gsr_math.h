@@ -180,6 +180,23 @@ __device__ __forceinline__ void load_sh(const float* row, int SHM, int n, float 
         for (int k = 0; k < 48; k++) v[k] = k < 3 * n ? row[k] : 0.f;
     }
 }
+// The split layout of training (GaussianModel's _features_dc [P][1][3] and
+// _features_rest [P][SHM-1][3] as two tensors, no concatenation): the DC row
+// and the rest row (4-B aligned, 180 B at SHM 16) in 16-B pieces.
+__device__ __forceinline__ void load_sh_split(const float* dc, const float* rest, int SHM, int n, float (&v)[48]) {
+    v[0] = dc[0];
+    v[1] = dc[1];
+    v[2] = dc[2];
+    if (SHM == 16) {
+        float r[45];
+        load_row<45>(rest, r);
+#pragma unroll
+        for (int k = 0; k < 45; k++) v[3 + k] = 3 + k < 3 * n ? r[k] : 0.f;
+    } else {
+#pragma unroll
+        for (int k = 3; k < 48; k++) v[k] = (k < 3 * n && k < 3 * SHM) ? rest[k - 3] : 0.f;
+    }
+}
 // dL/dsh row: entry 3k + c = Y_k dL/dRGB_c for k < n, 0 beyond (all 3 * SHM
 // entries written), generated straight into the stores.
 __device__ __forceinline__ void store_sh_grad(float* row, int SHM, int n, const float (&Y)[16], float d0, float d1,
@@ -198,6 +215,30 @@ __device__ __forceinline__ void store_sh_grad(float* row, int SHM, int n, const 
         for (int e = 0; e < 48; e++)
             if (e < 3 * SHM) row[e] = val(e);
         for (int e = 48; e < 3 * SHM; e++) row[e] = 0.f;
+    }
+}
+
+// store_sh_grad for the split layout: the DC row and the rest row
+__device__ __forceinline__ void store_sh_grad_split(float* dc, float* rest, int SHM, int n, const float (&Y)[16],
+                                                    float d0, float d1, float d2) {
+    auto val = [&](int e) {
+        const int k = e / 3, c = e - 3 * (e / 3);
+        const float d = c == 0 ? d0 : (c == 1 ? d1 : d2);
+        return k < n ? Y[k] * d : 0.f;
+    };
+    dc[0] = val(0);
+    dc[1] = val(1);
+    dc[2] = val(2);
+    if (SHM == 16) {
+        float r[45];
+#pragma unroll
+        for (int e = 0; e < 45; e++) r[e] = val(3 + e);
+        store_row<45>(rest, r);
+    } else {
+#pragma unroll
+        for (int e = 3; e < 48; e++)
+            if (e < 3 * SHM) rest[e - 3] = val(e);
+        for (int e = 48; e < 3 * SHM; e++) rest[e - 3] = 0.f;
     }
 }
 

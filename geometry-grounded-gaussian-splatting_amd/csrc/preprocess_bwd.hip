@@ -47,6 +47,7 @@ struct PreprocessBwdArgs {
     float* dL_drot;
     float* dL_dcov3D;
     float* dL_dsh;
+    float* dL_dsh_rest;  // split rows (BwdParams::dL_dsh_rest) or null
     float* dL_dsg_axis;
     float* dL_dsg_sharpness;
     float* dL_dsg_color;
@@ -56,6 +57,17 @@ struct PreprocessBwdArgs {
     // written (gsr_view_color_grads_chunked rebuilds them from every view's DC rows)
     float* dc_rows;
 };
+
+// a Gaussian's SH gradient rows zeroed (one row, or the DC and rest rows of the split layout)
+__device__ __forceinline__ void zero_sh_rows(const PreprocessBwdArgs& a, int idx) {
+    if (!a.dL_dsh) return;
+    if (a.dL_dsh_rest) {
+        for (int k = 0; k < 3; k++) a.dL_dsh[(size_t)idx * 3 + k] = 0.f;
+        for (int k = 0; k < 3 * (a.SHM - 1); k++) a.dL_dsh_rest[(size_t)idx * 3 * (a.SHM - 1) + k] = 0.f;
+    } else {
+        for (int k = 0; k < 3 * a.SHM; k++) a.dL_dsh[(size_t)idx * 3 * a.SHM + k] = 0.f;
+    }
+}
 
 template <bool ROWS = true>
 __device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
@@ -72,8 +84,7 @@ __device__ inline void zero_outputs(const PreprocessBwdArgs& a, int idx) {
         return;
     }
     if (!ROWS) return;
-    if (a.dL_dsh)
-        for (int k = 0; k < 3 * a.SHM; k++) a.dL_dsh[(size_t)idx * 3 * a.SHM + k] = 0.f;
+    zero_sh_rows(a, idx);
     for (int k = 0; k < a.SGM; k++) {
         const size_t o = (size_t)idx * a.SGM + k;
         if (a.dL_dsg_sharpness) a.dL_dsg_sharpness[o] = 0.f;
@@ -645,6 +656,9 @@ preprocess_bwd_kernel(PreprocessBwdArgs a) {
             a.dc_rows[3 * idx] = Y[0] * dR0;
             a.dc_rows[3 * idx + 1] = Y[0] * dR1;
             a.dc_rows[3 * idx + 2] = Y[0] * dR2;
+        } else if (a.dL_dsh_rest) {
+            store_sh_grad_split(a.dL_dsh + (size_t)idx * 3, a.dL_dsh_rest + (size_t)idx * (a.SHM - 1) * 3, a.SHM, n, Y,
+                                dR0, dR1, dR2);
         } else {
             store_sh_grad(a.dL_dsh + (size_t)idx * a.SHM * 3, a.SHM, n, Y, dR0, dR1, dR2);
         }
@@ -711,8 +725,7 @@ preprocess_bwd_kernel(PreprocessBwdArgs a) {
                 if (a.dL_dsg_color) a.dL_dsg_color[3 * o + c] = 0.f;
             }
         }
-        if (a.dL_dsh)
-            for (int k = 0; k < 3 * a.SHM; k++) a.dL_dsh[(size_t)idx * 3 * a.SHM + k] = 0.f;
+        zero_sh_rows(a, idx);
     }
     a.dL_dmean3D[3 * idx] = dm0;
     a.dL_dmean3D[3 * idx + 1] = dm1;
@@ -805,6 +818,7 @@ hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const 
     a.dL_drot = b.dL_drot;
     a.dL_dcov3D = b.dL_dcov3D;
     a.dL_dsh = b.dL_dsh;
+    a.dL_dsh_rest = b.dL_dsh_rest;
     a.dL_dsg_axis = b.dL_dsg_axis;
     a.dL_dsg_sharpness = b.dL_dsg_sharpness;
     a.dL_dsg_color = b.dL_dsg_color;
@@ -817,7 +831,7 @@ hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const 
     // input rows it loads by 16-B LDS-DMA (a tensor that is a view at a 4-B offset takes the per-lane path)
     const int so = option(kOptPbwdStage);
     auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    const bool stage_ok = p.shs && !dc_rows && p.SHM == 16 && (begin & 255) == 0 && al16(b.dL_dsh) &&
+    const bool stage_ok = p.shs && !dc_rows && !b.dL_dsh_rest && p.SHM == 16 && (begin & 255) == 0 && al16(b.dL_dsh) &&
                           (p.SGM == 0 || (p.SGM == kSG7 && p.SGD == kSG7 && al16(b.dL_dsg_color) &&
                                           al16(b.dL_dsg_sharpness) && al16(b.dL_dsg_axis) &&
                                           al16(p.sg_color) && al16(p.sg_sharpness) && al16(p.sg_axis)));

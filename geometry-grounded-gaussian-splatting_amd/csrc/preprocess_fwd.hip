@@ -30,6 +30,7 @@ struct PreprocessArgs {
     const float* rotations;
     const float* cov3D_precomp;
     const float* shs;
+    const float* shs_rest;  // split rows (FwdParams::shs_rest) or null
     const float* sg_axis;
     const float* sg_sharpness;
     const float* sg_color;
@@ -272,7 +273,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_PR
         float Y[16];
         sh_basis(a.D, dx, dy, dz, Y);
         const int n = sh_count(a.D);
-        if constexpr (!HOIST) load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
+        if constexpr (!HOIST) {
+            if (a.shs_rest)
+                load_sh_split(a.shs + (size_t)idx * 3, a.shs_rest + (size_t)idx * (a.SHM - 1) * 3, a.SHM, n, sh);
+            else
+                load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
+        }
         col[0] = Y[0] * sh[0];
         col[1] = Y[0] * sh[1];
         col[2] = Y[0] * sh[2];
@@ -377,6 +383,7 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
     a.rotations = p.rotations;
     a.cov3D_precomp = p.cov3D_precomp;
     a.shs = p.shs;
+    a.shs_rest = p.shs_rest;
     a.sg_axis = p.sg_axis;
     a.sg_sharpness = p.sg_sharpness;
     a.sg_color = p.sg_color;
@@ -401,7 +408,7 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
     dsort_zero_region(gs.dsort_tmp, p.P, &a.zero_first, &a.zero_words);
     a.zero_K = gs.offsets_K;
     // (the hoisted instance needs every colour row: SH + 7 SG lobes, scales / rotations, no precomputed colours)
-    const bool hoist = p.SGM == 7 && p.SGD == 7 && p.shs && p.scales && !p.colors_precomp && !p.no_color;
+    const bool hoist = p.SGM == 7 && p.SGD == 7 && p.shs && !p.shs_rest && p.scales && !p.colors_precomp && !p.no_color;
     if (hoist)
         hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
     else

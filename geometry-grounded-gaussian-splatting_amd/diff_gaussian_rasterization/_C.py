@@ -44,7 +44,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 
 def _load():
@@ -70,6 +70,10 @@ def _load():
                                          + [f] * 3 + [vp] * 4 + [vp] * 4 + [vp] * 4 + [vp] * 11 + [i, i, vp])
     L.gsr_rasterize_backward_ex.restype = i
     L.gsr_rasterize_backward_ex.argtypes = L.gsr_rasterize_backward.argtypes[:-1] + [i, _CHUNK, vp, vp, vp]
+    L.gsr_rasterize_forward_ex2.restype = i
+    L.gsr_rasterize_forward_ex2.argtypes = L.gsr_rasterize_forward_ex.argtypes + [vp]
+    L.gsr_rasterize_backward_ex2.restype = i
+    L.gsr_rasterize_backward_ex2.argtypes = L.gsr_rasterize_backward_ex.argtypes + [vp, vp]
     L.gsr_sample_depth_forward.restype = i
     L.gsr_sample_depth_forward.argtypes = ([_ALLOC, vp] * 6 + [i] * 4 + [vp] * 4 + [f] + [vp] * 5 + [f] * 3 + [i]
                                            + [vp, vp, i, vp] + [ctypes.POINTER(i)] * 3)
@@ -295,6 +299,16 @@ def _dev_contig(t, name):
     return t.contiguous()
 
 
+def _split_rest(sh, sh_rest, P):
+    """The rest rows of the split SH layout, checked, or None (one [P, M, 3] tensor)."""
+    if sh_rest is None:
+        return None
+    if sh is None or sh.numel() == 0 or tuple(sh.shape) != (P, 1, 3) or sh_rest.dim() != 3 or \
+            sh_rest.size(0) != P or sh_rest.size(2) != 3 or sh_rest.size(1) < 1:
+        raise RuntimeError("gsr: split SH rows are sh [P, 1, 3] and sh_rest [P, M-1, 3]")
+    return _dev_contig(sh_rest, "sh_rest")
+
+
 def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -307,7 +321,11 @@ def _check(rc):
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, cov3D_precomp, sh, sg_axis,
                         sg_sharpness, sg_color, sh_degree, sg_degree, scale_modifier, viewmatrix, projmatrix,
                         tan_fovx, tan_fovy, kernel_size, image_height, image_width, campos, prefiltered,
-                        require_depth, debug):
+                        require_depth, debug, sh_rest=None):
+    """The reference's 25 arguments (rasterize_points.cu:36-139).  `sh_rest`
+    (not in the reference): the split SH layout of training — `sh` the DC
+    rows [P, 1, 3] and `sh_rest` the rest [P, M-1, 3] as GaussianModel keeps
+    them, without their concatenation (gsr_rasterize_forward_ex2)."""
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     L = _load()
@@ -325,6 +343,9 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         sg_color=sg_color, viewmatrix=viewmatrix, projmatrix=projmatrix, campos=campos).items()}
     SHM = sh.size(1) if sh is not None and sh.size(0) != 0 else 0
     SGM = sg_color.size(1) if sg_color is not None and sg_color.size(0) != 0 else 0
+    rest = _split_rest(sh, sh_rest, P)
+    if rest is not None:
+        SHM = 1 + sh_rest.size(1)
     color = torch.empty(3, H, W, **fopt)
     mdepth = torch.empty(1, H, W, **fopt)
     alpha = torch.empty(1, H, W, **fopt)
@@ -334,7 +355,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     scratch = _ScratchBlocks(dev)
     K = ctypes.c_int(0)
     with torch.cuda.device(dev):
-        rc = L.gsr_rasterize_forward_ex(
+        rc = L.gsr_rasterize_forward_ex2(
             bufs[0].cb, None, bufs[1].cb, None, bufs[2].cb, None, bufs[3].cb, None,
             P, int(sh_degree), SHM, int(sg_degree), SGM, _ptr(args["background"]), W, H, _ptr(args["means3D"]),
             _ptr(args["colors"]), _ptr(args["opacity"]), _ptr(args["scales"]), _ptr(args["rotations"]),
@@ -342,7 +363,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
             _ptr(args["sg_color"]), float(scale_modifier), _ptr(args["viewmatrix"]), _ptr(args["projmatrix"]),
             _ptr(args["campos"]), float(tan_fovx), float(tan_fovy), float(kernel_size), int(bool(prefiltered)),
             _ptr(color), _ptr(mdepth), _ptr(alpha), _ptr(normal), _ptr(radii), int(bool(require_depth)),
-            int(bool(debug)), _stream(dev), ctypes.byref(K), scratch.cb, None)
+            int(bool(debug)), _stream(dev), ctypes.byref(K), scratch.cb, None, _ptr(rest))
     del scratch
     _check(rc)
     return (K.value, color, alpha, normal, mdepth, radii, bufs[0].tensor, bufs[1].tensor, bufs[2].tensor,
@@ -354,20 +375,25 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
                                  projmatrix, tan_fovx, tan_fovy, kernel_size, dL_dout_color, dL_dout_mdepth,
                                  dL_dout_alpha, dL_dout_normal, alphas, normalmap, mdepth, campos, radii,
                                  geomBuffer, R, binningBuffer, imageBuffer, tileBuffer, require_depth, debug,
-                                 exchange=None):
+                                 exchange=None, sh_rest=None):
     """The reference's 35 arguments and 11 gradients (rasterize_points.cu:141-258).
     `exchange` (not in the reference; gsr_dist.OverlappedViewGrads) runs the
     per-Gaussian backward in exchange.chunks Gaussian ranges through
     gsr_rasterize_backward_ex and calls exchange.on_chunk(begin, end, grads)
     after each range is queued; with exchange.dc_rows(...) a buffer, only the
     DC gradient rows are written there (the SH / SG rows are the exchange's to
-    rebuild before the gradients are used)."""
+    rebuild before the gradients are used).  `sh_rest` (the split SH layout,
+    see rasterize_gaussians): dsh is then [P, 1, 3] and a 12th gradient,
+    dsh_rest [P, M-1, 3], is returned (gsr_rasterize_backward_ex2)."""
     L = _load()
     P = means3D.size(0)
     img = dL_dout_color if dL_dout_color is not None else alphas  # (a None upstream gradient is zero)
     H, W = img.size(1), img.size(2)
     SHM = sh.size(1) if sh is not None and sh.size(0) != 0 else 0
     SGM = sg_color.size(1) if sg_color is not None and sg_color.size(0) != 0 else 0
+    rest = _split_rest(sh, sh_rest, P)
+    if rest is not None and exchange is not None:
+        raise RuntimeError("gsr: the split SH layout and an in-backward view exchange do not combine")
     dev = means3D.device
     fopt = dict(dtype=torch.float32, device=dev)
     alloc = torch.zeros if P == 0 else torch.empty  # the kernels overwrite every element
@@ -375,6 +401,9 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
                 dopacity=alloc(P, 1, **fopt), dcov3D=alloc(P, 6, **fopt), dsh=alloc(P, SHM, 3, **fopt),
                 dsg_axis=alloc(P, SGM, 3, **fopt), dsg_sharpness=alloc(P, SGM, **fopt),
                 dsg_color=alloc(P, SGM, 3, **fopt), dscales=alloc(P, 3, **fopt), drotations=alloc(P, 4, **fopt))
+    if rest is not None:
+        outs["dsh_rest"] = alloc(*sh_rest.shape, **fopt)
+        SHM = 1 + sh_rest.size(1)
     if P != 0:
         a = {k: _dev_contig(v, k) for k, v in dict(
             background=background, means3D=means3D, colors=colors, opacity=opacity, scales=scales,
@@ -394,7 +423,7 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
             cb = exchange.hook(grads)  # (errors held by the exchange, raised by settle below)
             hook = _CHUNK(lambda _ctx, b, e: cb(b, e))
         with torch.cuda.device(dev):
-            rc = L.gsr_rasterize_backward_ex(
+            rc = L.gsr_rasterize_backward_ex2(
                 scratch.cb, None, P, int(sh_degree), SHM, int(sg_degree), SGM, int(R), _ptr(a["background"]), W, H,
                 _ptr(a["means3D"]), _ptr(a["colors"]), _ptr(a["opacity"]), _ptr(a["scales"]), _ptr(a["rotations"]),
                 _ptr(a["cov3D_precomp"]), _ptr(a["sh"]), _ptr(a["sg_axis"]), _ptr(a["sg_sharpness"]),
@@ -406,15 +435,16 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
                 _ptr(outs["dcolors"]), _ptr(outs["dopacity"]), _ptr(outs["dscales"]), _ptr(outs["drotations"]),
                 _ptr(outs["dcov3D"]), _ptr(outs["dsh"]), _ptr(outs["dsg_axis"]), _ptr(outs["dsg_sharpness"]),
                 _ptr(outs["dsg_color"]), int(bool(require_depth)), int(bool(debug)), chunks, hook, None,
-                None if dc is None else _ptr(dc), _stream(dev))
+                None if dc is None else _ptr(dc), _stream(dev), _ptr(rest), _ptr(outs.get("dsh_rest")))
         if exchange is not None:  # a failed backward still posts every range's collectives (no peer blocks)
             exchange.settle(rc == 0)
         _check(rc)
         if KEEP_BWD_SCRATCH:
             global last_bwd_scratch
             last_bwd_scratch = scratch.tensor
-    return (outs["dmeans2D"], outs["dcolors"], outs["dopacity"], outs["dmeans3D"], outs["dcov3D"], outs["dsh"],
-            outs["dsg_axis"], outs["dsg_sharpness"], outs["dsg_color"], outs["dscales"], outs["drotations"])
+    g = (outs["dmeans2D"], outs["dcolors"], outs["dopacity"], outs["dmeans3D"], outs["dcov3D"], outs["dsh"],
+         outs["dsg_axis"], outs["dsg_sharpness"], outs["dsg_color"], outs["dscales"], outs["drotations"])
+    return g if rest is None else g + (outs["dsh_rest"],)
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

@@ -56,8 +56,10 @@ def rasterize_gaussians(means3D, means2D, sh, sg_axis, sg_sharpness, sg_color, c
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, sg_axis, sg_sharpness, sg_color, colors_precomp, opacities, scales,
-                rotations, cov3Ds_precomp, raster_settings):
+                rotations, cov3Ds_precomp, raster_settings, sh_rest=None):
+        # (sh_rest, not in the reference: the split SH layout, sh = DC rows [P, 1, 3], GaussianRasterizer)
         s = raster_settings
+        kw_rest = {} if sh_rest is None else {"sh_rest": sh_rest}
         args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis,
                 sg_sharpness, sg_color, s.sh_degree, s.sg_degree, s.scale_modifier, s.viewmatrix, s.projmatrix,
                 s.tanfovx, s.tanfovy, s.kernel_size, s.image_height, s.image_width, s.campos, s.prefiltered,
@@ -65,13 +67,13 @@ class _RasterizeGaussians(torch.autograd.Function):
         if s.debug:
             cpu_args = cpu_deep_copy_tuple(args)
             try:
-                out = _C.rasterize_gaussians(*args)
+                out = _C.rasterize_gaussians(*args, **kw_rest)
             except Exception as ex:
                 torch.save(cpu_args, "snapshot_fw.dump")
                 print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
                 raise ex
         else:
-            out = _C.rasterize_gaussians(*args)
+            out = _C.rasterize_gaussians(*args, **kw_rest)
         num_rendered, color, alpha, normal, mdepth, radii, geomBuffer, binningBuffer, imgBuffer, tileBuffer = out
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
@@ -81,7 +83,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis,
                               sg_sharpness, sg_color, alpha, normal, mdepth, radii, geomBuffer, binningBuffer,
-                              imgBuffer, tileBuffer)
+                              imgBuffer, tileBuffer, sh_rest)
         return color, radii, mdepth, alpha, normal
 
     @staticmethod
@@ -90,14 +92,14 @@ class _RasterizeGaussians(torch.autograd.Function):
         num_rendered = ctx.num_rendered
         s = ctx.raster_settings
         (means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis, sg_sharpness, sg_color,
-         alpha, normal, mdepth, radii, geomBuffer, binningBuffer, imgBuffer, tileBuffer) = ctx.saved_tensors
+         alpha, normal, mdepth, radii, geomBuffer, binningBuffer, imgBuffer, tileBuffer, sh_rest) = ctx.saved_tensors
         args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh, sg_axis,
                 sg_sharpness, sg_color, s.sh_degree, s.sg_degree, s.scale_modifier, s.viewmatrix, s.projmatrix,
                 s.tanfovx, s.tanfovy, s.kernel_size, grad_color, grad_mdepth, grad_alpha, grad_normal, alpha, normal,
                 mdepth, s.campos, radii, geomBuffer, num_rendered, binningBuffer, imgBuffer, tileBuffer,
                 s.require_depth, s.debug)
         ex = _view_exchange
-        kw = {}
+        kw = {} if sh_rest is None else {"sh_rest": sh_rest}
         if ex is not None:  # gsr_dist.OverlappedViewGrads: the exchange rides on the backward's Gaussian ranges
             ex.begin(s.campos, means3D.shape[0], scales.numel() > 0, sh.numel() > 0)
             kw["exchange"] = ex
@@ -119,11 +121,13 @@ class _RasterizeGaussians(torch.autograd.Function):
         if ex is not None:
             ex.finish(g, means3D, sg_axis, sg_sharpness, sg_color, s.sh_degree, s.sg_degree)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
-         grad_sg_axis, grad_sg_sharpness, grad_sg_color, grad_scales, grad_rotations) = g
+         grad_sg_axis, grad_sg_sharpness, grad_sg_color, grad_scales, grad_rotations) = g[:11]
+        grad_sh_rest = g[11] if len(g) > 11 else None
         if sh.numel():
             _colour_backward_calls += 1
         return (grad_means3D, grad_means2D, grad_sh, grad_sg_axis, grad_sg_sharpness, grad_sg_color,
-                grad_colors_precomp, grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None)
+                grad_colors_precomp, grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None,
+                grad_sh_rest)
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -163,6 +167,11 @@ class GaussianRasterizer(nn.Module):
         if ((scales is None or rotations is None) and cov3D_precomp is None) or (
                 (scales is not None or rotations is not None) and cov3D_precomp is not None):
             raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        # shs may also be the pair (features_dc [P, 1, 3], features_rest [P, M-1, 3]) as GaussianModel keeps
+        # them: the kernels read and write the two as they are (no concatenation: gsr.h, the split SH layout)
+        sh_rest = None
+        if isinstance(shs, (tuple, list)):
+            shs, sh_rest = shs
         if shs is None:
             shs = torch.Tensor([])
         if colors_precomp is None:
@@ -173,6 +182,9 @@ class GaussianRasterizer(nn.Module):
             rotations = torch.Tensor([])
         if cov3D_precomp is None:
             cov3D_precomp = torch.Tensor([])
+        if sh_rest is not None:
+            return _RasterizeGaussians.apply(means3D, means2D, shs, sg_axis, sg_sharpness, sg_color, colors_precomp,
+                                             opacities, scales, rotations, cov3D_precomp, raster_settings, sh_rest)
         return rasterize_gaussians(means3D, means2D, shs, sg_axis, sg_sharpness, sg_color, colors_precomp,
                                    opacities, scales, rotations, cov3D_precomp, raster_settings)
 

@@ -155,6 +155,10 @@ class TrainGaussians(torch.nn.Module):
 
     @property
     def get_features(self):
+        # the pair as GaussianModel keeps it: GaussianRasterizer takes the split SH layout without the
+        # concatenation (192 MB at 1M Gaussians, and the gradient's split); torch_getters: the reference's cat
+        if not self.torch_getters:
+            return self._features_dc, self._features_rest
         return torch.cat((self._features_dc, self._features_rest), dim=1)
 
     @property

@@ -153,6 +153,46 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
                               float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
                               int chunks, gsr_chunk_fn on_chunk, void* chunk_ctx, float* dc_rows, void* stream);
 
+/*
+ * The split SH layout of training (round 5): GaussianModel keeps the DC and
+ * the higher-order SH coefficients as two tensors (_features_dc [P,1,3],
+ * _features_rest [P,SHM-1,3]) and get_features concatenates them every call
+ * (scene/gaussian_model.py:165-169: 192 MB at 1M Gaussians, and the
+ * gradient's split in the backward).  These two entry points take them as
+ * they are: `shs` is then the DC rows [P][3] and `shs_rest` the rest
+ * [P][SHM-1][3] (SHM counts all coefficients, as before); the backward writes
+ * dL_dsh [P][3] and dL_dsh_rest [P][SHM-1][3].  NULL shs_rest is exactly
+ * the _ex call.  Not combined with dc_rows (the overlapped exchange).
+ */
+int gsr_rasterize_forward_ex2(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                              gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
+                              int P, int sh_degree, int SHM, int sg_degree, int SGM, const float* background,
+                              int width, int height, const float* means3D, const float* colors_precomp,
+                              const float* opacities, const float* scales, const float* rotations,
+                              const float* cov3D_precomp, const float* shs, const float* sg_axis,
+                              const float* sg_sharpness, const float* sg_color, float scale_modifier,
+                              const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                              float tan_fovy, float kernel_size, int prefiltered, float* out_color, float* out_mdepth,
+                              float* out_alpha, float* out_normal, int* radii, int require_depth, int debug,
+                              void* stream, int* num_rendered, gsr_alloc_fn scratch_alloc, void* scratch_ctx,
+                              const float* shs_rest);
+int gsr_rasterize_backward_ex2(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, int P, int sh_degree, int SHM,
+                               int sg_degree, int SGM, int R, const float* background, int width, int height,
+                               const float* means3D, const float* colors_precomp, const float* opacities,
+                               const float* scales, const float* rotations, const float* cov3D_precomp,
+                               const float* shs, const float* sg_axis, const float* sg_sharpness,
+                               const float* sg_color, float scale_modifier, const float* viewmatrix,
+                               const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                               float kernel_size, const int* radii, const float* alphas, const float* normalmap,
+                               const float* mdepth, const void* geom_buffer, const void* binning_buffer,
+                               const void* image_buffer, const void* tile_buffer, const float* dL_dpix,
+                               const float* dL_dpix_mdepth, const float* dL_dalphas, const float* dL_dpixel_normals,
+                               float* dL_dmean3D, float* dL_dmean2D, float* dL_dcolor, float* dL_dopacity,
+                               float* dL_dscale, float* dL_drot, float* dL_dcov3D, float* dL_dsh, float* dL_dsg_axis,
+                               float* dL_dsg_sharpness, float* dL_dsg_color, int require_depth, int debug,
+                               int chunks, gsr_chunk_fn on_chunk, void* chunk_ctx, float* dc_rows, void* stream,
+                               const float* shs_rest, float* dL_dsh_rest);
+
 /* The Gaussian range size gsr_rasterize_backward_ex uses for `chunks` ranges
  * of P Gaussians: ceil(ceil(P / chunks) / 256) * 256 (whole 256-Gaussian
  * workgroups; the last range holds the rest).  The range-major layout of the

@@ -254,3 +254,35 @@ def _check_getters(g, gen):
         scale = max(float(y.norm()) for y in gb)
         for j, (x, y) in enumerate(zip(ga, gb)):
             assert float((x - y).norm()) <= 1e-5 * max(float(y.norm()), 1e-2 * scale), (k, j, _rel(x, y))
+
+
+def test_split_sh_layout_matches_concatenated(setup):
+    """The split SH layout (features_dc, features_rest handed to the
+    rasterizer as a pair: gsr_rasterize_{forward,backward}_ex2) against the
+    reference's concatenated get_features: images bit-identical, every
+    gradient (the DC and rest rows against the two slices of the
+    concatenated gradient) equal up to the float atomics' order."""
+    gsr_train, step, view, nearest = setup
+    from gaussian_renderer import render
+    g = step.g
+    class _Cat:  # the same model with the reference's concatenating get_features (all else delegated)
+        def __getattr__(self, name):
+            return getattr(g, name)
+
+        @property
+        def get_features(self):
+            return torch.cat((g._features_dc, g._features_rest), dim=1)
+
+    outs = {}
+    for torch_getters, pc in ((True, _Cat()), (False, g)):
+        pkg = render(view, pc, step.pipe, step.bg, step.kernel_size, require_depth=True)
+        gen = torch.Generator(device="cuda").manual_seed(11)
+        loss = (pkg["render"] * torch.randn(pkg["render"].shape, device="cuda", generator=gen)).sum() + \
+            (pkg["median_depth"] * torch.randn(pkg["median_depth"].shape, device="cuda", generator=gen)).sum()
+        leaves = [g._features_dc, g._features_rest, g._xyz, g._opacity]
+        outs[torch_getters] = (pkg, torch.autograd.grad(loss, leaves))
+    (pa, ga), (pb, gb) = outs[False], outs[True]
+    for k in ("render", "median_depth", "normal", "mask"):
+        assert torch.equal(pa[k], pb[k]), k
+    for x, y in zip(ga, gb):  # (the accumulated dL/dcolour the SH rows derive from is summed by atomics)
+        assert x.shape == y.shape and _rel(x, y) <= 1e-5, _rel(x, y)
