@@ -187,11 +187,16 @@ __device__ __forceinline__ void load_sh_split(const float* dc, const float* rest
     v[0] = dc[0];
     v[1] = dc[1];
     v[2] = dc[2];
-    if (SHM == 16) {
-        float r[45];
-        load_row<45>(rest, r);
+    if (SHM == 16) {  // straight into v (a staging array of its own raised the kernel's VGPRs 126 -> 147)
 #pragma unroll
-        for (int k = 0; k < 45; k++) v[3 + k] = 3 + k < 3 * n ? r[k] : 0.f;
+        for (int k = 0; k < 44; k += 4) {
+            const f4u t = *reinterpret_cast<const f4u*>(rest + k);
+            v[3 + k] = 3 + k < 3 * n ? t.x : 0.f;
+            v[4 + k] = 4 + k < 3 * n ? t.y : 0.f;
+            v[5 + k] = 5 + k < 3 * n ? t.z : 0.f;
+            v[6 + k] = 6 + k < 3 * n ? t.w : 0.f;
+        }
+        v[47] = 47 < 3 * n ? rest[44] : 0.f;
     } else {
 #pragma unroll
         for (int k = 3; k < 48; k++) v[k] = (k < 3 * n && k < 3 * SHM) ? rest[k - 3] : 0.f;
@@ -230,10 +235,10 @@ __device__ __forceinline__ void store_sh_grad_split(float* dc, float* rest, int 
     dc[1] = val(1);
     dc[2] = val(2);
     if (SHM == 16) {
-        float r[45];
 #pragma unroll
-        for (int e = 0; e < 45; e++) r[e] = val(3 + e);
-        store_row<45>(rest, r);
+        for (int e = 0; e < 44; e += 4)
+            *reinterpret_cast<f4u*>(rest + e) = f4u{val(3 + e), val(4 + e), val(5 + e), val(6 + e)};
+        rest[44] = val(47);
     } else {
 #pragma unroll
         for (int e = 3; e < 48; e++)

@@ -70,7 +70,7 @@ __device__ __forceinline__ void cull_foot(const PreprocessArgs& a, int idx) {
 // SH row, 196-B SG lobe rows) are requested at the top with the geometry
 // inputs, before the culling branches (one memory round trip instead of
 // three); the plain instance loads them where they are used.
-template <bool HOIST>
+template <bool HOIST, bool SPLIT = false>
 #ifndef GSR_PRE_WAVES
 #define GSR_PRE_WAVES 1
 #endif
@@ -273,12 +273,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_PR
         float Y[16];
         sh_basis(a.D, dx, dy, dz, Y);
         const int n = sh_count(a.D);
-        if constexpr (!HOIST) {
-            if (a.shs_rest)
-                load_sh_split(a.shs + (size_t)idx * 3, a.shs_rest + (size_t)idx * (a.SHM - 1) * 3, a.SHM, n, sh);
-            else
-                load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
-        }
+        if constexpr (SPLIT)  // (its own instance: the one-row kernel keeps its 126 VGPRs, 4 waves per SIMD)
+            load_sh_split(a.shs + (size_t)idx * 3, a.shs_rest + (size_t)idx * (a.SHM - 1) * 3, a.SHM, n, sh);
+        else if constexpr (!HOIST)
+            load_sh(a.shs + (size_t)idx * a.SHM * 3, a.SHM, n, sh);
         col[0] = Y[0] * sh[0];
         col[1] = Y[0] * sh[1];
         col[2] = Y[0] * sh[2];
@@ -411,6 +409,8 @@ hipError_t launch_preprocess_fwd(const FwdParams& p, const GeomState& gs, int* r
     const bool hoist = p.SGM == 7 && p.SGD == 7 && p.shs && !p.shs_rest && p.scales && !p.colors_precomp && !p.no_color;
     if (hoist)
         hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
+    else if (p.shs_rest)
+        hipLaunchKernelGGL((preprocess_fwd_kernel<false, true>), dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
     else
         hipLaunchKernelGGL(preprocess_fwd_kernel<false>, dim3((p.P + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
