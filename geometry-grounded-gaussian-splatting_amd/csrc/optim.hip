@@ -178,10 +178,30 @@ __global__ void __launch_bounds__(256) normalize_rows_kernel(int n, int D, const
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float* r = x + (size_t)i * D;
+    float* o = out + (size_t)i * D;
+    if (D == 4 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+                    reinterpret_cast<uintptr_t>(gy)) & 15) == 0) {  // quaternions: one 16-B access each way
+        const float4 v = *reinterpret_cast<const float4*>(r);
+        const float len = sqrtf(((v.x * v.x + v.y * v.y) + v.z * v.z) + v.w * v.w), m = fmaxf(len, 1e-12f);
+        const float4 u = make_float4(v.x / m, v.y / m, v.z / m, v.w / m);
+        if (!backward) {
+            *reinterpret_cast<float4*>(o) = u;
+            return;
+        }
+        const float4 g = *reinterpret_cast<const float4*>(gy + (size_t)i * 4);
+        float4 d;
+        if (len > 1e-12f) {
+            const float dot = ((u.x * g.x + u.y * g.y) + u.z * g.z) + u.w * g.w;
+            d = make_float4((g.x - u.x * dot) / m, (g.y - u.y * dot) / m, (g.z - u.z * dot) / m, (g.w - u.w * dot) / m);
+        } else {
+            d = make_float4(g.x / m, g.y / m, g.z / m, g.w / m);
+        }
+        *reinterpret_cast<float4*>(o) = d;
+        return;
+    }
     float ss = 0.f;
     for (int k = 0; k < D; k++) ss += r[k] * r[k];
     const float len = sqrtf(ss), m = fmaxf(len, 1e-12f);
-    float* o = out + (size_t)i * D;
     if (!backward) {
         for (int k = 0; k < D; k++) o[k] = r[k] / m;
         return;

@@ -766,13 +766,28 @@ preprocess_bwd_kernel(PreprocessBwdArgs a) {
             const float d = c == 0 ? st_d0 : (c == 1 ? st_d1 : st_d2);
             return k < nsh ? Y[k] * d : 0.f;
         };
-        float4* row = reinterpret_cast<float4*>(stage + 48 * slot);
+        if (a.dL_dsh_rest) {  // the split layout: the wave's 45-float rest rows, then its 3-float DC rows
+            float* rest = stage + 45 * slot;
+            float* dc = stage + 45 * 64 + 3 * slot;
 #pragma unroll
-        for (int i = 0; i < 12; i++) row[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        wave_store_rows(a.dL_dsh + (size_t)wbase * 48, stage, n * 48, lane);
+            for (int e = 0; e < 3; e++) dc[e] = val(e);
+#pragma unroll
+            for (int e = 0; e < 45; e++) rest[e] = val(3 + e);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_store_rows(a.dL_dsh + (size_t)wbase * 3, stage + 45 * 64, n * 3, lane);
+            wave_store_rows(a.dL_dsh_rest + (size_t)wbase * 45, stage, n * 45, lane);
+        } else {
+            float4* row = reinterpret_cast<float4*>(stage + 48 * slot);
+#pragma unroll
+            for (int i = 0; i < 12; i++)
+                row[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_store_rows(a.dL_dsh + (size_t)wbase * 48, stage, n * 48, lane);
+        }
     }
 }
 
@@ -831,7 +846,7 @@ hipError_t launch_preprocess_bwd(const BwdParams& b, const GeomState& gs, const 
     // input rows it loads by 16-B LDS-DMA (a tensor that is a view at a 4-B offset takes the per-lane path)
     const int so = option(kOptPbwdStage);
     auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    const bool stage_ok = p.shs && !dc_rows && !b.dL_dsh_rest && p.SHM == 16 && (begin & 255) == 0 && al16(b.dL_dsh) &&
+    const bool stage_ok = p.shs && !dc_rows && (!b.dL_dsh_rest || al16(b.dL_dsh_rest)) && p.SHM == 16 && (begin & 255) == 0 && al16(b.dL_dsh) &&
                           (p.SGM == 0 || (p.SGM == kSG7 && p.SGD == kSG7 && al16(b.dL_dsg_color) &&
                                           al16(b.dL_dsg_sharpness) && al16(b.dL_dsg_axis) &&
                                           al16(p.sg_color) && al16(p.sg_sharpness) && al16(p.sg_axis)));
