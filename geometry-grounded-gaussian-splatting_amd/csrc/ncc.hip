@@ -11,10 +11,18 @@
 // One lane per pixel.  The pixels are the valid ones of a view in raster
 // order, so the 64 lanes of a wave read a 67 x 4-pixel strip of the
 // reference image and a similar warped strip of the neighbour image: the
-// 49 x (<= 4 + 4) gathers per pixel are served by L1/L2, and the kernel is
-// bound by its per-tap arithmetic (homography, bilinear weights, gradient
-// terms).  Divisions by the homogeneous coordinate are one v_rcp_f32 per tap
-// (the reference builds with --use_fast_math, warp-patch-ncc/setup.py:18).
+// 49 x (<= 4 + 4) gathers per pixel are served by L1/L2.  Divisions by the
+// homogeneous coordinate are one v_rcp_f32 per tap (the reference builds with
+// --use_fast_math, warp-patch-ncc/setup.py:18).
+// Round 5 (GSR_NCC_TAPS2): the taps' gathers are issued per group of 3-4 taps
+// before their arithmetic (the per-tap version waited on every tap's loads at
+// 2 waves per SIMD), the reference's per-tap division for K_r^-1 of the tap is
+// hoisted out of the rows, the homography-gradient dot product is folded to
+// five operations, the three gradient sums keep their y and z components per
+// row, and the margin test is taken on the extremes of the warps: ~60 VALU per
+// tap at 4 waves per SIMD (128 VGPRs; ncc.o is compiled without SLP
+// vectorisation, which packed the scalar chains at the cost of ~400 moves).
+// pm_terms_kernel at the e2e scene: 0.51-0.55 -> 0.21-0.24 ms.
 #include "gsr_kernels.h"
 
 namespace gsr {
@@ -44,6 +52,12 @@ __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b
 __device__ __forceinline__ f3 operator*(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
+#ifndef GSR_NCC_TAPS2
+#define GSR_NCC_TAPS2 1  // the folded tap loop (ncc_pixel); 0: the per-tap restatement
+#endif
+#ifndef GSR_NCC_WAVES
+#define GSR_NCC_WAVES 4  // waves per SIMD the NCC kernels are compiled for (<= 128 VGPRs)
+#endif
 constexpr int kNccRadius = 3;          // RADIUS of the reference's <3, true> instance
 constexpr float kNccHalfExtent = 1.5f;  // RADIUS * 0.5 (half-pixel steps)
 
@@ -81,6 +95,114 @@ __device__ __forceinline__ NccPix ncc_pixel(const NccArgs& a, int ux, int uy, fl
         f3 g_n = {0.f, 0.f, 0.f}, g_n2 = {0.f, 0.f, 0.f}, g_rn = {0.f, 0.f, 0.f};
         const float* Ir = a.image_r;
         const float* In = a.image_n;
+#if GSR_NCC_TAPS2
+        if (a.Wn < 3 || a.Hn < 3) {
+            ok = false;  // (no warp can lie inside the margin; the taps below assume two columns and rows)
+        } else {
+            // Per tap: the warp (un, vn) = H (u + du/2, v + dv/2, 1) / z, the bilinear sample c_n of the
+            // neighbour image there and its gradient s right, right = K_r^-1 (u + du/2, v + dv/2, 1), with
+            // s = left . aux folded to rz (dcx (kx - un kz) + dcy (ky - vn kz)).  The three gradient sums
+            // sum_taps w s right (w = 1, 2 c_n, c_r) keep x per tap and y, z per row (right.y is the
+            // row's, right.z = 1).  A warp inside the margin has u0 + 1 = ceil(nextafter(un)) (and
+            // likewise v), so the four taps are base, base + 1, base + Wn, base + Wn + 1; the margin
+            // test is taken once on the extremes of un and vn (their sum catches NaN).
+            const float kx = a.fx_n * aux.x + a.cx_n * aux.z, ky = a.fy_n * aux.y + a.cy_n * aux.z, kz = aux.z;
+            float rx[2 * kNccRadius + 1];
+#pragma unroll
+            for (int du = -kNccRadius; du <= kNccRadius; du++) rx[du + kNccRadius] = (ux + 0.5f * du - a.cx_r) / a.fx_r;
+            float umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY, fin = 0.f;
+            float X1 = 0.f, X2 = 0.f, X3 = 0.f, Y1 = 0.f, Y2 = 0.f, Y3 = 0.f, Z1 = 0.f, Z2 = 0.f, Z3 = 0.f;
+            const int Wn = a.Wn, Hn = a.Hn, Wr = a.Wr;
+            // taps du0..du1 of row dv: their warps and gathers first, then the arithmetic (one memory
+            // round trip per group of taps, not per tap)
+            auto taps = [&](int dv, const float* r0, const float* r1, const f3& H_uc_v, float& R1, float& R2,
+                            float& R3, auto odd_tag, auto lo_tag, auto hi_tag) {
+                constexpr bool odd_v = decltype(odd_tag)::value;
+                constexpr int du0 = decltype(lo_tag)::value, du1 = decltype(hi_tag)::value, n = du1 - du0 + 1;
+                float t_un[n], t_vn[n], t_rz[n], t_c[n][4], t_cr[n];
+#pragma unroll
+                for (int k = 0; k < n; k++) {
+                    const int du = du0 + k;
+                    const bool odd_u = (du & 1) != 0;
+                    const int o = du >> 1;
+                    // reference image at (u + du/2, v + dv/2) (the reference's line cache, its weights)
+                    float c_r = odd_u ? 0.5f * (r0[o] + r0[o + 1]) : r0[o];
+                    if constexpr (odd_v) c_r = odd_u ? 0.25f * ((r0[o] + r0[o + 1]) + (r1[o] + r1[o + 1]))
+                                                     : 0.5f * (r0[o] + r1[o]);
+                    t_cr[k] = c_r;
+                    const f3 H_uv = H_uc_v + H[0] * (0.5f * du);
+                    const float rz = __builtin_amdgcn_rcpf(H_uv.z);
+                    const float un = H_uv.x * rz, vn = H_uv.y * rz;
+                    t_un[k] = un;
+                    t_vn[k] = vn;
+                    t_rz[k] = rz;
+                    const int u0 = min(max((int)floorf(un), 0), Wn - 2), v0 = min(max((int)floorf(vn), 0), Hn - 2);
+                    const float* q = In + (v0 * Wn + u0);
+                    t_c[k][0] = q[0];
+                    t_c[k][1] = q[1];
+                    t_c[k][2] = q[Wn];
+                    t_c[k][3] = q[Wn + 1];
+                }
+#pragma unroll
+                for (int k = 0; k < n; k++) {
+                    const float c_r = t_cr[k], rz = t_rz[k], un = t_un[k], vn = t_vn[k];
+                    umin = fminf(umin, un);
+                    umax = fmaxf(umax, un);
+                    vmin = fminf(vmin, vn);
+                    vmax = fmaxf(vmax, vn);
+                    fin += un + vn;
+                    const float fu = floorf(un), fv = floorf(vn);
+                    const float c00n = t_c[k][0], c01n = t_c[k][1], c10n = t_c[k][2], c11n = t_c[k][3];
+                    const float wv0 = (fv + 1.f) - vn, wv1 = vn - fv, wu0 = (fu + 1.f) - un, wu1 = un - fu;
+                    const float c_n = wv0 * (wu0 * c00n + wu1 * c01n) + wv1 * (wu0 * c10n + wu1 * c11n);
+                    s_r += c_r;
+                    s_n += c_n;
+                    s_r2 += c_r * c_r;
+                    s_n2 += c_n * c_n;
+                    s_rn += c_r * c_n;
+                    const float dcx = wv0 * (c01n - c00n) + wv1 * (c11n - c10n);
+                    const float dcy = wu0 * (c10n - c00n) + wu1 * (c11n - c01n);
+                    const float s = rz * (dcx * (kx - un * kz) + dcy * (ky - vn * kz));
+                    const float s2 = s * c_n, s3 = s * c_r;
+                    const float x = rx[du0 + k + kNccRadius];
+                    R1 += s;
+                    R2 += s2;
+                    R3 += s3;
+                    X1 += x * s;
+                    X2 += x * s2;
+                    X3 += x * s3;
+                }
+            };
+            auto row = [&](int dv, auto odd_tag) {
+                const float dv_f = 0.5f * dv;
+                const float* r0 = Ir + (size_t)(uy + (dv >> 1)) * Wr + ux;
+                const float* r1 = r0 + Wr;
+                const f3 H_uc_v = H_uc + H[1] * dv_f;
+                const float right_y = (uy + dv_f - a.cy_r) / a.fy_r;
+                float R1 = 0.f, R2 = 0.f, R3 = 0.f;
+                taps(dv, r0, r1, H_uc_v, R1, R2, R3, odd_tag, std::integral_constant<int, -kNccRadius>{},
+                     std::integral_constant<int, 0>{});
+                taps(dv, r0, r1, H_uc_v, R1, R2, R3, odd_tag, std::integral_constant<int, 1>{},
+                     std::integral_constant<int, kNccRadius>{});
+                Y1 += right_y * R1;
+                Y2 += right_y * R2;
+                Y3 += right_y * R3;
+                Z1 += R1;
+                Z2 += R2;
+                Z3 += R3;
+            };
+#pragma unroll 1
+            for (int dv = -kNccRadius; dv <= kNccRadius; dv++) {
+                if (dv & 1) row(dv, std::true_type{});  // (uniform: a scalar branch)
+                else row(dv, std::false_type{});
+            }
+            ok = umin - kNccHalfExtent > 0 && umax + kNccHalfExtent < Wn - 1 && vmin - kNccHalfExtent > 0 &&
+                 vmax + kNccHalfExtent < Hn - 1 && fabsf(fin) < INFINITY;
+            g_n = {X1, Y1, Z1};
+            g_n2 = f3{X2, Y2, Z2} * 2.f;
+            g_rn = {X3, Y3, Z3};
+        }
+#else
         for (int dv = -kNccRadius; dv <= kNccRadius; dv++) {
             const float dv_f = 0.5f * dv;
             const bool odd_v = (dv & 1) != 0;
@@ -131,6 +253,7 @@ __device__ __forceinline__ NccPix ncc_pixel(const NccArgs& a, int ux, int uy, fl
                 g_rn = g_rn + ga * c_r;
             }
         }
+#endif
         constexpr float kInv = 1.f / 49.f;
         const float cross = s_rn - s_r * s_n * kInv;
         const float var_r = s_r2 - s_r * s_r * kInv;
@@ -150,7 +273,7 @@ __device__ __forceinline__ NccPix ncc_pixel(const NccArgs& a, int ux, int uy, fl
     return NccPix{ok, out_ncc, out_gd, out_gn};
 }
 
-__global__ void __launch_bounds__(256) ncc_kernel(NccArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_NCC_WAVES, 8))) ncc_kernel(NccArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
     const int ux = a.uvs[2 * idx], uy = a.uvs[2 * idx + 1];
@@ -274,7 +397,7 @@ __device__ __forceinline__ void pm_block_sums(float (&v)[4], float* out) {
     if (threadIdx.x < 4) out[threadIdx.x] = (s[0][threadIdx.x] + s[1][threadIdx.x]) + (s[2][threadIdx.x] + s[3][threadIdx.x]);
 }
 
-__global__ void __launch_bounds__(256) pm_terms_kernel(PmArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_NCC_WAVES, 8))) pm_terms_kernel(PmArgs a) {
     const int n = a.H * a.W;
     const int p = blockIdx.x * 256 + threadIdx.x;
     float sums[4] = {0.f, 0.f, 0.f, 0.f};
