@@ -459,15 +459,30 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
 #pragma unroll
                 for (int q = kAccNormal; q < kAccFields; q++) f[q] = 0.f;
             }
+#ifndef GSR_TIME_BWD_PROBE
+#define GSR_TIME_BWD_PROBE 0  // (timing builds only, gradients wrong: 1 = no reductions, 2 = no atomics)
+#endif
+#if GSR_TIME_BWD_PROBE == 1
+            float red = f[0];
+#pragma unroll
+            for (int q = 1; q < 16; q++) red = (lane & 15) == q ? f[q] : red;
+            red *= post_scale;
+            const float abs_red = fabs_sum;
+#else
             const float red = wave_transpose_reduce16(f) * post_scale;
             const float abs_red = wave_sum_dpp(fabs_sum);
+#endif
             // (wave-uniform: the record's address in scalar registers, each lane's field an offset)
             const uint32_t g = __builtin_amdgcn_readfirstlane(s_id[j]);
             // lanes 0, 4, .., 60 add the 16 fields of the record (one 64-B line, one atomic
             // instruction), lane 1 adds |dmean2D|
             const bool field_lane = (lane & 3) == 0 && (GEOM || (lane >> 2) < kAccNormal);
+#if GSR_TIME_BWD_PROBE == 2
+            if (field_lane && red == 1234.5f && abs_red == 1.f && g == 7u) a.acc[lane] = red;
+#else
             if (field_lane) atomicAdd(a.acc + (size_t)g * kAccFields + (lane >> 2), red);
             if (lane == 1) atomicAdd(a.acc_abs + g, abs_red);
+#endif
         }
     }
 }

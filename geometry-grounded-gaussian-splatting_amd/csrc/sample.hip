@@ -11,13 +11,20 @@
 // render_fwd.hip in SAMPLE mode; the Gaussian side reuses preprocess_fwd,
 // the binning and preprocess_bwd.
 //
-// Points are grouped per tile (stable radix sort on the tile id, as the
-// reference) and cut into chunks of 256 points, one 256-lane workgroup each
+// Points are grouped per tile and cut into chunks of 256 points, one 256-lane workgroup each
 // (the reference uses 512-point blocks, 2 points per thread: a point's result
 // does not depend on the grouping, every point stops at its own last
 // contributor).  No host synchronisation besides the forward's one: the
 // chunk count is derived on the device (sample_setup_kernel) and read
 // together with K.
+// The grouping (round 5, GSR_POINT_SCATTER): the reference sorts the points
+// by tile id (SortPairs, stable).  No result depends on the order of a tile's
+// points, so they are scattered instead: the per-tile counts the points
+// kernel already takes are scanned into the tile ranges (sample_setup) and
+// each wave reserves a run of its tile's range with one atomic per distinct
+// tile (sample_scatter_kernel) — one pass over 4 B per point instead of the
+// radix sort's histogram and two onesweep passes (62 + 16 us for 2.07M points
+// at the e2e scene).  Within a wave the points keep their order.
 #pragma clang fp contract(off)
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -27,6 +34,9 @@
 
 namespace gsr {
 
+#ifndef GSR_POINT_SCATTER
+#define GSR_POINT_SCATTER 1  // 0: the reference's stable sort by tile id (rocprim radix sort)
+#endif
 using PointSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                    rocprim::default_config, 0>;
 
@@ -37,6 +47,7 @@ static unsigned point_key_bits(uint32_t tiles) { return 32u - (unsigned)__builti
 
 size_t point_sort_temp_bytes(int PN, uint32_t tiles) {
     size_t bytes = 0;
+    if (GSR_POINT_SCATTER) return 0;
     (void)rocprim::radix_sort_pairs<PointSortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                                      rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr,
                                                      (size_t)PN, 0u, point_key_bits(tiles));
@@ -94,6 +105,7 @@ hipError_t launch_sample_points(const FwdParams& p, int PN, const float* points3
     hipLaunchKernelGGL(sample_points_kernel, dim3((PN + 255) / 256), dim3(256), 0, stream, PN, points3D, p.view,
                        p.proj, p.W, p.H, p.grid_x, p.grid_y, ps.xy, ps.t, pb.keys_unsorted, st.counts);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (GSR_POINT_SCATTER) return hipSuccess;  // (sample_scatter_kernel, after the setup's scan)
     size_t bytes = pb.sort_tmp_bytes;
     return rocprim::radix_sort_pairs<PointSortConfig>(pb.sort_tmp, bytes, pb.keys_unsorted, pb.keys,
                                                       rocprim::counting_iterator<uint32_t>(0), pb.pt_list,
@@ -167,12 +179,40 @@ __global__ void __launch_bounds__(1024)
     }
 }
 
+// Each point into its tile's range (GSR_POINT_SCATTER): a wave takes one run of
+// slots per distinct tile among its lanes from the end of that tile's range
+// (counts[t] counts down to 0), its lanes in lane order within the run.
+__global__ void __launch_bounds__(256)
+    sample_scatter_kernel(int PN, uint32_t tiles, const uint32_t* __restrict__ keys, uint32_t* __restrict__ counts,
+                          const uint2* __restrict__ pt_ranges, uint32_t* __restrict__ pt_list) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t t = idx < PN ? keys[idx] : tiles;
+    const uint32_t lane = threadIdx.x & 63;
+    bool pending = t < tiles;  // (culled points carry t = tiles: in no range)
+    for (unsigned long long pm = __ballot(pending); pm != 0ull; pm = __ballot(pending)) {
+        // (every lane stays in the loop: the leader is the first still-pending lane, read by lane index)
+        const uint32_t lead = (uint32_t)__builtin_amdgcn_readlane((int)t, __builtin_ctzll(pm));
+        const unsigned long long same = __ballot(pending && t == lead);
+        uint32_t base = 0u;
+        if (lane == (uint32_t)__builtin_ctzll(same)) base = atomicSub(&counts[lead], (uint32_t)__popcll(same));
+        // (the leader's lane id is wave-uniform, so the run's base is a lane read)
+        base = __shfl(base, __builtin_ctzll(same), 64);
+        if (pending && t == lead) {
+            const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+            pt_list[pt_ranges[t].x + base - (uint32_t)__popcll(same) + rank] = (uint32_t)idx;
+            pending = false;
+        }
+    }
+}
+
 hipError_t launch_sample_setup(int PN, uint32_t tiles, const PointBinState& pb, const SampleTiles& st,
                                hipStream_t stream) {
-    (void)PN;
-    (void)pb;
     hipLaunchKernelGGL(sample_setup_kernel, dim3(1), dim3(1024), 0, stream, tiles, st.counts, st.pt_ranges,
                        st.chunk_off, st.totals);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !GSR_POINT_SCATTER || PN == 0) return e;
+    hipLaunchKernelGGL(sample_scatter_kernel, dim3((PN + 255) / 256), dim3(256), 0, stream, PN, tiles,
+                       pb.keys_unsorted, st.counts, st.pt_ranges, pb.pt_list);
     return hipGetLastError();
 }
 
@@ -378,22 +418,31 @@ __global__ void __launch_bounds__(256) sample_bwd_kernel(SampleBwdArgs a) {
     }
 }
 
-// The same with two points per lane (GSR_SAMPLE_BWD_PAIRS): a 128-lane
-// workgroup per 256-point chunk, the lane's points p and p + 128 in the
-// halves of packed registers.  Per (wave, Gaussian) step the record reads,
-// the skip ballot, the transpose reduction and the atomic serve 128 points
-// instead of 64, and the per-point arithmetic runs as v_pk_* pairs; every
-// packed operation rounds as the scalar one, so alpha and the contribute
-// decisions stay bit-identical to the forward's.
+// The same with 2 NPR points per lane (GSR_SAMPLE_BWD_PAIRS): a workgroup of
+// 128 / NPR lanes per 256-point chunk, the lane's points in NPR packed pairs
+// (pair k: points lane + 2k L and lane + (2k + 1) L, L the lane count).  Per
+// (wave, Gaussian) step the record reads, the skip ballot, the transpose
+// reduction and the atomic serve 2 NPR points per lane instead of one, and
+// the per-point arithmetic runs as v_pk_* pairs; every packed operation
+// rounds as the scalar one, so alpha and the contribute decisions stay
+// bit-identical to the forward's.  NPR = 2 (round 5): one wave per chunk, as
+// render_bwd's one wave per tile.
 typedef float sf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ sf2 ssplat(float v) { return sf2{v, v}; }
 __device__ __forceinline__ sf2 ssel(bool ca, bool cb, sf2 x, sf2 y) { return sf2{ca ? x.x : y.x, cb ? x.y : y.y}; }
 
-constexpr int kSbLanes = kTilePixels / 2;
+#ifndef GSR_SAMPLE_BWD_NPR
+#define GSR_SAMPLE_BWD_NPR 2
+#endif
 
-__global__ void __launch_bounds__(kSbLanes) sample_bwd_pairs_kernel(SampleBwdArgs a) {
-    __shared__ float4 s_w0[kTilePixels], s_w1[kTilePixels], s_w2[kTilePixels];
-    __shared__ uint32_t s_id[kTilePixels];
+template <int NPR>
+__global__ void __launch_bounds__(kTilePixels / (2 * NPR)) sample_bwd_pairs_kernel(SampleBwdArgs a) {
+    constexpr int L = kTilePixels / (2 * NPR);  // lanes
+    constexpr int NQ = 2 * NPR;                 // points per lane
+    constexpr int B = kTilePixels / NPR;        // records per LDS batch (2 per lane; NPR = 2: 6.5 KB, 6 waves per SIMD)
+    constexpr int RL = B / L;
+    __shared__ float4 s_w0[B], s_w1[B], s_w2[B];
+    __shared__ uint32_t s_id[B];
 
     if (blockIdx.x >= a.totals[2]) return;  // uniform over the block
     const uint32_t chunk = a.chunk_order ? a.chunk_order[blockIdx.x] : xcd_remap(blockIdx.x, a.totals[2]);
@@ -404,14 +453,16 @@ __global__ void __launch_bounds__(kSbLanes) sample_bwd_pairs_kernel(SampleBwdArg
     const uint2 pr = a.pt_ranges[tile];
     const uint32_t base = pr.x + (chunk - a.chunk_off[tile]) * kTilePixels + tid;
 
-    // per-point seed (sample_backward.cu:138-158), one point per half
-    float px[2] = {0.f, 0.f}, py[2] = {0.f, 0.f}, md[2] = {0.f, 0.f}, dLD[2] = {0.f, 0.f}, dT[2] = {0.f, 0.f};
-    float gpx[2] = {0.f, 0.f}, gpy[2] = {0.f, 0.f};
-    uint32_t last[2] = {0u, 0u}, pid[2] = {0u, 0u};
-    bool in[2] = {false, false}, on[2] = {false, false}, cached[2] = {false, false};
+    // per-point seed (sample_backward.cu:138-158), point q at slot base + q L
+    float px[NQ], py[NQ], md[NQ], dLD[NQ], dT[NQ], gpx[NQ], gpy[NQ];
+    uint32_t last[NQ], pid[NQ];
+    bool in[NQ], on[NQ], cached[NQ];
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const uint32_t slot = base + q * kSbLanes;
+    for (int q = 0; q < NQ; q++) {
+        px[q] = py[q] = md[q] = dLD[q] = dT[q] = gpx[q] = gpy[q] = 0.f;
+        last[q] = pid[q] = 0u;
+        on[q] = cached[q] = false;
+        const uint32_t slot = base + q * L;
         in[q] = slot < pr.y;
         if (!in[q]) continue;
         pid[q] = a.pt_list[slot];
@@ -437,45 +488,64 @@ __global__ void __launch_bounds__(kSbLanes) sample_bwd_pairs_kernel(SampleBwdArg
         cached[q] = a.pt_cached[id] != 0;
         dT[q] = cached[q] ? a.pt_dT[id] : 0.f;
     }
-    const int rounds = (max_contrib + kTilePixels - 1) / kTilePixels;
+    const int rounds = (max_contrib + B - 1) / B;
+    // every list entry, then every record, requested before any is stored
     auto stage = [&](int i, bool ids) {
+        uint32_t g[RL];
+        float4 r[RL][3];
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int k = tid + h * kSbLanes;
-            const int c = i * kTilePixels + k;
-            if (c < max_contrib) {
-                const uint32_t g = a.point_list[range.x + c];
-                const Splat* sp = a.splats + g;
-                s_w0[k] = sp->w0;
-                s_w1[k] = sp->w1;
-                s_w2[k] = sp->w2;
-                if (ids) s_id[k] = g;
+        for (int h = 0; h < RL; h++) {
+            const int c = i * B + tid + h * L;
+            g[h] = c < max_contrib ? a.point_list[range.x + c] : 0u;
+        }
+#pragma unroll
+        for (int h = 0; h < RL; h++) {
+            const int c = i * B + tid + h * L;
+            const Splat* sp = a.splats + g[h];
+            const bool ok = c < max_contrib;
+            r[h][0] = ok ? sp->w0 : make_float4(0.f, 0.f, 0.f, 0.f);
+            r[h][1] = ok ? sp->w1 : make_float4(0.f, 0.f, 0.f, 0.f);
+            r[h][2] = ok ? sp->w2 : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int h = 0; h < RL; h++) {
+            const int k = tid + h * L;
+            if (i * B + k < max_contrib) {
+                s_w0[k] = r[h][0];
+                s_w1[k] = r[h][1];
+                s_w2[k] = r[h][2];
+                if (ids) s_id[k] = g[h];
             }
         }
     };
 
     // pre-pass dT/dt_m (sample_backward.cu:170-215) for points the forward did not cache
     {
-        const bool need0 = on[0] && !cached[0], need1 = on[1] && !cached[1];
-        const uint32_t wave_last = wave_max_u(max(need0 ? last[0] : 0u, need1 ? last[1] : 0u));
+        bool need[NQ];
+        uint32_t mine = 0u;
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            need[q] = on[q] && !cached[q];
+            mine = max(mine, need[q] ? last[q] : 0u);
+        }
+        const uint32_t wave_last = wave_max_u(mine);
         const bool block_needs = __syncthreads_or(wave_last != 0u);
         uint32_t c = 0;
         int toDo = max_contrib;
-        for (int i = 0; block_needs && i < rounds; i++, toDo -= kTilePixels) {
+        for (int i = 0; block_needs && i < rounds; i++, toDo -= B) {
             __syncthreads();
             stage(i, false);
             __syncthreads();
-            const int n = min(kTilePixels, toDo);
+            const int n = min(B, toDo);
             for (int j = 0; j < n && c < wave_last; j++) {
                 c++;
                 const float4 w0 = s_w0[j], w1 = s_w1[j], w2 = s_w2[j];
 #pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    const bool need = q ? need1 : need0;
+                for (int q = 0; q < NQ; q++) {
                     const float dx = w0.x - px[q], dy = w0.y - py[q];
                     const float power = splat_power(w0, w1, dx, dy);
                     const float alpha = fminf(0.99f, w1.y * __expf(power));
-                    if (!(need && c <= last[q] && !(power > 0.f) && !(alpha < 1.0f / 255.0f))) continue;
+                    if (!(need[q] && c <= last[q] && !(power > 0.f) && !(alpha < 1.0f / 255.0f))) continue;
                     const float t_peak = splat_tpeak(w1, w2, dx, dy);
                     const float t_delta = (md[q] - t_peak) * w2.y;
                     const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
@@ -484,89 +554,122 @@ __global__ void __launch_bounds__(kSbLanes) sample_bwd_pairs_kernel(SampleBwdArg
             }
         }
     }
-    const sf2 kappa = {on[0] ? dLD[0] / fmaxf(-dT[0], 1e-7f) : 0.f, on[1] ? dLD[1] / fmaxf(-dT[1], 1e-7f) : 0.f};
-    const uint32_t wave_last = wave_max_u(max(on[0] ? last[0] : 0u, on[1] ? last[1] : 0u));
-    const sf2 pixx = {px[0], px[1]}, pixy = {py[0], py[1]}, mDepth = {md[0], md[1]};
-    sf2 dpx = {gpx[0], gpx[1]}, dpy = {gpy[0], gpy[1]};
+    sf2 kappa[NPR], pixx[NPR], pixy[NPR], mDepth[NPR], dpx[NPR], dpy[NPR];
+    uint32_t mine = 0u;
+#pragma unroll
+    for (int k = 0; k < NPR; k++) {
+        const int q0 = 2 * k, q1 = 2 * k + 1;
+        kappa[k] = {on[q0] ? dLD[q0] / fmaxf(-dT[q0], 1e-7f) : 0.f, on[q1] ? dLD[q1] / fmaxf(-dT[q1], 1e-7f) : 0.f};
+        pixx[k] = {px[q0], px[q1]};
+        pixy[k] = {py[q0], py[q1]};
+        mDepth[k] = {md[q0], md[q1]};
+        dpx[k] = {gpx[q0], gpx[q1]};
+        dpy[k] = {gpy[q0], gpy[q1]};
+        mine = max(mine, max(on[q0] ? last[q0] : 0u, on[q1] ? last[q1] : 0u));
+    }
+    const uint32_t wave_last = wave_max_u(mine);
 
     // main pass, front to back (sample_backward.cu:228-354)
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
     constexpr float kLog2e = 1.44269504088896340736f;
     uint32_t contributor = 0;
     int toDo = max_contrib;
-    for (int i = 0; i < rounds; i++, toDo -= kTilePixels) {
+    for (int i = 0; i < rounds; i++, toDo -= B) {
         __syncthreads();
         stage(i, true);
         __syncthreads();
-        const int n = min(kTilePixels, toDo);
+        const int n = min(B, toDo);
         for (int j = 0; j < n && contributor < wave_last; j++) {
             contributor++;
             const float4 w0 = s_w0[j], w1 = s_w1[j];
-            sf2 dx = ssplat(w0.x) - pixx, dy = ssplat(w0.y) - pixy;
-            sf2 power;
-            {
+            sf2 dx[NPR], dy[NPR], G[NPR], og[NPR];
+            bool va[NPR], vb[NPR];
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < NPR; k++) {
+                dx[k] = ssplat(w0.x) - pixx[k];
+                dy[k] = ssplat(w0.y) - pixy[k];
+                sf2 power;
+                {
 #pragma clang fp contract(off)
-                const sf2 ax = (ssplat(w0.z) * dx) * dx;  // splat_power, per half
-                const sf2 qq = __builtin_elementwise_fma(ssplat(w1.x) * dy, dy, ax);
-                power = __builtin_elementwise_fma(ssplat(-0.5f), qq, -((ssplat(w0.w) * dx) * dy));
+                    const sf2 ax = (ssplat(w0.z) * dx[k]) * dx[k];  // splat_power, per half
+                    const sf2 qq = __builtin_elementwise_fma(ssplat(w1.x) * dy[k], dy[k], ax);
+                    power = __builtin_elementwise_fma(ssplat(-0.5f), qq, -((ssplat(w0.w) * dx[k]) * dy[k]));
+                }
+                const sf2 pe = power * ssplat(kLog2e);  // __expf(x) = v_exp_f32(x log2 e)
+                G[k] = sf2{__builtin_amdgcn_exp2f(pe.x), __builtin_amdgcn_exp2f(pe.y)};
+                og[k] = ssplat(w1.y) * G[k];
+                va[k] = on[2 * k] & (contributor <= last[2 * k]) & !(power.x > 0.f) & !(og[k].x < 1.0f / 255.0f);
+                vb[k] = on[2 * k + 1] & (contributor <= last[2 * k + 1]) & !(power.y > 0.f) &
+                        !(og[k].y < 1.0f / 255.0f);
+                any = any | va[k] | vb[k];
             }
-            const sf2 pe = power * ssplat(kLog2e);  // __expf(x) = v_exp_f32(x log2 e)
-            const sf2 G = {__builtin_amdgcn_exp2f(pe.x), __builtin_amdgcn_exp2f(pe.y)};
-            const sf2 og = ssplat(w1.y) * G;
-            const bool va = on[0] & (contributor <= last[0]) & !(power.x > 0.f) & !(og.x < 1.0f / 255.0f);
-            const bool vb = on[1] & (contributor <= last[1]) & !(power.y > 0.f) & !(og.y < 1.0f / 255.0f);
-            if (__ballot(va | vb) == 0ull) continue;  // wave-uniform skip (warp.any)
+            if (__ballot(any) == 0ull) continue;  // wave-uniform skip (warp.any)
             const float4 w2 = s_w2[j];
-            // (an invalid half: offsets 0 keep its terms finite, its gradient factors are zeroed below)
-            dx = ssel(va, vb, dx, ssplat(0.f));
-            dy = ssel(va, vb, dy, ssplat(0.f));
-            const sf2 alpha = {fminf(0.99f, og.x), fminf(0.99f, og.y)};
-            sf2 t_peak;
-            {
-#pragma clang fp contract(off)
-                t_peak = __builtin_elementwise_fma(ssplat(w1.w), dy, ssplat(w1.z) * dx) + ssplat(w2.x);
-            }
             const float rsig = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, w2.y)));
-            const sf2 md_tp = mDepth - t_peak;
-            const sf2 t_delta = md_tp * ssplat(rsig);
-            const sf2 ge = ((ssplat(-0.5f) * t_delta) * t_delta) * ssplat(kLog2e);
-            const sf2 G_exp = {__builtin_amdgcn_exp2f(ge.x), __builtin_amdgcn_exp2f(ge.y)};
-            const sf2 Gt = alpha * G_exp;
-            const sf2 omg = ssplat(1.f) - Gt, oma = ssplat(1.f) - alpha;
-            sf2 dL_dGt = (kappa * ssplat(0.25f)) * sf2{fast_rcp(omg.x), fast_rcp(omg.y)};
-            dL_dGt = ssel(md_tp.x > 0.f, md_tp.y > 0.f, dL_dGt, -dL_dGt);
-            dL_dGt = ssel(va && rsig > 0.f, vb && rsig > 0.f, dL_dGt, ssplat(0.f));
-            const sf2 kr = ssel(va && t_delta.x > 0.f, vb && t_delta.y > 0.f,
-                                ssplat(0.5f) * sf2{fast_rcp(oma.x), fast_rcp(oma.y)}, ssplat(0.f));
-            const sf2 dL_dopa = dL_dGt * G_exp - kappa * kr;
-            const sf2 dL_ddelta = -dL_dGt * Gt * t_delta;
-            const sf2 dL_drsig = dL_ddelta * md_tp;
-            const sf2 dL_dt = -dL_ddelta * ssplat(rsig);
-            const sf2 dL_dG = ssplat(w1.y) * dL_dopa;
-            const sf2 Gv = ssel(va, vb, G, ssplat(0.f));  // (power > 0 may have overflowed G)
-            const sf2 gdx = Gv * dx, gdy = Gv * dy;
-            const sf2 dG_ddelx = -gdx * ssplat(w0.z) - gdy * ssplat(w0.w);
-            const sf2 dG_ddely = -gdy * ssplat(w1.x) - gdx * ssplat(w0.w);
-            const sf2 dL_ddelx = dL_dG * dG_ddelx + dL_dt * ssplat(w1.z);
-            const sf2 dL_ddely = dL_dG * dG_ddely + dL_dt * ssplat(w1.w);
-            dpx -= dL_ddelx;
-            dpy -= dL_ddely;
-            const sf2 c0 = ssplat(-0.5f) * gdx * dL_dG, c2 = ssplat(-0.5f) * gdy * dL_dG;
-            const sf2 cx = c0 * dx, cy = c0 * dy, cz = c2 * dy, ops = Gv * dL_dopa;
-            const sf2 tx = dL_dt * dx, ty = dL_dt * dy;
+            sf2 Fmx, Fmy, Fcx, Fcy, Fcz, Fops, Ftx, Fty, Fdt, Fdr;
+#pragma unroll
+            for (int k = 0; k < NPR; k++) {
+                // (an invalid half: offsets 0 keep its terms finite, its gradient factors are zeroed below)
+                const sf2 dxk = ssel(va[k], vb[k], dx[k], ssplat(0.f));
+                const sf2 dyk = ssel(va[k], vb[k], dy[k], ssplat(0.f));
+                const sf2 alpha = {fminf(0.99f, og[k].x), fminf(0.99f, og[k].y)};
+                sf2 t_peak;
+                {
+#pragma clang fp contract(off)
+                    t_peak = __builtin_elementwise_fma(ssplat(w1.w), dyk, ssplat(w1.z) * dxk) + ssplat(w2.x);
+                }
+                const sf2 md_tp = mDepth[k] - t_peak;
+                const sf2 t_delta = md_tp * ssplat(rsig);
+                const sf2 ge = ((ssplat(-0.5f) * t_delta) * t_delta) * ssplat(kLog2e);
+                const sf2 G_exp = {__builtin_amdgcn_exp2f(ge.x), __builtin_amdgcn_exp2f(ge.y)};
+                const sf2 Gt = alpha * G_exp;
+                const sf2 omg = ssplat(1.f) - Gt, oma = ssplat(1.f) - alpha;
+                sf2 dL_dGt = (kappa[k] * ssplat(0.25f)) * sf2{fast_rcp(omg.x), fast_rcp(omg.y)};
+                dL_dGt = ssel(md_tp.x > 0.f, md_tp.y > 0.f, dL_dGt, -dL_dGt);
+                dL_dGt = ssel(va[k] && rsig > 0.f, vb[k] && rsig > 0.f, dL_dGt, ssplat(0.f));
+                const sf2 kr = ssel(va[k] && t_delta.x > 0.f, vb[k] && t_delta.y > 0.f,
+                                    ssplat(0.5f) * sf2{fast_rcp(oma.x), fast_rcp(oma.y)}, ssplat(0.f));
+                const sf2 dL_dopa = dL_dGt * G_exp - kappa[k] * kr;
+                const sf2 dL_ddelta = -dL_dGt * Gt * t_delta;
+                const sf2 dL_drsig = dL_ddelta * md_tp;
+                const sf2 dL_dt = -dL_ddelta * ssplat(rsig);
+                const sf2 dL_dG = ssplat(w1.y) * dL_dopa;
+                const sf2 Gv = ssel(va[k], vb[k], G[k], ssplat(0.f));  // (power > 0 may have overflowed G)
+                const sf2 gdx = Gv * dxk, gdy = Gv * dyk;
+                const sf2 dG_ddelx = -gdx * ssplat(w0.z) - gdy * ssplat(w0.w);
+                const sf2 dG_ddely = -gdy * ssplat(w1.x) - gdx * ssplat(w0.w);
+                const sf2 dL_ddelx = dL_dG * dG_ddelx + dL_dt * ssplat(w1.z);
+                const sf2 dL_ddely = dL_dG * dG_ddely + dL_dt * ssplat(w1.w);
+                dpx[k] -= dL_ddelx;
+                dpy[k] -= dL_ddely;
+                const sf2 c0 = ssplat(-0.5f) * gdx * dL_dG, c2 = ssplat(-0.5f) * gdy * dL_dG;
+                const sf2 cx = c0 * dxk, cy = c0 * dyk, cz = c2 * dyk, ops = Gv * dL_dopa;
+                const sf2 tx = dL_dt * dxk, ty = dL_dt * dyk;
+                Fmx = k ? Fmx + dL_ddelx : dL_ddelx;
+                Fmy = k ? Fmy + dL_ddely : dL_ddely;
+                Fcx = k ? Fcx + cx : cx;
+                Fcy = k ? Fcy + cy : cy;
+                Fcz = k ? Fcz + cz : cz;
+                Fops = k ? Fops + ops : ops;
+                Ftx = k ? Ftx + tx : tx;
+                Fty = k ? Fty + ty : ty;
+                Fdt = k ? Fdt + dL_dt : dL_dt;
+                Fdr = k ? Fdr + dL_drsig : dL_drsig;
+            }
             float f[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) f[q] = 0.f;
-            f[kAccMean2D + 0] = (dL_ddelx.x + dL_ddelx.y) * ddelx_dx;
-            f[kAccMean2D + 1] = (dL_ddely.x + dL_ddely.y) * ddely_dy;
-            f[kAccConic + 0] = cx.x + cx.y;
-            f[kAccConic + 1] = cy.x + cy.y;
-            f[kAccConic + 2] = cz.x + cz.y;
-            f[kAccConic + 3] = ops.x + ops.y;
-            f[kAccPlane + 0] = tx.x + tx.y;
-            f[kAccPlane + 1] = ty.x + ty.y;
-            f[kAccPlane + 2] = dL_dt.x + dL_dt.y;
-            f[kAccPlane + 3] = dL_drsig.x + dL_drsig.y;
+            f[kAccMean2D + 0] = (Fmx.x + Fmx.y) * ddelx_dx;
+            f[kAccMean2D + 1] = (Fmy.x + Fmy.y) * ddely_dy;
+            f[kAccConic + 0] = Fcx.x + Fcx.y;
+            f[kAccConic + 1] = Fcy.x + Fcy.y;
+            f[kAccConic + 2] = Fcz.x + Fcz.y;
+            f[kAccConic + 3] = Fops.x + Fops.y;
+            f[kAccPlane + 0] = Ftx.x + Ftx.y;
+            f[kAccPlane + 1] = Fty.x + Fty.y;
+            f[kAccPlane + 2] = Fdt.x + Fdt.y;
+            f[kAccPlane + 3] = Fdr.x + Fdr.y;
             const float red = wave_transpose_reduce16(f);
             // lanes 4k hold field k; colour (0-2) and normal (9-11) are zero here
             const int field = lane >> 2;
@@ -578,12 +681,13 @@ __global__ void __launch_bounds__(kSbLanes) sample_bwd_pairs_kernel(SampleBwdArg
     }
     const float* Pm = a.proj;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < NQ; q++) {
         if (!in[q]) continue;
         // dL/dpoints2D in NDC units, then the projection backward
         // (preprocessPointsCUDA bwd, sample_backward.cu:42-75)
         const uint32_t id = pid[q];
-        const float gx2 = (q ? dpx.y : dpx.x) * ddelx_dx, gy2 = (q ? dpy.y : dpy.x) * ddely_dy;
+        const sf2 gxp = dpx[q >> 1], gyp = dpy[q >> 1];
+        const float gx2 = ((q & 1) ? gxp.y : gxp.x) * ddelx_dx, gy2 = ((q & 1) ? gyp.y : gyp.x) * ddely_dy;
         const float mx = a.points3D[3 * id], my = a.points3D[3 * id + 1], mz = a.points3D[3 * id + 2];
         const float hw = Pm[3] * mx + Pm[7] * my + Pm[11] * mz + Pm[15];
         const float m_w = 1.0f / (hw + 0.0000001f);
@@ -633,8 +737,9 @@ hipError_t launch_sample_bwd(const SampleBwdParams& b, const GeomState& gs, cons
     a.acc = ws.acc;
     a.chunk_order = ws.tile_order;
     const uint32_t bound = sample_chunk_bound(b.PN, tiles);
+    constexpr int kNpr = GSR_SAMPLE_BWD_NPR;
     if (GSR_SAMPLE_BWD_PAIRS)
-        hipLaunchKernelGGL(sample_bwd_pairs_kernel, dim3(bound), dim3(kSbLanes), 0, stream, a);
+        hipLaunchKernelGGL(sample_bwd_pairs_kernel<kNpr>, dim3(bound), dim3(kTilePixels / (2 * kNpr)), 0, stream, a);
     else
         hipLaunchKernelGGL(sample_bwd_kernel, dim3(bound), dim3(kTilePixels), 0, stream, a);
     return hipGetLastError();

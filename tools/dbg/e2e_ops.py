@@ -21,7 +21,7 @@ ts, view, nearest = gsr_train.synthetic_training_setup(P, W, H, 3, 0, device="cu
 for _ in range(5):
     ts.step(view, nearest)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=True) as prof:
     ts.step(view, nearest)
     torch.cuda.synchronize()
 keys = ("aten::zeros", "aten::zero_", "aten::fill_", "aten::add", "aten::add_", "aten::mul", "aten::copy_", "aten::cat",
@@ -35,3 +35,11 @@ for e in rows[:60]:
     print(f"{e.key:22s} {e.count:5d} {e.device_time_total:10.1f}  {str(e.input_shapes)[:150]}")
 print()
 print(prof.key_averages().table(sort_by="device_time_total", row_limit=40, max_name_column_width=60))
+print()
+# where the glue comes from: python call sites of the fills and elementwise ops
+for e in sorted(prof.key_averages(group_by_stack_n=6), key=lambda e: -e.device_time_total):
+    if e.key in ("aten::zero_", "aten::mul", "aten::add_", "aten::add", "aten::sub", "aten::where", "aten::mean",
+                 "aten::sum", "aten::clone", "aten::div", "aten::neg", "aten::abs") and e.device_time_total > 4:
+        print(f"{e.key:14s} {e.count:3d} {e.device_time_total:8.1f} us")
+        for fr in e.stack[:6]:
+            print("      ", fr)
