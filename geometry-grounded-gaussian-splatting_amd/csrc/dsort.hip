@@ -11,11 +11,11 @@
 // and one kernel per 8-bit digit, and the look-back state of all four passes
 // is zeroed once.
 //
-// Pass kernel (one 1024-lane workgroup per tile of 8192 keys, 12288 above 2M
+// Pass kernel (one 1024-lane workgroup per tile of 6144 keys, 12288 above 2M
 // keys — 16 waves per CU
 // for latency; tiles numbered in the order workgroups start, by an atomic
 // counter, so every look-back target is running or done):
-//  1. each wave ranks its 512 / 768 keys (8 / 12 per lane, position i*64 + lane) by
+//  1. each wave ranks its 384 / 768 keys (6 / 12 per lane, position i*64 + lane) by
 //     digit with 8 ballots per item (peer lanes), a per-wave digit counter in
 //     LDS giving the stable rank among the wave's earlier items;
 //  2. per digit (lanes 0-255): the wave counts combined into the tile's
@@ -40,7 +40,7 @@ namespace gsr {
 #define GSR_DS_THREADS 1024
 #endif
 #ifndef GSR_DS_ITEMS
-#define GSR_DS_ITEMS 8  // keys per lane up to kDsBigP keys (round 3; was 4: C5 depth order 0.294 -> 0.222 ms)
+#define GSR_DS_ITEMS 6  // keys per lane up to kDsBigP keys (round 3: 4 -> 8, C5 depth order 0.294 -> 0.222 ms; round 5: 8 -> 6 at C3, 123 -> 163 tiles for 256 CUs: 0.0805 -> 0.0774 ms; 4: 0.083, 512 lanes x 8: 0.088)
 #endif
 #ifndef GSR_DS_ITEMS_BIG
 #define GSR_DS_ITEMS_BIG 12  // above kDsBigP (C5: 0.221 -> 0.188 ms; 12 at C3: 0.080 -> 0.088, 16: 0.207 / 0.098)
