@@ -280,10 +280,14 @@ class _SampleDepth(torch.autograd.Function):
         ctx.num_duplicated_tiles = num_duplicated_tiles
         ctx.save_for_backward(points3D, means3D, opacities, scales, rotations, cov3D_precomp, inside, geomBuffer,
                               binningBuffer, pointBuffer, pointBinningBuffer, tileBuffer, duplicatedTileBuffer)
+        # (no zero-filled gradient for the bool `inside`, nor for unused points: None reaches backward)
+        ctx.set_materialize_grads(False)
         return camera_points, inside
 
     @staticmethod
     def backward(ctx, grad_camera_points, grad_inside):
+        if grad_camera_points is None:
+            return None, None, None, None, None, None, None
         s = ctx.raster_settings
         (points3D, means3D, opacities, scales, rotations, cov3D_precomp, inside, geomBuffer, binningBuffer,
          pointBuffer, pointBinningBuffer, tileBuffer, duplicatedTileBuffer) = ctx.saved_tensors

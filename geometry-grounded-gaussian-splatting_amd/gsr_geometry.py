@@ -44,10 +44,13 @@ class _DepthToNormal(torch.autograd.Function):
         ctx.save_for_backward(d)
         ctx.cam = (H, W, Fx, Fy, Cx, Cy)
         ctx.mark_non_differentiable(valid)
+        ctx.set_materialize_grads(False)  # (no zero-filled gradient for `valid`)
         return normal, valid
 
     @staticmethod
     def backward(ctx, g_normal, g_valid):
+        if g_normal is None:
+            return None, None, None, None, None, None, None
         (d,) = ctx.saved_tensors
         H, W, Fx, Fy, Cx, Cy = ctx.cam
         L = _lib()

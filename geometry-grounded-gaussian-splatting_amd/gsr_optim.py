@@ -68,10 +68,13 @@ class _ScaleOpacity(torch.autograd.Function):
             _rc(L, L.gsr_scale_opacity_3d_filter(P, s.data_ptr(), o.data_ptr(), f.data_ptr(), scales.data_ptr(),
                                                  op.data_ptr(), _C._stream(s.device)))
         ctx.save_for_backward(s, o, f)
+        ctx.set_materialize_grads(False)  # (a caller of one getter leaves the other output's gradient None)
         return scales, op
 
     @staticmethod
     def backward(ctx, g_scales, g_op):
+        if g_scales is None and g_op is None:
+            return None, None, None
         L = _lib()
         s, o, f = ctx.saved_tensors
         ds, do = torch.empty_like(s), torch.empty_like(o)
