@@ -214,9 +214,6 @@ constexpr uint32_t kLastMask = 0x3fffffffu, kLoEv = 1u << 30, kHiEv = 1u << 31; 
 #endif
 constexpr int kRefineWalks = GSR_REFINE_WALKS;
 // SAMPLE mode: Halley walks from the query point's own distance (GSR_SAMPLE_GUESS, in the kernel)
-#ifndef GSR_COMPOSITE_PAIRS
-#define GSR_COMPOSITE_PAIRS 0  // the composite's footprint terms two entries at a time (packed)
-#endif
 #ifndef GSR_SAMPLE_GUESS
 #define GSR_SAMPLE_GUESS 1
 #endif
@@ -512,7 +509,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
     // One list entry g (0-based) at this lane, the reference's per-pixel loop
     // body: w0, w1 are the record's footprint words, w2f / w3f fetch the rest
     // only when the lane blends.
-    // (step_pre: the footprint terms dx, dy, power and alpha already evaluated, GSR_COMPOSITE_PAIRS)
+    // (step_pre: with the footprint terms dx, dy, power and alpha evaluated by the caller)
     auto step_pre = [&](const float4& w0, const float4& w1, auto&& w2f, auto&& w3f, int g, float dx, float dy,
                         float power, float alpha) {
         if constexpr (STATS) {
@@ -611,28 +608,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                     const uint32_t v = wave_or_dpp(wbits);
                     if ((tid & 63) == 0 && v) atomicOr(&s_union[word], v);
                 }
-            }
-        } else if (GSR_COMPOSITE_PAIRS) {
-            // two entries' footprint terms at once, in the halves of packed registers (splat_power's
-            // roundings; __expf(x) = v_exp_f32(x log2 e)), then the two steps in order
-            const f32x2 px2 = {pixx, pixx}, py2 = {pixy, pixy};
-            for (int j = 0; !done && j < n; j += 2) {
-                const int j2 = min(j + 1, n - 1);
-                const float4 a0 = s_w0[j], a1 = s_w1[j], b0 = s_w0[j2], b1 = s_w1[j2];
-                const f32x2 dx = f32x2{a0.x, b0.x} - px2, dy = f32x2{a0.y, b0.y} - py2;
-                f32x2 power;
-                {
-#pragma clang fp contract(off)
-                    const f32x2 q = __builtin_elementwise_fma(f32x2{a1.x, b1.x} * dy, dy, (f32x2{a0.z, b0.z} * dx) * dx);
-                    power = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f}, q, -((f32x2{a0.w, b0.w} * dx) * dy));
-                }
-                const f32x2 pe = power * f32x2{kLog2e, kLog2e};
-                const f32x2 og = f32x2{a1.y, b1.y} * f32x2{__builtin_amdgcn_exp2f(pe.x), __builtin_amdgcn_exp2f(pe.y)};
-                step_pre(a0, a1, [&] { return s_w2[j]; }, [&] { return s_w3[j]; }, i * kBatch + j, dx.x, dy.x, power.x,
-                         fminf(0.99f, og.x));
-                if (!done && j + 1 < n)
-                    step_pre(b0, b1, [&] { return s_w2[j + 1]; }, [&] { return s_w3[j + 1]; }, i * kBatch + j + 1, dx.y,
-                             dy.y, power.y, fminf(0.99f, og.y));
             }
         } else {
             for (int j = 0; !done && j < n; j++)
