@@ -97,6 +97,7 @@ class TrainGaussians(torch.nn.Module):
         self.register_buffer("filter_3D", raw.filter_3D.detach().clone())
         self.active_sh_degree, self.active_sg_degree = sh_degree, sg_degree
         self.torch_getters = False
+        self._step_cache = None  # (TrainStep: the fused getters' outputs shared by render and sample_depth)
         n = raw.xyz.shape[0]
         dev = raw.xyz.device
         self.max_radii2D = torch.zeros(n, device=dev)
@@ -114,6 +115,23 @@ class TrainGaussians(torch.nn.Module):
                                    eps=1e-15)
 
     # ---- getters (gaussian_model.py:146-212) ----
+    def _cached(self, key, fn):
+        # within a TrainStep (begin_step .. end_step) each fused getter runs once: render and the PatchMatch
+        # sample_depth take the same outputs (the parameters do not change between them), so one kernel
+        # each way instead of two or three, and the two consumers' gradients meet at the outputs
+        c = self._step_cache
+        if c is None:
+            return fn()
+        if key not in c:
+            c[key] = fn()
+        return c[key]
+
+    def begin_step(self):
+        self._step_cache = {}
+
+    def end_step(self):
+        self._step_cache = None
+
     @property
     def get_xyz(self):
         return self._xyz
@@ -127,13 +145,13 @@ class TrainGaussians(torch.nn.Module):
     @property
     def get_scaling_with_3D_filter(self):
         if not self.torch_getters:
-            return scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D)[0]
+            return self._cached("so", lambda: scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D))[0]
         return torch.sqrt(torch.square(self.get_scaling) + torch.square(self.filter_3D))
 
     @property
     def get_opacity_with_3D_filter(self):
         if not self.torch_getters:
-            return scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D)[1]
+            return self._cached("so", lambda: scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D))[1]
         sq = torch.square(self.get_scaling)
         coef = torch.sqrt(sq.prod(dim=1) / (sq + torch.square(self.filter_3D)).prod(dim=1))
         return torch.sigmoid(self._opacity) * coef[..., None]
@@ -141,7 +159,7 @@ class TrainGaussians(torch.nn.Module):
     @property
     def get_scaling_n_opacity_with_3D_filter(self):
         if not self.torch_getters:
-            return scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D)
+            return self._cached("so", lambda: scaling_n_opacity_with_3D_filter(self._scaling, self._opacity, self.filter_3D))
         sq = torch.square(self.get_scaling)
         after = sq + torch.square(self.filter_3D)
         coef = sq.prod(dim=1).sqrt() * after.prod(dim=1).rsqrt()
@@ -150,7 +168,7 @@ class TrainGaussians(torch.nn.Module):
     @property
     def get_rotation(self):
         if not self.torch_getters:
-            return normalize_rows(self._rotation)
+            return self._cached("rot", lambda: normalize_rows(self._rotation))
         return F.normalize(self._rotation)
 
     @property
@@ -309,12 +327,19 @@ class TrainStep:
         g = self.g
         self.stamps = []
         self._mark()
+        g.begin_step()
+        try:
+            return self._step(g, view, nearest)
+        finally:
+            g.end_step()
+
+    def _step(self, g, view, nearest):
         pkg = render(view, g, self.pipe, self.bg, self.kernel_size, require_depth=True)
         image = pkg["render"]
         self._mark()
         depth_normal, valid_points = depth_to_normal(view, pkg["median_depth"])
         err = 1 - torch.linalg.vecdot(pkg["normal"], depth_normal, dim=0)
-        normal_loss = torch.where(valid_points.squeeze(), err, torch.zeros_like(err)).mean()
+        normal_loss = torch.where(valid_points.squeeze(), err, 0.0).mean()  # (a scalar 0: no zero-filled map)
         self._mark()
         ncc_loss, geo_loss = self.patchmatch(g, pkg, view, nearest, self.kernel_size, self.pipe)
         self._mark()
