@@ -221,6 +221,10 @@ constexpr int kRefineWalks = GSR_REFINE_WALKS;
 #define GSR_SAMPLE_WALKS 5
 #endif
 constexpr int kSampleWalks = GSR_SAMPLE_WALKS;
+#ifndef GSR_SAMPLE_NO_ENDS
+#define GSR_SAMPLE_NO_ENDS 0
+#endif
+constexpr bool kSampleNoEnds = GSR_SAMPLE_NO_ENDS;
 #ifndef GSR_REFINE_TOL
 #define GSR_REFINE_TOL 3e-5f
 #endif
@@ -1672,10 +1676,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 const float lo_w = win_lo(), hi_w = win_hi();
                 const float e0 = lo_w, e8 = __builtin_fmaf((hi_w - lo_w) * (1.f / (float)kSplit), (float)kSplit, lo_w);
                 const float t0 = fminf(fmaxf(pt_t, e0), e8);
-                const Refine r = halley(own_src, 1, pin, t0, e0, e8, true, e0, e8, pin, kSampleWalks, fmaxf(t0, 1.f),
-                                        false, false);
+                // (GSR_SAMPLE_NO_ENDS: every walk the packed two-contributor walk, no window-end samples; a
+                // root found well inside the first window implies the reference's in_range test, T being
+                // non-increasing — the render path's phase-2 argument — and one near or past an end is left
+                // to the passes, which decide in_range with their own samples)
+                const Refine r = halley(own_src, 1, pin, t0, e0, e8, !kSampleNoEnds, e0, e8, pin, kSampleWalks,
+                                        fmaxf(t0, 1.f), false, false);
                 in_range = r.in_range;
                 refined = r.refined;
+                if (kSampleNoEnds && refined) {
+                    const float margin = 1e-4f * fmaxf(r.t_ref, 1.f);
+                    refined = r.t_ref > e0 + margin && r.t_ref < e8 - margin;
+                }
                 t_ref = r.t_ref;
                 ref_t = r.ref_t;
                 ref_D = r.ref_D;
