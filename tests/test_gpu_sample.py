@@ -178,6 +178,29 @@ def test_sample_points_on_tile_borders():
     _run(c, pts)
 
 
+def test_sample_points_crowded_tiles():
+    """Most points in two tiles (several 256-point chunks each, whole waves of
+    one tile: the scatter's per-wave runs), culled points interleaved (behind
+    the camera: key = tiles, in no range) and a point count that is not a
+    multiple of 256: the grouping is order-free, every point's result and the
+    gradients as the oracle's."""
+    c = Hh.small_case(P=800, W=96, H=64, seed=9, log_scale=math.log(0.05))
+    g = torch.Generator().manual_seed(21)
+    n = 3333
+    W, H = c["W"], c["H"]
+    tile_x = torch.where(torch.rand(n, generator=g) < 0.5, 1.0, 3.0)
+    px = tile_x * 16.0 + torch.rand(n, generator=g) * 15.0
+    py = 16.0 + torch.rand(n, generator=g) * 15.0
+    z = torch.rand(n, generator=g) * 2.5 + 1.5
+    z = torch.where(torch.rand(n, generator=g) < 0.1, -z, z)  # (behind the camera: culled)
+    fx, fy = W / (2 * c["tanx"]), H / (2 * c["tany"])
+    cam_pts = torch.stack([(px - (W - 1) / 2) / fx * z.abs(), (py - (H - 1) / 2) / fy * z.abs(), z], 1)
+    V = c["cam"].world_view_transform
+    pts = ((cam_pts - V[3, :3]) @ torch.linalg.inv(V[:3, :3])).float().contiguous()
+    out, o = _run(c, pts)
+    assert 0 < o["num_points"] < n
+
+
 def test_sample_tile_borders_ragged_grid():
     """The sample pad at tile borders, and a ragged grid."""
     c = Hh.small_case(P=800, W=96, H=64, seed=9, log_scale=math.log(0.05))
