@@ -467,7 +467,7 @@ int gsr_set_option(int opt, int value) {
 }
 
 
-int gsr_abi_version(void) { return 19; }
+int gsr_abi_version(void) { return 20; }
 
 int gsr_backward_chunk_size(int P, int chunks) {
     if (P < 0 || chunks < 1) return -1;
@@ -738,8 +738,8 @@ int gsr_rasterize_backward_ex2(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, 
         return fail(GSR_ERR_ARGS, "missing SG gradients");
     if (chunks < 1) return fail(GSR_ERR_ARGS, "chunks must be >= 1");
     if (dc_rows && !shs) return fail(GSR_ERR_ARGS, "dc_rows needs the SH colour path");
-    if (shs_rest && (!shs || SHM < 2 || !dL_dsh_rest || dc_rows))
-        return fail(GSR_ERR_ARGS, "split SH rows need the DC rows, SHM >= 2, both gradients and no dc_rows");
+    if (shs_rest && (!shs || SHM < 2 || !dL_dsh_rest))
+        return fail(GSR_ERR_ARGS, "split SH rows need the DC rows, SHM >= 2 and both gradients");
     b.f.shs_rest = shs_rest;
     b.dL_dsh_rest = dL_dsh_rest;
     b.R = R;
@@ -1181,9 +1181,10 @@ int gsr_view_color_grads_chunked(int P, int sh_degree, int SHM, int sg_degree, i
                                  const float* gathered, const float* campos, const float* means3D,
                                  const float* sg_axis, const float* sg_sharpness, const float* sg_color,
                                  float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness, float* dL_dsg_color,
-                                 void* stream_ptr) {
+                                 float* dL_dsh_rest, void* stream_ptr) {
     if (P < 0 || n_views < 1 || chunk < 1 || sh_degree < 0 || sh_degree > 3 ||
-        SHM < (sh_degree + 1) * (sh_degree + 1) || SGM < 0 || sg_degree < 0 || sg_degree > 7 || sg_degree > SGM)
+        SHM < (sh_degree + 1) * (sh_degree + 1) || SGM < 0 || sg_degree < 0 || sg_degree > 7 || sg_degree > SGM ||
+        (dL_dsh_rest && SHM < 2))
         return fail(GSR_ERR_ARGS, "view colour grads: invalid arguments");
     if (P > 0 && (!gathered || !campos || !means3D || !dL_dsh ||
                   (SGM > 0 && (!dL_dsg_axis || !dL_dsg_sharpness || !dL_dsg_color)) ||
@@ -1191,7 +1192,7 @@ int gsr_view_color_grads_chunked(int P, int sh_degree, int SHM, int sg_degree, i
         return fail(GSR_ERR_ARGS, "view colour grads: missing buffer");
     hipError_t e = launch_view_color_grads(P, sh_degree, SHM, sg_degree, SGM, n_views, gathered, means3D, sg_axis,
                                            sg_sharpness, sg_color, dL_dsh, dL_dsg_axis, dL_dsg_sharpness,
-                                           dL_dsg_color, (hipStream_t)stream_ptr, chunk, campos);
+                                           dL_dsg_color, (hipStream_t)stream_ptr, chunk, campos, dL_dsh_rest);
     return e == hipSuccess ? GSR_OK : fail(GSR_ERR_HIP, "view colour grads", e);
 }
 

@@ -155,7 +155,7 @@ hipError_t launch_view_color_grads(int P, int D, int SHM, int SGD, int SGM, int 
                                    const float* means3D, const float* sg_axis, const float* sg_sharpness,
                                    const float* sg_color, float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness,
                                    float* dL_dsg_color, hipStream_t stream, int chunk = 0,
-                                   const float* campos = nullptr);
+                                   const float* campos = nullptr, float* dL_dsh_rest = nullptr);
 hipError_t launch_densify_stats(int P, const float* vgrad, const int* radii, float* max_radii2D, float* accum,
                                 float* accum_abs, float* denom, hipStream_t stream);
 

@@ -41,6 +41,7 @@ struct ViewColorArgs {
     float* dL_dsg_color;
     int chunk;
     const float* campos;  // [n_views][4] when chunk > 0
+    float* dL_dsh_rest;   // split SH layout: dL_dsh is the DC rows [P][1][3], these the rest [P][SHM - 1][3]
 };
 
 constexpr int kMaxSG = 7;
@@ -125,7 +126,15 @@ __global__ void __launch_bounds__(256) view_color_grads_kernel(ViewColorArgs a) 
             }
         }
     }
-    if (a.dL_dsh) {
+    if (a.dL_dsh && a.dL_dsh_rest) {  // (the split layout: GaussianModel's features_dc / features_rest)
+        float* dc = a.dL_dsh + (size_t)idx * 3;
+        float* rest = a.dL_dsh_rest + (size_t)idx * (a.SHM - 1) * 3;
+        dc[0] = dsh[0], dc[1] = dsh[1], dc[2] = dsh[2];
+#pragma unroll
+        for (int e = 3; e < 48; e++)
+            if (e < 3 * a.SHM) rest[e - 3] = dsh[e];
+        for (int e = 48; e < 3 * a.SHM; e++) rest[e - 3] = 0.f;
+    } else if (a.dL_dsh) {
         float* out = a.dL_dsh + (size_t)idx * a.SHM * 3;
         if (sh_rows_vec4(out, a.SHM)) {
             float4* q = reinterpret_cast<float4*>(out);
@@ -160,10 +169,11 @@ __global__ void __launch_bounds__(256) view_color_grads_kernel(ViewColorArgs a) 
 hipError_t launch_view_color_grads(int P, int D, int SHM, int SGD, int SGM, int n_views, const float* gathered,
                                    const float* means3D, const float* sg_axis, const float* sg_sharpness,
                                    const float* sg_color, float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness,
-                                   float* dL_dsg_color, hipStream_t stream, int chunk, const float* campos) {
+                                   float* dL_dsg_color, hipStream_t stream, int chunk, const float* campos,
+                                   float* dL_dsh_rest) {
     if (P == 0) return hipSuccess;
     ViewColorArgs a{P, D, SHM, SGD, SGM, n_views, gathered, means3D, sg_axis, sg_sharpness, sg_color,
-                    dL_dsh, dL_dsg_axis, dL_dsg_sharpness, dL_dsg_color, chunk, campos};
+                    dL_dsh, dL_dsg_axis, dL_dsg_sharpness, dL_dsg_color, chunk, campos, dL_dsh_rest};
     hipLaunchKernelGGL(view_color_grads_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }

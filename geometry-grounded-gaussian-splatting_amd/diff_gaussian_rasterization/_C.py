@@ -44,7 +44,7 @@ class AdamGroup(ctypes.Structure):
 
 
 # include/gsr.h ABI these bindings are written for (gsr_abi_version)
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 
 def _load():
@@ -96,7 +96,7 @@ def _load():
     L.gsr_view_color_grads.restype = i
     L.gsr_view_color_grads.argtypes = [i] * 6 + [vp] * 10
     L.gsr_view_color_grads_chunked.restype = i
-    L.gsr_view_color_grads_chunked.argtypes = [i] * 7 + [vp] * 11
+    L.gsr_view_color_grads_chunked.argtypes = [i] * 7 + [vp] * 12
     L.gsr_backward_chunk_size.restype = i
     L.gsr_backward_chunk_size.argtypes = [i, i]
     L.gsr_mark_visible.restype = i
@@ -392,8 +392,6 @@ def rasterize_gaussians_backward(background, means3D, colors, opacity, scales, r
     SHM = sh.size(1) if sh is not None and sh.size(0) != 0 else 0
     SGM = sg_color.size(1) if sg_color is not None and sg_color.size(0) != 0 else 0
     rest = _split_rest(sh, sh_rest, P)
-    if rest is not None and exchange is not None:
-        raise RuntimeError("gsr: the split SH layout and an in-backward view exchange do not combine")
     dev = means3D.device
     fopt = dict(dtype=torch.float32, device=dev)
     alloc = torch.zeros if P == 0 else torch.empty  # the kernels overwrite every element
@@ -632,18 +630,24 @@ def densify_stats(viewspace_grad, radii, max_radii2D, accum, accum_abs, denom) -
 
 def view_color_grads_chunked(gathered, campos, n_views: int, chunk: int, means3D, sh_degree: int, dL_dsh,
                              sg_degree: int = 0, sg_axis=None, sg_sharpness=None, sg_color=None, dL_dsg_axis=None,
-                             dL_dsg_sharpness=None, dL_dsg_color=None) -> None:
+                             dL_dsg_sharpness=None, dL_dsg_color=None, dL_dsh_rest=None) -> None:
     """gsr_view_color_grads_chunked: view_color_grads for the range-by-range
     gathered layout (include/gsr.h): gathered [n_views * P * 3] DC rows in
-    ranges of `chunk` Gaussians, campos [n_views, 4]."""
+    ranges of `chunk` Gaussians, campos [n_views, 4].  With `dL_dsh_rest` (the
+    split SH layout) dL_dsh is the DC rows [P, 1, 3] and dL_dsh_rest the rest
+    [P, SHM - 1, 3]."""
     L = _load()
     P = means3D.shape[0]
-    SHM = dL_dsh.shape[1]
+    SHM = dL_dsh.shape[1] if dL_dsh_rest is None else 1 + dL_dsh_rest.shape[1]
     SGM = dL_dsg_color.shape[1] if dL_dsg_color is not None and dL_dsg_color.numel() else 0
     if gathered.numel() != n_views * P * 3 or campos.numel() != 4 * n_views or chunk < 1:
         raise RuntimeError("gsr view_color_grads_chunked: `gathered` must hold n_views * 3 P floats, `campos` "
                            "n_views * 4, chunk >= 1")
-    want = {"means3D": (means3D, (P, 3)), "dL_dsh": (dL_dsh, (P, SHM, 3))}
+    want = {"means3D": (means3D, (P, 3)), "dL_dsh": (dL_dsh, (P, SHM, 3) if dL_dsh_rest is None else (P, 1, 3))}
+    if dL_dsh_rest is not None:
+        if SHM < 2:
+            raise RuntimeError("gsr view_color_grads_chunked: the split SH layout needs SHM >= 2")
+        want["dL_dsh_rest"] = (dL_dsh_rest, (P, SHM - 1, 3))
     if SGM:
         want.update(dL_dsg_axis=(dL_dsg_axis, (P, SGM, 3)), dL_dsg_sharpness=(dL_dsg_sharpness, (P, SGM)),
                     dL_dsg_color=(dL_dsg_color, (P, SGM, 3)))
@@ -661,7 +665,7 @@ def view_color_grads_chunked(gathered, campos, n_views: int, chunk: int, means3D
         _check(L.gsr_view_color_grads_chunked(P, int(sh_degree), SHM, int(sg_degree), SGM, int(n_views), int(chunk),
                                               _ptr(gathered), _ptr(campos), _ptr(means3D), p(sg_axis),
                                               p(sg_sharpness), p(sg_color), _ptr(dL_dsh), p(dL_dsg_axis),
-                                              p(dL_dsg_sharpness), p(dL_dsg_color), _stream(dev)))
+                                              p(dL_dsg_sharpness), p(dL_dsg_color), p(dL_dsh_rest), _stream(dev)))
 
 
 def view_color_grads(gathered, n_views: int, means3D, sh_degree: int, dL_dsh, sg_degree: int = 0, sg_axis=None,

@@ -295,11 +295,21 @@ class OverlappedViewGrads:
 
     Failure: a rank whose backward fails part-way posts its remaining
     ranges on NaN rows (no peer blocks) and re-raises.  Every backward ends
-    with one more tiny all-reduce (MAX) of a failure flag on every rank, read
-    back by the host, so the PEERS raise too ("a peer rank's rasterizer
-    backward failed") instead of handing NaN-summed gradients to the
-    optimizer.  That read is the exchange's one host synchronisation per
-    backward, after its last collective.
+    with one more tiny all-reduce (MAX) of a failure flag on every rank, so
+    the PEERS raise too ("a peer rank's rasterizer backward failed").  When
+    they raise is `sync_check`'s choice:
+      * False (the default for device tensors): the flag is copied to pinned
+        host memory behind an event and read at the next `begin()` (the next
+        rasterizer backward) or by an explicit `check()` — no host
+        synchronisation per backward, so the host keeps queueing the rest of
+        the backward and the optimizer step while the GPU works.  A training
+        loop that must never apply a step with a failed peer calls `check()`
+        before `optimizer.step()` (one wait on an event the GPU has long
+        passed by then, since the step's gradients are complete);
+      * True (the default for host tensors, where the read costs nothing):
+        `finish()` reads the flag and raises in the same backward, at the
+        price of one host synchronisation per backward after its last
+        collective.
 
     Semantics: each rasterizer backward exchanges its own gradients, so
     several renders per step and gradient accumulation sum correctly (the
@@ -310,9 +320,12 @@ class OverlappedViewGrads:
     signature as _C.view_color_grads_chunked; CPU tests only).
     """
 
-    def __init__(self, group: Optional[dist.ProcessGroup] = None, chunks: int = 4, expand=None):
+    def __init__(self, group: Optional[dist.ProcessGroup] = None, chunks: int = 4, expand=None,
+                 sync_check: Optional[bool] = None):
         self.group = group
+        self.sync_check = sync_check
         self._status = None  # one float per backward: MAX over the ranks of "this rank's backward failed"
+        self._pending = None  # (pinned host copy of the flag, event) of the last backward, read by check()
         self.chunks = max(1, int(chunks))
         self.world = dist.get_world_size(group)
         if expand is None:
@@ -360,9 +373,25 @@ class OverlappedViewGrads:
         from diff_gaussian_rasterization import _C
         return _C.backward_chunk_size(P, self.chunks)
 
+    def check(self) -> None:
+        """Raise if the last backward's failure flag (MAX over the ranks) is
+        set: a peer rank's rasterizer backward failed and the summed
+        gradients of that step are invalid.  Waits only for the event behind
+        the flag's copy (the last collective of that backward)."""
+        pending, self._pending = self._pending, None
+        if pending is None:
+            return
+        flag, event = pending
+        if event is not None:
+            event.synchronize()
+        if float(flag[0]) > 0.0:
+            raise RuntimeError("OverlappedViewGrads: a peer rank's rasterizer backward failed; this step's summed "
+                               "gradients are invalid (NaN in that rank's ranges)")
+
     def begin(self, campos: torch.Tensor, P: int, scales_path: bool, sh_path: bool) -> None:
         if self._active:  # a backward that neither finished nor failed cleanly: settle its collectives first
             self.abort()
+        self.check()  # (the previous backward's deferred failure flag)
         self._works = []
         self._P, self._scales, self._sh = P, scales_path, sh_path
         self._cs = self.chunk_size(P) if P else 1
@@ -402,7 +431,7 @@ class OverlappedViewGrads:
             raise RuntimeError(f"OverlappedViewGrads: backward range [{b}, {e}) does not follow the range layout "
                                f"(next {self._next}, size {self._cs}, P {self._P})")
         (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dsg_axis, dsg_sharpness, dsg_color, dscales,
-         drotations) = grads
+         drotations) = grads[:11]
         rows = [dmeans3D[b:e], dopacity[b:e]]
         rows += [dscales[b:e], drotations[b:e]] if self._scales else [dcov3D[b:e]]
         if not self._sh:
@@ -465,6 +494,23 @@ class OverlappedViewGrads:
                         w.wait()
                     except Exception:  # noqa: BLE001 - already failing; the original error is what is raised
                         pass
+                if not self._sync():  # deferred: this rank's next begin() raises as its peers' do (lockstep)
+                    self._defer_flag()
+
+    def _sync(self) -> bool:
+        return self.sync_check if self.sync_check is not None else not self._status.is_cuda
+
+    def _defer_flag(self) -> None:
+        """The deferred check: the all-reduced flag copied behind the
+        backward's last collective, read by check() / the next begin()."""
+        if self._status.is_cuda:
+            flag = torch.empty(1, dtype=torch.float32, pin_memory=True)
+            flag.copy_(self._status, non_blocking=True)
+            event = torch.cuda.Event()
+            event.record()
+            self._pending = (flag, event)
+        else:
+            self._pending = (self._status.clone(), None)
 
     def _post_status(self, failed: bool) -> None:
         """The backward's last collective, posted by every rank exactly once
@@ -477,6 +523,7 @@ class OverlappedViewGrads:
         self._works.append(dist.all_reduce(self._status, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
 
     def finish(self, grads, means3D, sg_axis, sg_sharpness, sg_color, sh_degree: int, sg_degree: int) -> None:
+        """`grads`: the backward's 11 gradients (+ dsh_rest, the split SH layout)."""
         if self._next != self._P:
             msg = f"OverlappedViewGrads: the backward's ranges covered [0, {self._next}) of {self._P} Gaussians"
             self.abort()
@@ -486,17 +533,20 @@ class OverlappedViewGrads:
         for w in self._works:
             w.wait()  # (RCCL: the backward's stream waits for the collective)
         self._works = []
-        if float(self._status) > 0.0:  # host read of the flag: every rank learns that one failed
-            raise RuntimeError("OverlappedViewGrads: a peer rank's rasterizer backward failed; this step's summed "
-                               "gradients are invalid (NaN in that rank's ranges)")
+        if self._sync():
+            self._pending = (self._status, None)
+            self.check()  # host read of the flag: every rank learns that one failed
+        else:
+            self._defer_flag()
         if not self._sh or self._P == 0:
             return
         (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dsg_axis, dsg_sharpness, dsg_color, dscales,
-         drotations) = grads
+         drotations) = grads[:11]
+        kw = {} if len(grads) < 12 else {"dL_dsh_rest": grads[11]}  # (the split SH layout)
         sg = [None if t is None or not t.numel() else t.detach() for t in (sg_axis, sg_sharpness, sg_color)]
         self.expand(self._gathered, self._campos_all.view(self.world, 4), self.world, self._cs,
                     means3D.detach(), sh_degree, dsh, sg_degree, *sg,
-                    *[None if t is None or not t.numel() else t for t in (dsg_axis, dsg_sharpness, dsg_color)])
+                    *[None if t is None or not t.numel() else t for t in (dsg_axis, dsg_sharpness, dsg_color)], **kw)
 
     def verify_replicas(self, params: Iterable[torch.Tensor]) -> None:
         """Opt-in check after a training step's whole backward: every rank's

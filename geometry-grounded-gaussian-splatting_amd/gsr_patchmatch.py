@@ -108,7 +108,8 @@ class _Terms(torch.autograd.Function):
         ctx.save_for_backward(md_c, n_c, p_c, ins, w, flags, gd, gn, out)
         ctx.consts = consts
         ctx.shapes = (md.shape, normal.shape, pin.shape)
-        return out[0], out[1]
+        # (copies: `out` is saved for the backward, so the caller may change the returned losses in place)
+        return out[0].clone(), out[1].clone()
 
     @staticmethod
     def backward(ctx, g_geo, g_ncc):
@@ -154,7 +155,16 @@ class _Consts:
 
 def patchmatch_fused(gaussians, render_pkg, view, nearest, kernel_size, pipe):
     """(ncc_loss, geo_loss) of PatchMatch.__call__ (utils/loss_utils.py:140-267)
-    for `view` against `nearest`, as gsr_train.patchmatch, on the fused kernels."""
+    for `view` against `nearest`, as gsr_train.patchmatch, on the fused kernels.
+
+    No nearest camera: the reference's two [1]-shaped zeros (loss_utils.py:141-142).
+    An empty geometric or NCC mask gives 0-dim zeros where the reference returns
+    [1]-shaped ones (loss_utils.py:223-224, 264-265): telling them apart would
+    need the mask count on the host, i.e. a synchronisation per iteration; the
+    value and its broadcast into the total loss are the same."""
+    if nearest is None:
+        z = lambda: torch.zeros(1, dtype=torch.float32, device=render_pkg["median_depth"].device)  # noqa: E731
+        return z(), z()
     md = render_pkg["median_depth"]
     intr = (float(view.Fx), float(view.Fy), float(view.Cx), float(view.Cy))
     with torch.no_grad():

@@ -290,6 +290,9 @@ def patchmatch(gaussians, render_pkg, view, nearest, kernel_size, pipe):
     (ncc * weights)[ncc_mask]) are taken as masked sums (`masked_mean`), so the
     only host synchronisation left is the valid-pixel count warp_patch_ncc
     needs (tests/test_gpu_train.py checks both forms agree)."""
+    if nearest is None:  # loss_utils.py:141-142
+        z = lambda: torch.zeros(1, dtype=torch.float32, device=render_pkg["median_depth"].device)  # noqa: E731
+        return z(), z()
     t = patchmatch_terms(gaussians, render_pkg, view, nearest, kernel_size, pipe)
     # The reference returns (0, 0) when no pixel passes d_mask (loss_utils.py:223-224) and its NCC mean is
     # over a non-empty set otherwise; the mean of an empty set would be NaN, so both means take empty=0.

@@ -162,7 +162,8 @@ int gsr_rasterize_backward_ex(gsr_alloc_fn geom_bwd_alloc, void* geom_bwd_ctx, i
  * they are: `shs` is then the DC rows [P][3] and `shs_rest` the rest
  * [P][SHM-1][3] (SHM counts all coefficients, as before); the backward writes
  * dL_dsh [P][3] and dL_dsh_rest [P][SHM-1][3].  NULL shs_rest is exactly
- * the _ex call.  Not combined with dc_rows (the overlapped exchange).
+ * the _ex call.  With dc_rows (the overlapped exchange, ABI 20) neither SH
+ * gradient tensor is written: gsr_view_color_grads_chunked rebuilds both.
  */
 int gsr_rasterize_forward_ex2(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
                               gsr_alloc_fn image_alloc, void* image_ctx, gsr_alloc_fn tile_alloc, void* tile_ctx,
@@ -366,12 +367,15 @@ int gsr_densify_stats(int P, const float* vgrad, const int* radii, float* max_ra
  * range by range: the Gaussians in ranges of `chunk` (the last shorter);
  * range [b, b + len) occupies gathered[3 n_views b, 3 n_views (b + len)) as
  * [n_views][len][3] DC rows; the camera centres are campos [n_views][4].
+ * dL_dsh_rest (ABI 20; NULL: the one-tensor layout): the split SH layout of
+ * gsr_rasterize_backward_ex2 — dL_dsh is then the DC rows [P, 1, 3] and
+ * dL_dsh_rest the other SHM - 1 rows [P, SHM - 1, 3].
  */
 int gsr_view_color_grads_chunked(int P, int sh_degree, int SHM, int sg_degree, int SGM, int n_views, int chunk,
                                  const float* gathered, const float* campos, const float* means3D,
                                  const float* sg_axis, const float* sg_sharpness, const float* sg_color,
                                  float* dL_dsh, float* dL_dsg_axis, float* dL_dsg_sharpness, float* dL_dsg_color,
-                                 void* stream);
+                                 float* dL_dsh_rest, void* stream);
 
 int gsr_view_color_grads(int P, int sh_degree, int SHM, int sg_degree, int SGM, int n_views, const float* gathered,
                          const float* means3D, const float* sg_axis, const float* sg_sharpness, const float* sg_color,

@@ -223,7 +223,7 @@ def test_library_exports_header_symbols():
     for n in names:
         assert hasattr(lib, n), n
     lib.gsr_abi_version.restype = ctypes.c_int
-    assert lib.gsr_abi_version() == _C.ABI_VERSION == 19
+    assert lib.gsr_abi_version() == _C.ABI_VERSION == 20
     lib.gsr_stage_name.restype = ctypes.c_char_p
     assert lib.gsr_stage_name(5) == b"render_fwd"
 

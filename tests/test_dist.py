@@ -12,6 +12,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+import pytest
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
@@ -278,7 +280,7 @@ def _overlap_grads(P, seed):
             torch.zeros(P, 0, 3), torch.zeros(P, 0), torch.zeros(P, 0, 3), r(P, 3), r(P, 4))
 
 
-def _error_worker(rank, world, port, outdir):
+def _error_worker(rank, world, port, outdir, sync_check=None):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "geometry-grounded-gaussian-splatting_amd"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -292,7 +294,7 @@ def _error_worker(rank, world, port, outdir):
                 raise ValueError("injected failure in range [8, 16)")
             super().on_chunk(b, e, grads)
 
-    ex = Failing(chunks=4, expand=_expand_chunked_ref)
+    ex = Failing(chunks=4, expand=_expand_chunked_ref, sync_check=sync_check)
     ex.chunk_size = lambda P_: 8
     grads = _overlap_grads(P, seed=rank)
     mine = [t.clone() for t in grads]
@@ -309,6 +311,15 @@ def _error_worker(rank, world, port, outdir):
         raised = str(e)
     out = {"raised": raised, "works_left": len(ex._works), "active": ex._active,
            "means3D": grads[3], "mine": mine[3]}
+    if sync_check is False:  # deferred: the flag is read by the next begin() (or check()), before any collective
+        out["raised_in_backward"] = raised
+        try:
+            ex.begin(torch.zeros(3), P, True, True)
+            out["raised"] = None
+            ex.abort()
+        except RuntimeError as e:
+            out["raised"] = str(e) if raised is None else raised
+        out["active_after_begin"] = ex._active
     # the next backward runs normally after the failed one: the group is still in lockstep
     ex2 = OverlappedViewGrads(chunks=4, expand=_expand_chunked_ref)
     ex2.chunk_size = lambda P_: 8
@@ -325,7 +336,8 @@ def _error_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def test_overlapped_exchange_failure_keeps_ranks_in_lockstep(tmp_path):
+@pytest.mark.parametrize("sync_check", [None, False])
+def test_overlapped_exchange_failure_keeps_ranks_in_lockstep(tmp_path, sync_check):
     """A range whose exchange raises on one rank: that rank still
     posts every remaining range's collectives — on NaN rows — waits for all of
     its works and re-raises; the peer's backward completes its collectives (no
@@ -333,12 +345,15 @@ def test_overlapped_exchange_failure_keeps_ranks_in_lockstep(tmp_path):
     the end of every backward), so no rank hands NaN-summed gradients to its
     optimizer; the next step runs normally on both."""
     port = _free_port()
-    mp.start_processes(_error_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_error_worker, args=(2, port, str(tmp_path), sync_check), nprocs=2, join=True,
+                       start_method="spawn")
     e0 = torch.load(tmp_path / "e0.pt", weights_only=True)
     e1 = torch.load(tmp_path / "e1.pt", weights_only=True)
     assert e0["raised"] == "injected failure in range [8, 16)"
     assert e1["raised"] is not None and "a peer rank's rasterizer backward failed" in e1["raised"]
     assert e0["works_left"] == 0 and not e0["active"] and not e1["active"]
+    if sync_check is False:  # deferred (ADVICE r5): the peer's backward returns; its next begin() raises
+        assert e1["raised_in_backward"] is None and not e1["active_after_begin"]
     m1 = e1["means3D"]
     torch.testing.assert_close(m1[:8], e0["mine"][:8] + e1["mine"][:8])  # posted before the failure: summed
     assert torch.isnan(m1[8:]).all()  # the failed rank's remaining ranges: NaN, not silently one view

@@ -343,12 +343,26 @@ def _checksum(t: torch.Tensor) -> int:
     return int((bits * w).sum())
 
 
+def _range_sums(t: torch.Tensor, ranges) -> torch.Tensor:
+    """[n_ranges, 2] float64: the sum and the absolute sum of t's rows in each
+    Gaussian range (queued on the stream, no host synchronisation)."""
+    return torch.stack([torch.stack([t[b:e].double().sum(), t[b:e].double().abs().sum()]) for b, e in ranges])
+
+
 def _full_rank_worker(rank, world, port, outdir, P, sg_degree, views, forms, chunks):
     """One rank of the view-parallel step at full workload (bench.py's N > 1
     step): its own 1080p orbit view of the shared scene, forward
     + backward through the HIP rasterizer, then each exchange form on fresh
     parameters; the float64 sum over the ranks of the plain per-view
-    gradients is the yardstick, formed in float64 by an all-reduce."""
+    gradients is the yardstick, formed in float64 by an all-reduce.
+
+    Self-diagnosing: per Gaussian range of the overlapped form,
+    every tensor's error against the yardstick, and the range sums of what
+    this rank posted (taken right after each range's collectives are posted,
+    so the posting itself is not delayed) beside the same sums of its plain
+    gradients — _run_full_ranks prints them on failure, which tells a wrong
+    kernel output on one rank (posted != plain there) from a wrong transport
+    (the posted sums add up to something other than the result)."""
     import json
     import math
     import sys
@@ -394,6 +408,11 @@ def _full_rank_worker(rank, world, port, outdir, P, sg_degree, views, forms, chu
         return {k: (t.grad if t.grad is not None else torch.zeros_like(t)) for k, t in ps.items()}, n_vis
 
     plain, n_vis = step(fresh())
+    from diff_gaussian_rasterization import _C as _gsr_C
+    cs_ = _gsr_C.backward_chunk_size(P, chunks)
+    ranges = [(b, min(P, b + cs_)) for b in range(0, P, cs_)]
+    dkeys = ["means3D", "opacities", "scales", "rotations", "shs"]
+    plain_sums = {k: _range_sums(plain[k] if k != "shs" else plain[k][:, 0], ranges).cpu().tolist() for k in dkeys}
     want = {}
     for k in keys:  # the yardstick: sum over the views in float64
         w = plain[k].double()
@@ -405,7 +424,19 @@ def _full_rank_worker(rank, world, port, outdir, P, sg_degree, views, forms, chu
     for form in forms:
         ps = fresh()
         if form == "overlap":
-            with OverlappedViewGrads(chunks=chunks):
+            ex = OverlappedViewGrads(chunks=chunks)
+            posted = []
+            orig_on_chunk = ex.on_chunk
+
+            def on_chunk(b, e, grads, ex=ex, orig=orig_on_chunk, posted=posted):
+                orig(b, e, grads)
+                g11 = grads[:11]
+                rows = {"means3D": g11[3], "opacities": g11[2], "scales": g11[9], "rotations": g11[10]}
+                sums = {k: _range_sums(v, [(b, e)])[0] for k, v in rows.items()}
+                sums["shs"] = _range_sums(ex._dc.view(-1, 3), [(b, e)])[0]  # the DC rows all-gathered
+                posted.append(sums)
+            ex.on_chunk = on_chunk
+            with ex:
                 got, _ = step(ps)
         elif form == "factored":
             ex = FactoredViewGrads(ps["means3D"], ps["opacities"], ps["scales"], ps["rotations"], ps["shs"],
@@ -429,6 +460,15 @@ def _full_rank_worker(rank, world, port, outdir, P, sg_degree, views, forms, chu
             dist.all_reduce(cs, op=dist.ReduceOp.MAX)  # max and -min over the ranks
             out[k] = {"rel_l2": err, "finite": bool(torch.isfinite(a).all()),
                       "replicas_identical": int(cs[0]) == -int(cs[1])}
+            if k in dkeys:  # per range: error, the result's range sums
+                a2 = a if k != "shs" else a[:, 0]
+                w2 = want[k] if k != "shs" else want[k][:, 0]
+                out[k]["ranges"] = [float((a2[b:e].double() - w2[b:e]).norm() / w2[b:e].norm().clamp_min(1e-30))
+                                    for b, e in ranges]
+                out[k]["got_sums"] = _range_sums(a2, ranges).cpu().tolist()
+        if form == "overlap":
+            out["_posted"] = {k: [p[k].cpu().tolist() for p in posted] for k in dkeys}
+            out["_plain"] = plain_sums
         res["forms"][form] = out
         del got, ps
     res["seconds"] = round(time.time() - t_start, 1)
@@ -437,6 +477,30 @@ def _full_rank_worker(rank, world, port, outdir, P, sg_degree, views, forms, chu
     print(f"[rank {rank}] done in {res['seconds']} s", flush=True)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _print_overlap_diagnosis(rs) -> None:
+    """On a failure: per range and tensor of the overlapped form, the error
+    against the yardstick; each rank's posted range sums against its plain
+    gradients' (a rank whose kernel output was wrong); and the posted sums
+    over the ranks against the result's (a transport that lost rows)."""
+    for form, d0 in rs[0]["forms"].items():
+        for k, v in d0.items():
+            if k.startswith("_") or "ranges" not in v:
+                continue
+            print(f"[diag] {form} {k}: per-range rel L2 " + " ".join(f"{x:.2e}" for x in v["ranges"]))
+    if "overlap" not in rs[0]["forms"]:
+        return
+    for k in rs[0]["forms"]["overlap"]["_posted"]:
+        n_ranges = len(rs[0]["forms"]["overlap"]["_posted"][k])
+        for i in range(n_ranges):
+            posted = [r["forms"]["overlap"]["_posted"][k][i] for r in rs]
+            plain = [r["forms"]["overlap"]["_plain"][k][i] for r in rs]
+            got = rs[0]["forms"]["overlap"][k]["got_sums"][i]
+            rel = [abs(p[0] - q[0]) / max(q[1], 1e-30) for p, q in zip(posted, plain)]
+            tot = sum(p[0] for p in posted)
+            print(f"[diag] overlap {k} range {i}: posted-vs-plain per rank " + " ".join(f"{x:.1e}" for x in rel)
+                  + f"; sum of posted {tot:.6e} vs result {got[0]:.6e} (abs-sum scale {got[1]:.3e})")
 
 
 def _run_full_ranks(tmp_path, world, P, sg_degree, views, forms, chunks=4):
@@ -451,12 +515,19 @@ def _run_full_ranks(tmp_path, world, P, sg_degree, views, forms, chunks=4):
     mp.start_processes(_full_rank_worker, args=(world, port, str(tmp_path), P, sg_degree, views, forms, chunks),
                        nprocs=world, join=True, start_method="spawn")
     rs = [json.load(open(tmp_path / f"full{r}.json")) for r in range(world)]
+    bad = any(not v["finite"] or not v["replicas_identical"] or v["rel_l2"] > 1e-5
+              for r in rs for d in r["forms"].values() for k, v in d.items() if not k.startswith("_"))
+    if bad:
+        _print_overlap_diagnosis(rs)
     for r in rs:
         print(f"rank {r['rank']}: {r['visible']} visible Gaussians, {r['seconds']} s, "
-              + ", ".join(f"{f}: max rel L2 {max(v['rel_l2'] for v in d.values()):.2e}" for f, d in r["forms"].items()))
+              + ", ".join(f"{f}: max rel L2 {max(v['rel_l2'] for k, v in d.items() if not k.startswith('_')):.2e}"
+                          for f, d in r["forms"].items()))
         assert r["visible"] > 0.3 * P, r["visible"]  # every view sees a large part of the scene
         for form, d in r["forms"].items():
             for k, v in d.items():
+                if k.startswith("_"):
+                    continue
                 assert v["finite"], (r["rank"], form, k)
                 assert v["replicas_identical"], (r["rank"], form, k)  # bit-identical on every rank
                 assert v["rel_l2"] <= 1e-5, (r["rank"], form, k, v["rel_l2"])
@@ -484,3 +555,96 @@ def test_c5_two_ranks_full_workload(tmp_path):
     overlapped (7 ranges) and factored exchanges against the float64 sum of
     the two views' plain gradients (bit-identical replicas, rel. L2 <= 1e-5)."""
     _run_full_ranks(tmp_path, 2, 5_000_000, 7, 8, ["overlap", "factored"], chunks=7)
+
+
+@pytest.mark.timeout(900)
+def test_c5_eight_ranks_full_workload(tmp_path):
+    """C5's 8-GPU leg (BASELINE.json configs[4]) at its workload, rehearsed
+    as 8 ranks sharing cuda:0 over gloo: 5M Gaussians with
+    SH 3 + SG 7 at 1920x1080, 8 orbit views — the 8-view range-major DC-row
+    gather (8 x 5M x 12 B) and 8 replicas of the SG-7 state — for the
+    overlapped (7 ranges) and factored exchanges against the float64 sum of
+    the 8 views' plain gradients (bit-identical replicas, rel. L2 <= 1e-5).
+    RCCL over xGMI itself stays the driver's 8-GPU run."""
+    _run_full_ranks(tmp_path, 8, 5_000_000, 7, 8, ["overlap", "factored"], chunks=7)
+
+
+# ---- the training step's split SH layout through the overlapped exchange (ADVICE r5) ----
+def _train_rank_worker(rank, world, port, outdir):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [root, os.path.join(root, "geometry-grounded-gaussian-splatting_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gsr_train
+    from gaussian_renderer import render
+    from gsr_dist import OverlappedViewGrads
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    step, view, nearest = gsr_train.synthetic_training_setup(20_000, 320, 240, device="cuda", seed=3)
+    g = step.g
+    mine = gsr_train.orbit_views(8, 320, 240, dev)[2 + 3 * rank]  # this rank's view
+    gen = torch.Generator().manual_seed(40 + rank)
+    w = {k: torch.randn(s, generator=gen).to(dev) for k, s in
+         (("render", (3, 240, 320)), ("median_depth", (1, 240, 320)), ("normal", (3, 240, 320)))}
+    params = {n: p for n, p in g.named_parameters() if p.numel()}
+
+    def render_grads():
+        """A loss on the render outputs alone (no other term on the parameters):
+        the raw parameters' gradients through the fused getters and the split
+        SH pair, as TrainStep's render call forms them."""
+        g.optimizer.zero_grad(set_to_none=True)
+        g.begin_step()
+        try:
+            pkg = render(mine, g, step.pipe, step.bg, 0.0, require_depth=True)
+            assert isinstance(g.get_features, tuple)  # the split layout is what the exchange sees
+            loss = sum((pkg[k] * w[k]).sum() for k in w)
+            loss.backward()
+        finally:
+            g.end_step()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().clone() for n, p in params.items()}
+
+    plain = render_grads()
+    with OverlappedViewGrads(chunks=3) as ex:
+        over = render_grads()
+        ex.check()
+        # a whole TrainStep (render + depth-normal + PatchMatch + L1/SSIM + backward + densify + Adam) with the
+        # exchange installed: the render backward exchanges its split-SH gradients, the step completes
+        loss = step.step(view, nearest)
+        ex.check()
+    finite = bool(torch.isfinite(loss)) and all(bool(torch.isfinite(p).all()) for p in params.values())
+    torch.save({"plain": {k: v.cpu() for k, v in plain.items()}, "over": {k: v.cpu() for k, v in over.items()},
+                "finite": finite}, os.path.join(outdir, f"t{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_train_step_split_sh_through_overlapped_exchange(tmp_path):
+    """TrainGaussians.get_features hands the rasterizer the split
+    SH pair (features_dc, features_rest), and the overlapped exchange now
+    rebuilds both gradient tensors (gsr_view_color_grads_chunked's split
+    output, ABI 20).  Two ranks on cuda:0 (gloo), each with its own view: a
+    loss on the render outputs gives every raw parameter (through the fused
+    getters) the sum over the two views of its plain gradient, identically on
+    both ranks; and a whole TrainStep runs with the exchange installed."""
+    import socket
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_train_rank_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    r = [torch.load(tmp_path / f"t{k}.pt", weights_only=True) for k in range(2)]
+    assert r[0]["finite"] and r[1]["finite"]
+    for k, p0 in r[0]["plain"].items():
+        want = p0.double() + r[1]["plain"][k].double()
+        a, b = r[0]["over"][k], r[1]["over"][k]
+        assert torch.equal(a, b), k  # the replicas stay bit-identical
+        err = float((a.double() - want).norm() / want.norm().clamp_min(1e-30))
+        print(f"{k}: rel L2 {err:.2e}")
+        assert err <= 1e-5, (k, err)

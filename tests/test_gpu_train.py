@@ -286,3 +286,25 @@ def test_split_sh_layout_matches_concatenated(setup):
         assert torch.equal(pa[k], pb[k]), k
     for x, y in zip(ga, gb):  # (the accumulated dL/dcolour the SH rows derive from is summed by atomics)
         assert x.shape == y.shape and _rel(x, y) <= 1e-5, _rel(x, y)
+
+
+def test_patchmatch_no_nearest_camera_and_inplace_losses(setup):
+    """without a nearest camera both PatchMatch forms return the
+    reference's two [1]-shaped zeros (utils/loss_utils.py:141-142); and the
+    fused form's losses may be changed in place before the backward (they are
+    not the tensor its backward saves)."""
+    gsr_train, step, view, nearest = setup
+    from gaussian_renderer import render
+    from gsr_patchmatch import patchmatch_fused
+    g = step.g
+    pkg = render(view, g, step.pipe, step.bg, step.kernel_size, require_depth=True)
+    for fn in (patchmatch_fused, gsr_train.patchmatch):
+        ncc, geo = fn(g, pkg, view, None, step.kernel_size, step.pipe)
+        assert ncc.shape == (1,) and geo.shape == (1,) and float(ncc) == 0.0 and float(geo) == 0.0
+    ncc, geo = patchmatch_fused(g, pkg, view, nearest, step.kernel_size, step.pipe)
+    ref = torch.autograd.grad(0.6 * ncc + 0.02 * geo, [g._xyz], retain_graph=True)[0]
+    ncc, geo = patchmatch_fused(g, pkg, view, nearest, step.kernel_size, step.pipe)
+    ncc *= 0.6
+    geo *= 0.02
+    got = torch.autograd.grad(ncc + geo, [g._xyz])[0]
+    assert float((got - ref).norm()) <= 1e-6 * float(ref.norm()) + 1e-12
