@@ -53,6 +53,31 @@ def rel_err(a, b) -> float:
     return 0.0 if den == 0 and num == 0 else float(num / max(den, 1e-30))
 
 
+def record_margins(fields: dict, what: str = "") -> None:
+    """Parity margins: {field: (value, bar)} of one test
+    case.  Prints the worst field against its bar and appends one JSON line
+    per case to $GSR_MARGIN_LOG (default gpurun_out/parity_margins.jsonl at
+    the repository root, when that directory can be written)."""
+    import json
+    import os
+    if not fields:
+        return
+    test = os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0]
+    worst = max(fields, key=lambda k: fields[k][0] / fields[k][1])
+    v, bar = fields[worst]
+    print(f"[margin] {test} {what}: worst {worst} {v:.3e} against {bar:.0e} ({bar / max(v, 1e-300):.1f}x headroom)")
+    path = os.environ.get("GSR_MARGIN_LOG") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
+        __file__))), "gpurun_out", "parity_margins.jsonl")
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": test, "what": what, "worst": worst, "value": v, "bar": bar,
+                                "headroom": bar / max(v, 1e-300),
+                                "fields": {k: [float(a), float(b)] for k, (a, b) in fields.items()}}) + "\n")
+    except OSError:
+        pass
+
+
 def frac_bad(a, b, rtol, atol) -> float:
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)

@@ -154,20 +154,26 @@ def _oracle_backward_on_gpu_state(c, a, out, o, g):
 
 
 def _check_grads(gb, b, l2_bar=1e-4, max_bar=1e-4, report=None):
-    for name, t in zip(GRAD_NAMES, gb):
-        mine, ref = t.cpu().numpy().astype(np.float64), b[name].astype(np.float64)
-        assert mine.shape == ref.shape, name
-        if ref.size == 0:
-            continue
-        if not np.any(ref):
-            assert not np.any(mine), name
-            continue
-        l2 = np.linalg.norm(mine - ref) / np.linalg.norm(ref)
-        mx = Hh.rel_err(mine, ref)
-        if report is not None:
-            report[name] = (l2, mx)
-        assert l2 <= l2_bar, (name, l2)
-        assert mx <= max_bar, (name, mx)
+    margins = {}
+    try:
+        for name, t in zip(GRAD_NAMES, gb):
+            mine, ref = t.cpu().numpy().astype(np.float64), b[name].astype(np.float64)
+            assert mine.shape == ref.shape, name
+            if ref.size == 0:
+                continue
+            if not np.any(ref):
+                assert not np.any(mine), name
+                continue
+            l2 = np.linalg.norm(mine - ref) / np.linalg.norm(ref)
+            mx = Hh.rel_err(mine, ref)
+            if report is not None:
+                report[name] = (l2, mx)
+            margins[f"{name} L2"] = (l2, l2_bar)
+            margins[f"{name} max"] = (mx, max_bar)
+            assert l2 <= l2_bar, (name, l2)
+            assert mx <= max_bar, (name, mx)
+    finally:
+        Hh.record_margins(margins, "gradients vs oracle backward")
 
 
 SMALL = [
@@ -758,6 +764,12 @@ def _audit_full_images(c, out, o, report=None):
     rep["mdepth_max_rel_outside_ties"] = float(np.where(tie_px, 0.0, rel).max()) if rel.size else 0.0
     rep.update(composite_tie_pixels=n_chain, composite_tie_max_margin=worst_chain, mdepth_tie_pixels=n_md,
                mdepth_tie_max_margin=worst_md, unexplained=len(unexplained))
+    margins = {"mdepth rel (per pixel, outside ties)": (rep["mdepth_max_rel_outside_ties"], 1e-4)}
+    for name, t in (("color", color), ("alpha", alpha), ("normal", normal)):
+        a_, b_ = t.cpu().numpy().astype(np.float64), o[name].astype(np.float64)
+        d = (np.abs(a_ - b_) / max(np.abs(b_).max(), 1e-30)).reshape(-1, H, W).max(0)
+        margins[f"{name} / image max (outside ties)"] = (float(np.where(tie_px, 0.0, d).max()), 1e-4)
+    Hh.record_margins(margins, "images vs oracle, every pixel")
     print("image audit:", rep)
     if unexplained:
         print("unexplained pixels:", unexplained[:8])

@@ -68,15 +68,21 @@ def _run(c, pts, kernel_size=0.0, bwd_kernel_size=None, cov3D=None, check_bwd=Tr
     b = O.sample_backward(o["state"], *a[:9], o["inside"], g, c["tanx"], c["tany"], bks)
     gb = _C.sample_rasterized_depth_backward(*ga[:9], inside, _gpu(g), c["tanx"], c["tany"], bks, c["H"], c["W"],
                                              _gpu(c["cam"].camera_center), *out[5:11], K, RN, TN, False, False)
-    for name, t in zip(GRADS, gb):
-        mine, ref = t.cpu().numpy().astype(np.float64), b[name]
-        assert mine.shape == ref.shape, name
-        if not np.any(ref):
-            assert not np.any(mine), name
-            continue
-        l2 = np.linalg.norm(mine - ref) / np.linalg.norm(ref)
-        assert l2 <= 1e-4, (name, l2)
-        assert Hh.rel_err(mine, ref) <= 1e-3, (name, Hh.rel_err(mine, ref))
+    margins = {}
+    try:
+        for name, t in zip(GRADS, gb):
+            mine, ref = t.cpu().numpy().astype(np.float64), b[name]
+            assert mine.shape == ref.shape, name
+            if not np.any(ref):
+                assert not np.any(mine), name
+                continue
+            l2 = np.linalg.norm(mine - ref) / np.linalg.norm(ref)
+            margins[f"{name} L2"] = (l2, 1e-4)
+            margins[f"{name} max"] = (Hh.rel_err(mine, ref), 1e-3)
+            assert l2 <= 1e-4, (name, l2)
+            assert Hh.rel_err(mine, ref) <= 1e-3, (name, Hh.rel_err(mine, ref))
+    finally:
+        Hh.record_margins(margins, "sample_depth gradients vs oracle backward")
     return out, o
 
 
@@ -324,6 +330,8 @@ def test_sample_full_size():
     assert (ins != o["inside"]).mean() <= 1e-4
     got = out1[3].cpu().numpy()
     bad = np.abs(got - o["output"]) > 1e-4 * np.abs(o["output"]).max()
+    Hh.record_margins({"inside flips (fraction)": (float((ins != o["inside"]).mean()), 1e-4),
+                       "points beyond 1e-4 of max (fraction)": (float(bad.mean()), 1e-4)}, "full-size forward")
     assert bad.mean() <= 1e-4, bad.mean()
     del o
     K, RN, TN, output, inside = out1[:5]
@@ -335,10 +343,14 @@ def test_sample_full_size():
                                                    _gpu(cam1.camera_center), *out1[5:11], K, RN, TN, False, False)
 
     b1, b2, b12 = bwd(g1), bwd(g2), bwd(g1 + 2 * g2)
+    lin = {}
     for name, x, y, z in zip(GRADS, b1, b2, b12):
         assert torch.isfinite(z).all(), name
         want = (x + 2 * y).double()
         if float(want.norm()) == 0:
             continue
         err = float((z.double() - want).norm() / want.norm())
+        lin[name] = (err, 1e-4)
+    Hh.record_margins(lin, "full-size backward linearity")
+    for name, (err, _) in lin.items():
         assert err <= 1e-4, (name, err)
