@@ -362,9 +362,131 @@ def time_exchange(mode, P, shm, sgm, world, chunks, dev, reps=10):
             "bus_GBps": round(bus_bytes / (ms * 1e-3) / 1e9, 2)}
 
 
+# the e2e step's SAMPLE raster (render_fwd_kernel<SAMPLE>) as its rocprofv3 kernel name (tools/pmc_summary.py)
+SAMPLE_KERNEL = "render_fwd_kernel<true, false, true>"
+
+
+def sample_fwd_bytes(cap):
+    """Algorithmic bytes of one SAMPLE-raster launch (stage sample_fwd) from a captured
+    sample_rasterized_depth call (_C.CAPTURE_SAMPLE): per tile, its list read once up to the
+    largest last contributor of its points (4-B id + the 48-B record words the raster stages),
+    and per point in view 12 B in (projected xy, |p_view|) + 26 B out (the point, inside, median
+    depth, last contributor, dT/dt_m and its flag).  Returns (bytes, list entries, points)."""
+    from diff_gaussian_rasterization import _C
+
+    pts = cap["points3D"].detach().reshape(-1, 3).float()
+    out = cap["out"]
+    PN = pts.shape[0]
+    _, last = _C.debug_sample_points(out[7], PN)
+    W, H = cap["W"], cap["H"]
+    ph = torch.cat([pts, torch.ones(PN, 1, device=pts.device)], 1) @ cap["projmatrix"].float()
+    ndc = (ph[:, :2] / (ph[:, 3:4] + 1e-7)).double()
+    tx = torch.floor((((ndc[:, 0] + 1.0) * W - 1.0) * 0.5 + 0.5) / 16.0).long()  # rasterizer_impl.cu:127-131
+    ty = torch.floor((((ndc[:, 1] + 1.0) * H - 1.0) * 0.5 + 0.5) / 16.0).long()
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    m = out[4].reshape(-1) & (tx >= 0) & (tx < gx) & (ty >= 0) & (ty < gy)
+    lt = torch.from_numpy(last.astype("int64")).to(pts.device)
+    maxl = torch.zeros(gx * gy, dtype=torch.int64, device=pts.device).scatter_reduce(
+        0, (ty * gx + tx)[m], lt[m], reduce="amax")
+    entries, n_in = int(maxl.sum()), int(m.sum())
+    return entries * (4 + 48) + n_in * 38, entries, n_in
+
+
+def e2e_cpu_baseline(args, ts, view, nearest, cap):
+    """The training iteration's work on the host cores, component by component, on the same
+    state: the torch-CPU getters (gaussian_model.py:146-212), the C oracle's raster forward +
+    backward of the view (tile stride as bench.py's cpu_baseline) and sample_depth forward +
+    backward of the PatchMatch points from the nearest view, the oracle's warp_patch_ncc over
+    every pixel, the SSIM and depth-to-normal losses forward + backward in torch-CPU
+    (oracle/ssim_ref.py, fp32), and one torch-CPU Adam step over the parameters.  The value is
+    1 / (sum of the component times): a sum of measured components, not one chained run."""
+    sys.path.insert(0, ROOT)
+    import gsr_scene as S
+    from oracle import gsr_oracle as O
+    from oracle import ssim_ref as SR
+
+    cores, host = host_cores()
+    torch.set_num_threads(cores)
+    O.set_threads(cores)
+    g = ts.g
+    raw = S.RawGaussians(*[getattr(g, "_" + f).detach().cpu() if f != "filter_3D" else g.filter_3D.detach().cpu()
+                           for f in ("xyz", "features_dc", "features_rest", "scaling", "rotation", "opacity",
+                                     "sg_axis", "sg_sharpness", "sg_color", "filter_3D")])
+    sec = {}
+    gb = getter_baseline(raw, cores)
+    sec["getters"] = gb["ms_per_call"] * 1e-3
+    inp = {k: v.detach().contiguous() for k, v in S.activated_inputs(raw).items()}
+    W, H = args.width, args.height
+    cam = lambda v: (v.world_view_transform.cpu(), v.full_proj_transform.cpu(), v.camera_center.cpu(),  # noqa: E731
+                     math.tan(v.FoVx / 2), math.tan(v.FoVy / 2))
+    wv, fp, cc, tx_, ty_ = cam(view)
+    stride = args.cpu_tile_stride or 1
+    O.set_tile_stride(stride)
+    a = (torch.zeros(3), inp["means3D"], None, inp["opacities"], inp["scales"], inp["rotations"], None, inp["shs"],
+         inp["sg_axis"], inp["sg_sharpness"], inp["sg_color"], args.sh_degree, args.sg_degree, 1.0, wv, fp, tx_, ty_,
+         0.0)
+    gr = S.upstream_grads(H, W)
+    o = O.forward(*a, H, W, cc, False, True)
+    tf = O.last_times()
+    O.backward(o["state"], *a, gr["color"], gr["mdepth"], gr["alpha"], gr["normal"], o["alpha"], o["normal"],
+               o["mdepth"], cc, o["radii"])
+    tb = O.last_times()
+    O.set_tile_stride(1)
+    sec["render"] = tf["preprocess_binning"] + stride * tf["render"] + stride * tb["render_bwd"] + tb["preprocess_bwd"]
+    del o
+    nwv, nfp, ncc_, ntx, nty = cam(nearest)
+    pts = cap["points3D"].detach().cpu().float()
+    t0 = time.perf_counter()
+    so = O.sample_forward(pts, inp["means3D"], inp["opacities"], inp["scales"], inp["rotations"], 1.0, None, nwv, nfp,
+                          ntx, nty, 0.0, H, W, ncc_, False)
+    O.sample_backward(so["state"], pts, inp["means3D"], inp["opacities"], inp["scales"], inp["rotations"], 1.0, None,
+                      nwv, nfp, so["inside"], torch.randn(pts.shape) * 1e-2, ntx, nty, 0.0)
+    sec["sample_depth"] = time.perf_counter() - t0
+    del so
+    # warp_patch_ncc at every pixel (the step computes it at the geometrically consistent ones)
+    ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    uvs = torch.stack([xs.reshape(-1), ys.reshape(-1)], 1).int()
+    dep = torch.full((H * W,), 5.0)
+    nrm = torch.tensor([0.0, 0.0, -1.0]).expand(H * W, 3).contiguous()
+    wr, wn = view.world_view_transform.cpu(), nearest.world_view_transform.cpu()
+    r_rel = wn[:3, :3].T @ wr[:3, :3]
+    t_rel = -r_rel @ wr[3, :3] + wn[3, :3]
+    gray = lambda v: (0.299 * v.original_image[0] + 0.587 * v.original_image[1] + 0.114 * v.original_image[2]).cpu()  # noqa: E731
+    t0 = time.perf_counter()
+    O.warp_patch_ncc(dep, nrm, uvs, r_rel.T.contiguous(), t_rel, gray(view), gray(nearest), view.Fx, view.Fy, view.Cx,
+                     view.Cy, nearest.Fx, nearest.Fy, nearest.Cx, nearest.Cy)
+    sec["ncc"] = time.perf_counter() - t0
+    img = view.original_image.cpu()[None].clone().requires_grad_(True)
+    gt = (img.detach() * 0.9 + 0.05)
+    t0 = time.perf_counter()
+    loss = 0.8 * (img - gt).abs().mean() + 0.2 * (1.0 - SR.ssim(img, gt, padding="valid"))
+    loss.backward()
+    sec["l1_ssim"] = time.perf_counter() - t0
+    d = torch.full((1, H, W), 5.0, requires_grad=True)
+    t0 = time.perf_counter()
+    n_, _ = SR.depth_to_normal(d, view.Fx, view.Fy, view.Cx, view.Cy)
+    n_.sum().backward()
+    sec["depth_normal"] = time.perf_counter() - t0
+    ps = [torch.zeros(p.shape, requires_grad=True) for p in g.parameters() if p.numel()]
+    for q in ps:
+        q.grad = torch.ones_like(q)
+    opt = torch.optim.Adam(ps, lr=1e-3, eps=1e-15)
+    opt.step()
+    t0 = time.perf_counter()
+    opt.step()
+    sec["adam"] = time.perf_counter() - t0
+    total = sum(sec.values())
+    return {"value": round(1.0 / total, 6), "unit": "iters/s", "cores": cores, "kind": "port", "host": host,
+            "sample": ("one training iteration's components on the host cores, summed: "
+                       + ", ".join(f"{k} {v:.2f} s" for k, v in sec.items())
+                       + f" (raster tiles every {stride}th, extrapolated; C oracle and torch-CPU)"),
+            "component_s": {k: round(v, 4) for k, v in sec.items()}}
+
+
 def run_e2e(args, dev):
     """bench.py --e2e: one training iteration (gsr_train.TrainStep) per step."""
     import gsr_train
+    from diff_gaussian_rasterization import _C
 
     W, H, P = args.width, args.height, args.P
     ts, view, nearest = gsr_train.synthetic_training_setup(P, W, H, args.sh_degree, args.sg_degree, device=dev)
@@ -378,13 +500,76 @@ def run_e2e(args, dev):
         for k, v in ts.component_ms().items():
             comps[k].append(v)
     ts.timing = False
+    # the library's stages per step (untimed steps, every stage bracketed); the dominant one is the roofline's
+    _C.timing_collect()
+    _C.timing_stages(None)
+    _C.timing_enable(True)
+    for _ in range(max(1, args.stage_steps)):
+        ts.step(view, nearest)
+    torch.cuda.synchronize(dev)
+    _C.timing_enable(False)
+    table = {k: ms / max(1, args.stage_steps) for k, (ms, n) in _C.timing_collect().items() if n}
+    dom = max(table, key=table.get)
+    _C.timing_stages([dom])
+    _C.timing_enable(True)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = ts.step(view, nearest)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    _C.timing_enable(False)
+    _C.timing_stages(None)
+    dom_ms, dom_n = _C.timing_collect()[dom]
     ms = elapsed / args.steps * 1e3
+    # one more step with the sample_depth call captured (its points and per-point last contributors)
+    _C.CAPTURE_SAMPLE = True
+    try:
+        ts.step(view, nearest)
+        torch.cuda.synchronize(dev)
+        cap = _C.last_sample
+    finally:
+        _C.CAPTURE_SAMPLE = False
+        _C.last_sample = None
+    roofline = None
+    if dom == "sample_fwd" and cap is not None:
+        nbytes, entries, n_in = sample_fwd_bytes(cap)
+        launch_ms = dom_ms / max(1, dom_n)
+        achieved = nbytes / (launch_ms * 1e-3) / 1e9
+        traffic = pipe_busy = valu_insts = None
+        pmc_file = None
+        if args.preset_workload:
+            try:
+                with open(os.path.join(ROOT, "profiles", "pmc_e2e.json")) as f:
+                    kt = json.load(f)["kernels"][SAMPLE_KERNEL]
+                traffic, valu_insts = kt.get("hbm_bytes"), kt.get("valu_insts")
+                if kt.get("valu_active"):
+                    pipe_busy = kt["valu_active"] * 4 / (launch_ms * 1e-3 * CLOCK_HZ * SIMDS)
+                pmc_file = "profiles/pmc_e2e.json"
+            except Exception:  # noqa: BLE001 - no e2e PMC summary yet -> null
+                pass
+        hbm_frac = achieved / HBM_PEAK_GBPS
+        roofline = {"bound": "valu" if pipe_busy is not None and pipe_busy > hbm_frac else "hbm", "kernel": dom,
+                    "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(hbm_frac, 5), "traffic": traffic, "algorithmic_bytes_per_launch": int(nbytes),
+                    "algorithmic_units": (f"per tile its list read once up to the largest last contributor of its "
+                                          f"points ({entries} entries) x (4 + 48) B + {n_in} points in view x 38 B"),
+                    "avg_launch_ms": round(launch_ms, 4),
+                    "valu": None if pipe_busy is None else {"pipe_busy": round(pipe_busy, 4),
+                                                           "insts_per_launch": valu_insts,
+                                                           "pipe_busy_source": "SQ_ACTIVE_INST_VALU x 4 / SIMD-cycles "
+                                                                               "of the live launch time"},
+                    "pmc_source": pmc_file, "pmc_kernel": SAMPLE_KERNEL,
+                    "stage_ms_per_step": {k: round(v, 4) for k, v in table.items()}}
+    elif table:
+        roofline = {"kernel": dom, "achieved": None, "note": f"dominant stage {dom}: no e2e byte model for it",
+                    "stage_ms_per_step": {k: round(v, 4) for k, v in table.items()}}
+    cpu = None
+    if not args.no_cpu_baseline and cap is not None:
+        try:
+            cpu = e2e_cpu_baseline(args, ts, view, nearest, cap)
+        except Exception as e:  # noqa: BLE001 - report, never hide
+            cpu = {"value": None, "error": repr(e)}
     line = {
         "metric": "train iters/sec (full training iteration after iteration 7000) at 1080p, 1M Gaussians",
         "value": round(args.steps / elapsed, 3), "unit": "iters/s", "n_gpus": 1, "steps": args.steps,
@@ -397,7 +582,7 @@ def run_e2e(args, dev):
                                 "FusedAdam step"),
                    "P": P, "width": W, "height": H, "loss": float(loss)},
         "components_ms": {k: round(sorted(v)[len(v) // 2], 4) for k, v in comps.items()},
-        "roofline": None, "cpu_baseline": None,
+        "roofline": roofline, "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
 

@@ -221,6 +221,10 @@ constexpr int kRefineWalks = GSR_REFINE_WALKS;
 #define GSR_SAMPLE_WALKS 5
 #endif
 constexpr int kSampleWalks = GSR_SAMPLE_WALKS;
+#ifndef GSR_SAMPLE_DT_TOL
+#define GSR_SAMPLE_DT_TOL 0.004f  // (SAMPLE) longest step, relative to the curvature length, dT/dt_m is continued over
+#endif
+constexpr float kSampleDtTol = GSR_SAMPLE_DT_TOL;
 #ifndef GSR_SAMPLE_NO_ENDS
 #define GSR_SAMPLE_NO_ENDS 1  // (round 5: sample_fwd 0.839-0.844 -> 0.792-0.812 ms at the sample bench; 2 more of 1.27M points to the passes)
 #endif
@@ -374,6 +378,9 @@ __device__ unsigned long long g_render_stats[kRenderStats];
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
+#ifndef GSR_SAMPLE_WAVES
+#define GSR_SAMPLE_WAVES 7  // (the SAMPLE instance: 72 VGPRs; the grouped exact dT/dt_m walk took it to 74 = 6 waves)
+#endif
 
 // Median-depth phases 2b and 3 (render path) give each listed pixel as many
 // lanes as one round of the block allows (up to 16), instead of 4 and 1.
@@ -414,7 +421,7 @@ constexpr int kP2bWalks = GSR_P2B_WALKS;
 #endif
 
 template <bool GEOM, bool STATS = false, bool SAMPLE = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, 8))) render_fwd_kernel(RenderFwdArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPLE && GEOM && !STATS) ? GSR_SAMPLE_WAVES : GSR_FWD_WAVES, 8))) render_fwd_kernel(RenderFwdArgs a) {
     // LDS: composite staging (4 x 128 x 16 B = 8 KB) aliased with the
     // resident cache (3 x 256 x 16 B = 12 KB), the 8 KB of masks and the
     // phase exchange: 24.3 KB per block, 6 blocks (24 waves) per CU.
@@ -820,6 +827,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
         bool refined = false;   // median depth found by the root refinement
         float t_ref = 0.f;
         float ref_t = 0.f, ref_D = 0.f, ref_E = 0.f;  // the last refinement walk's depth, -H', H''
+        bool dt_loose = false;  // (SAMPLE) refined, but dT/dt_m continued over too long a step: walked exactly
         // one pass of the reference's bisection (render_forward.cu:560-645) over
         // the lanes still in range and not refined; FIRST evaluates all 9
         // samples, later passes reuse the bracketing ends
@@ -931,6 +939,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             float t_ref, ref_t, ref_D, ref_E;
             float t, lo, hi;
             bool lo_ev, hi_ev;  // lo / hi set by an evaluation of T (not the window's unevaluated ends)
+            float ref_F;        // the last walk's curvature bound F (sum |H'' terms|)
         };
         // One walk's update of a live pixel: log2 T, its derivatives -D, E and the curvature bound F at t
         // (the products and sums of the walk), the bracket, the Halley iterate, and acceptance.
@@ -975,6 +984,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 r.ref_t = t;
                 r.ref_D = D;
                 r.ref_E = E;
+                r.ref_F = F;
             }
             t = tn;
         };
@@ -1692,6 +1702,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
                 ref_t = r.ref_t;
                 ref_D = r.ref_D;
                 ref_E = r.ref_E;
+                // dT/dt_m continued from the last walk over the step to the root keeps a relative error
+                // ~(|step| F / D)^2 (up to kCurvTol^2 = 4e-4 by the acceptance test); the sample backward's
+                // implicit gradient scales with 1 / dT/dt_m, and its parity against the exact pre-pass
+                // (sample_backward.cu:77-140) sat at the 1e-4 bar (drotations, P600-W96-H64-seed1) — so a
+                // root whose step is longer than kSampleDtTol of the curvature length gets the exact walk
+                dt_loose = refined && fabsf(r.t_ref - r.ref_t) * r.ref_F > kSampleDtTol * r.ref_D;
+                if constexpr (STATS && !kClock) st[19] += dt_loose ? 1 : 0;
                 stamp(4);
             } else {
                 stamp(2);
@@ -1764,13 +1781,55 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FW
             }
             float dT_dtm = 0.f;
             const bool want_dT = !SAMPLE || a.query == kQuerySample;
-            if (refined) {
+            if (refined && !dt_loose) {
                 // the reference's dT/dt_m (render_backward.cu:876) is T H' ln2 = H' ln2 / 2 at T = 1/2;
                 // continued to mDepth_b from the last walk: H'(t) = -D + E (t - ref_t) (|t - ref_t| <= a
                 // Newton step of kRefineTol max(t, 1); the next term is ~(step / sigma)^2 relative)
                 if (mDepth_b != 0.f)
                     dT_dtm = (0.5f * 0.69314718055994530942f) * __builtin_fmaf(ref_E, mDepth_b - ref_t, -ref_D);
-            } else if (resident) {
+            }
+            // (SAMPLE) the exact dT/dt_m of the loose-continuation roots, per wave: those lanes' points
+            // compacted into groups of G lanes (the largest power of two up to 16 that fits them all in
+            // the wave), lane q of a group walking the contributors of index % G == q of its point's
+            // blended set, combined by DPP (gsum) and sent back to the owner — instead of every lane of
+            // the wave waiting while the few loose ones walk their whole sets (a quarter of the points
+            // are loose at the sample bench, in almost every wave)
+            float dT_grp = 0.f;
+            if constexpr (SAMPLE) {
+                const bool need = dt_loose && resident && want_dT && inside && mDepth_b != 0.f && last != 0;
+                const unsigned long long bl = __ballot(need);
+                if (bl != 0ull) {  // (wave-uniform)
+                    const int lane = tid & 63;
+                    const int n = __popcll(bl);
+                    int lg = 4;
+                    while (lg > 0 && (n << lg) > 64) lg--;
+                    const int G = 1 << lg;
+                    const int e = lane >> lg;
+                    const bool work = e < n;
+                    int owner = lane;
+                    unsigned long long m = bl;
+                    for (int i = 0; i < n; i++) {  // (scalar loop: the i-th loose lane of the wave)
+                        const int o = __builtin_ctzll(m);
+                        m &= m - 1ull;
+                        owner = e == i ? o : owner;
+                    }
+                    const float ot = __shfl(mDepth_b, owner, 64);
+                    const float ox = __shfl(lane_fx(), owner, 64), oy = __shfl(lane_fy(), owner, 64);
+                    const uint32_t ol = (uint32_t)__shfl((int)last, owner, 64);
+                    float d = 0.f;
+                    walk(s_mask + ((tid & ~63) + owner), ol, ox, oy, gfilter(G, lane & (G - 1)), work,
+                         each([&](float alpha, float t_peak, float rs, float, float) {
+                             const float t_delta = (ot - t_peak) * rs;
+                             const float Gt = alpha * __expf(-0.5f * t_delta * t_delta);
+                             d += fast_div(-0.25f * Gt, 1.f - Gt) * fabsf(t_delta) * rs;
+                         }));
+                    d = gsum(d, G);
+                    dT_grp = __shfl(d, __popcll(bl & ((1ull << lane) - 1ull)) << lg, 64);
+                }
+            }
+            if (SAMPLE && dt_loose) {
+                dT_dtm = dT_grp;  // (a tile past the LDS cache: 0, and md_ok tells the backward to recompute)
+            } else if (!refined && resident) {
                 lane_walk(want_dT && inside && mDepth_b != 0.f && last != 0,
                           each([&](float alpha, float t_peak, float rs, float, float) {
                               const float t_delta = (mDepth_b - t_peak) * rs;

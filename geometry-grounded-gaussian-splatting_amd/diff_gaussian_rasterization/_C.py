@@ -515,6 +515,12 @@ def evaluate_sdf_from_signle_view(points3D, means3D, opacity, scales, rotations,
                         image_height, image_width, campos, prefiltered, debug)
 
 
+# (measurement hook, bench.py --e2e: the last sample_rasterized_depth call's points, camera and outputs, for
+# the SAMPLE raster's algorithmic bytes)
+CAPTURE_SAMPLE = False
+last_sample = None
+
+
 def sample_rasterized_depth(points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                             viewmatrix, projmatrix, tan_fovx, tan_fovy, kernel_size, image_height, image_width,
                             campos, prefiltered, debug):
@@ -546,7 +552,11 @@ def sample_rasterized_depth(points3D, means3D, opacity, scales, rotations, scale
                 _stream(dev), ctypes.byref(K), ctypes.byref(RN), ctypes.byref(TN), scratch.cb, None)
         del scratch
         _check(rc)
-    return (K.value, RN.value, TN.value, output, inside, *[b.tensor for b in bufs])
+    res = (K.value, RN.value, TN.value, output, inside, *[b.tensor for b in bufs])
+    if CAPTURE_SAMPLE:
+        global last_sample
+        last_sample = dict(points3D=points3D, projmatrix=projmatrix, H=H, W=W, out=res)
+    return res
 
 
 def sample_rasterized_depth_backward(points3D, means3D, opacity, scales, rotations, scale_modifier, cov3D_precomp,

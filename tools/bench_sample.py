@@ -89,7 +89,7 @@ if os.environ.get("SAMPLE_STATS"):  # the SAMPLE raster's counters (and, in a -D
     _C.set_option(_C.OPT_RENDER_STATS, 0)
     print("walk wave-steps", s[0], "active lanes/step", round(s[1] / max(s[0], 1), 2), "composite wave-steps", s[2],
           "blending lanes/step", round(s[3] / max(s[2], 1), 2), "refine waves", s[4], "pass waves", s[5],
-          "root updates", s[6], "lanes left", s[7])
+          "root updates", s[6], "lanes left", s[7], "dT walked exactly (loose continuation)", s[19])
     if s[15]:
         for k, name in enumerate(("composite", "masks/staging", "probe walk", "Halley walks", "passes", "-", "-")):
             print(f"clock {name}: {s[8 + k]:.4g} ({s[8 + k] / s[15]:.3f})")

@@ -114,6 +114,8 @@ def kernel_table(src: str) -> dict:
     w = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     sq_csv = os.path.join(src, "sq", "run_counter_collection.csv")
     valu = per_kernel(sq_csv, "SQ_INSTS_VALU") if os.path.exists(sq_csv) else {}
+    active = per_kernel(sq_csv, "SQ_ACTIVE_INST_VALU") if os.path.exists(sq_csv) else {}
+    trans = per_kernel(sq_csv, "SQ_INSTS_VALU_TRANS_F32") if os.path.exists(sq_csv) else {}
     out = {}
     for k, lst in durs.items():
         lst = sorted(lst[1:] or lst)
@@ -121,7 +123,9 @@ def kernel_table(src: str) -> dict:
                   "fetch_kib": None if k not in f else round(f[k], 1),
                   "write_kib": None if k not in w else round(w[k], 1),
                   "hbm_bytes": None if k not in f or k not in w else round((2.0 * f[k] + w[k]) * 1024.0),
-                  "valu_insts": None if k not in valu else round(valu[k])}
+                  "valu_insts": None if k not in valu else round(valu[k]),
+                  "valu_trans_insts": None if k not in trans else round(trans[k]),
+                  "valu_active": None if k not in active else round(active[k])}
     return out
 
 
