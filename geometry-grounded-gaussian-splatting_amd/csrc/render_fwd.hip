@@ -469,6 +469,58 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
         pixx = xy.x;
         pixy = xy.y;
         pt_t = inside ? a.pt_t[pid] : 0.f;  // (GEOM: the refinement's start, GSR_SAMPLE_GUESS)
+#ifndef GSR_SAMPLE_SORT
+#define GSR_SAMPLE_SORT 1
+#endif
+        if constexpr (GEOM && GSR_SAMPLE_SORT) {
+            // The chunk's points reordered by their pixel cell in the tile (row-major 16 x 16), so each wave
+            // holds a compact patch of the tile as the render path's 16 x 4 strips: neighbouring points
+            // blend similar sets, which makes a wave's composite and walks less divergent (the scatter into
+            // the tile ranges leaves the points in arbitrary order).  A counting sort in LDS, before any
+            // staging uses it; no output depends on which lane works a point.
+            uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_rec);  // [256] counts, then offsets
+            uint32_t* s_sp = s_cnt + kTilePixels;                  // [256] point id, x, y, |p_view| by rank
+            float* s_sx = reinterpret_cast<float*>(s_sp + kTilePixels);
+            float* s_sy = s_sx + kTilePixels;
+            float* s_st = s_sy + kTilePixels;
+            uint32_t* s_wt = reinterpret_cast<uint32_t*>(s_st + kTilePixels);  // [4] wave totals
+            s_cnt[tid] = 0u;
+            __syncthreads();
+            const int tx0 = (int)(tile % a.grid_x) * kTile, ty0 = (int)(tile / a.grid_x) * kTile;
+            const int lx = min(max((int)floorf(pixx + 0.5f) - tx0, 0), kTile - 1);
+            const int ly = min(max((int)floorf(pixy + 0.5f) - ty0, 0), kTile - 1);
+            const uint32_t key = (uint32_t)(ly * kTile + lx);
+            const uint32_t rk = inside ? atomicAdd(&s_cnt[key], 1u) : 0u;
+            __syncthreads();
+            const uint32_t c = s_cnt[tid];
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if ((tid & 63) >= o) incl += y;
+            }
+            if ((tid & 63) == 63) s_wt[tid >> 6] = incl;
+            __syncthreads();
+            uint32_t off = 0;
+            for (int w = 0; w < (tid >> 6); w++) off += s_wt[w];
+            s_cnt[tid] = off + incl - c;  // (each lane rewrites only its own count, read above)
+            __syncthreads();
+            if (inside) {
+                const uint32_t d = s_cnt[key] + rk;
+                s_sp[d] = pid;
+                s_sx[d] = pixx;
+                s_sy[d] = pixy;
+                s_st[d] = pt_t;
+            }
+            const uint32_t n_in = s_wt[0] + s_wt[1] + s_wt[2] + s_wt[3];
+            __syncthreads();
+            inside = (uint32_t)tid < n_in;
+            pid = inside ? s_sp[tid] : 0u;
+            pixx = inside ? s_sx[tid] : 0.f;
+            pixy = inside ? s_sy[tid] : 0.f;
+            pt_t = inside ? s_st[tid] : 0.f;
+            __syncthreads();  // (the staging below reuses s_rec)
+        }
     } else {
         tile = a.tile_order ? a.tile_order[blockIdx.x] : xcd_remap(blockIdx.x, a.num_tiles);
         const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;

@@ -46,6 +46,7 @@ def _check(c, pts, cov3D=None):
     gK, gT, gin = _C.integrate_gaussians_to_points(*ga)
     assert gK == K
     assert np.array_equal(gin.cpu().numpy(), inside)
+    margins = {"integrate 1 - T (absolute)": (float(np.abs(gT.cpu().numpy() - T).max()), 1e-4)}
     assert np.abs(gT.cpu().numpy() - T).max() <= 1e-4, np.abs(gT.cpu().numpy() - T).max()
     assert 0.0 < T[inside].mean() < 1.0
     K, depth, sdf, inside = O.evaluate_sdf(*a)
@@ -53,6 +54,9 @@ def _check(c, pts, cov3D=None):
     assert gK == K
     assert np.array_equal(gin.cpu().numpy(), inside)
     assert inside.sum() > 0
+    margins["evaluate_sdf depth / max"] = (Hh.rel_err(gd.cpu().numpy(), depth), 1e-4)
+    margins["evaluate_sdf sdf / max depth"] = (float(np.abs(gs.cpu().numpy() - sdf).max() / np.abs(depth).max()), 1e-4)
+    Hh.record_margins(margins, "point queries vs oracle")
     assert Hh.rel_err(gd.cpu().numpy(), depth) <= 1e-4, Hh.rel_err(gd.cpu().numpy(), depth)
     assert np.abs(gs.cpu().numpy() - sdf).max() <= 1e-4 * np.abs(depth).max()
 

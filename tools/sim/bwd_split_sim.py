@@ -64,3 +64,32 @@ for _ in range(NT):
 print({k: v for k, v in tot.items()})
 print(f"halves / S = {tot['halves'] / tot['S']:.3f}, quarters / S = {tot['quarters'] / tot['S']:.3f}, "
       f"valid fraction of walked pixel-steps = {tot['valid'] / tot['pix_steps']:.3f}")
+# pixels sorted by last contributor: the lower half's pair is idle for every walked entry at or past
+# its largest last (a wave-uniform skip), how much of the walk that is
+rng = np.random.default_rng(2)
+skip = walked = 0
+for _ in range(NT):
+    t = int(rng.integers(gx * gy))
+    tx, ty = t % gx, t // gx
+    a, b = ranges[t]
+    ys, xs = np.mgrid[ty * 16:ty * 16 + 16, tx * 16:tx * 16 + 16]
+    inside = (xs < W) & (ys < H)
+    last = np.where(inside, nc[np.minimum(ys, H - 1), np.minimum(xs, W - 1)], 0).reshape(-1)
+    mc = int(last.max())
+    if mc == 0:
+        continue
+    g = plist[a:a + mc]
+    m = geo["means2D"][g].astype(np.float32)
+    co = geo["conic_opacity"][g].astype(np.float32)
+    xs_, ys_ = xs.reshape(-1).astype(np.float32), ys.reshape(-1).astype(np.float32)
+    dx = m[:, 0, None] - xs_[None]
+    dy = m[:, 1, None] - ys_[None]
+    power = -0.5 * (co[:, 0, None] * dx * dx + co[:, 2, None] * dy * dy) - co[:, 1, None] * dx * dy
+    alpha = np.minimum(0.99, co[:, 3, None] * np.exp(np.minimum(power, 0)))
+    valid = (np.arange(mc)[:, None] < last[None]) & (power <= 0) & (alpha >= 1 / 255)
+    anyv = valid.any(1)
+    lo_half_max = np.sort(last)[:128].max()
+    e = np.nonzero(anyv)[0]
+    walked += len(e)
+    skip += int((e >= lo_half_max).sum())
+print(f"last-sorted halves: the lower half idle for {skip / max(walked, 1):.3f} of the walked entries")
