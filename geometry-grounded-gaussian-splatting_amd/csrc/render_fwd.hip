@@ -56,6 +56,10 @@ constexpr int kBatch = GSR_BATCH;        // records per composite staging batch
 #define GSR_WALK_SOA 1
 #endif
 constexpr bool kWalkSoA = GSR_WALK_SOA;
+#ifndef GSR_SAMPLE_WALK_SOA
+#define GSR_SAMPLE_WALK_SOA GSR_WALK_SOA  // (the SAMPLE instance's own choice: A/B)
+#endif
+constexpr bool kSampleWalkSoA = GSR_SAMPLE_WALK_SOA;
 constexpr int kPlane = kResident + 1;
 constexpr int kPlanes = 12;  // x, y, conic a, b, c, opacity, plane x, y, |t|, rsigma, sc, ball
 constexpr int kRecSlots = 3 * kPlane > 4 * kBatch ? 3 * kPlane : 4 * kBatch;
@@ -761,12 +765,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
         float4* c_w0 = s_rec;
         float4* c_w1 = s_rec + kResident;
         float4* c_w2 = s_rec + 2 * kResident;
-        float* const s_pl = reinterpret_cast<float*>(s_rec);  // (kWalkSoA) kPlanes planes of kPlane floats
+        constexpr bool kSoA = SAMPLE ? kSampleWalkSoA : kWalkSoA;
+        float* const s_pl = reinterpret_cast<float*>(s_rec);  // (kSoA) kPlanes planes of kPlane floats
         auto pl = [&](int f, int j) -> float { return s_pl[f * kPlane + j]; };
         auto pl2 = [&](int f, int j1, int j2) -> f32x2 { return f32x2{s_pl[f * kPlane + j1], s_pl[f * kPlane + j2]}; };
         // one staged record as the three float4 words (w2 = |t|, rsigma, sc, ball)
         auto rec = [&](int j, float4& w0, float4& w1, float4& w2) {
-            if constexpr (kWalkSoA) {
+            if constexpr (kSoA) {
                 w0 = make_float4(pl(0, j), pl(1, j), pl(2, j), pl(3, j));
                 w1 = make_float4(pl(4, j), pl(5, j), pl(6, j), pl(7, j));
                 w2 = make_float4(pl(8, j), pl(9, j), pl(10, j), pl(11, j));
@@ -784,7 +789,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                 const float4 w0 = sp->w0, w1 = sp->w1, w2s = sp->w2;
                 const bool ball = w2s.y > 0.f;  // non-ball splats: g = 0 (bisect_step)
                 const float4 w2 = make_float4(w2s.x, w2s.y, ball ? w2s.y * kSqrtHalfLog2e : 0.f, ball ? 1.f : 0.f);
-                if constexpr (kWalkSoA) {
+                if constexpr (kSoA) {
                     const float v[kPlanes] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y, w2.z, w2.w};
 #pragma unroll
                     for (int f = 0; f < kPlanes; f++) s_pl[f * kPlane + k] = v[f];
@@ -839,7 +844,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                 // roundings (packed fp32 rounds as the scalar ops: alpha stays bit-identical to the
                 // composite's and the backward's); __expf(x) = v_exp_f32(x log2 e)
                 f32x2 X, Y, CA, CB, CC, OP, PX, PY, TT, RS, SC, BM;
-                if constexpr (kWalkSoA) {
+                if constexpr (kSoA) {
                     X = pl2(0, j1, j2), Y = pl2(1, j1, j2), CA = pl2(2, j1, j2), CB = pl2(3, j1, j2);
                     CC = pl2(4, j1, j2), OP = pl2(5, j1, j2), PX = pl2(6, j1, j2), PY = pl2(7, j1, j2);
                     TT = pl2(8, j1, j2), RS = pl2(9, j1, j2), SC = pl2(10, j1, j2), BM = pl2(11, j1, j2);
@@ -993,10 +998,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
             bool lo_ev, hi_ev;  // lo / hi set by an evaluation of T (not the window's unevaluated ends)
             float ref_F;        // the last walk's curvature bound F (sum |H'' terms|)
         };
+#ifdef GSR_DBG_PX
+        bool dbg_here = false;  // (development: the walked pixel is the traced one)
+#endif
         // One walk's update of a live pixel: log2 T, its derivatives -D, E and the curvature bound F at t
         // (the products and sums of the walk), the bracket, the Halley iterate, and acceptance.
         auto root_update = [&](Refine& r, bool& live, float& t, float& lo, float& hi, float A, float B, float D, float E,
                                float F, float scale) {
+#ifdef GSR_DBG_PX
+            if (dbg_here)
+                printf("root_update lane %d t %.7f H %g D %g E %g F %g [%.7f %.7f]\n", (int)(threadIdx.x & 63), t,
+                       __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f, D, E, F, lo, hi);
+#endif
             const float tol = kRefineTol * scale, tol_cond = kCondTol * scale, tol_loose = kLooseTol * scale;
             if constexpr (STATS) st[6] += 1;
             const float H = __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f;
@@ -1046,10 +1059,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
             const f32x2 TSE[1] = {f32x2{e0, e8}};
             for (int k = 0; k < walks && a.passes > 1; k++) {
                 if (__ballot(live) == 0ull) break;
+                if constexpr (STATS && SAMPLE && !kClock) st_phase = k < 3 ? k : 3;  // (walk stats per walk index)
                 float A = 1.f, B = 1.f, D = 0.f, E = 0.f, F = 0.f;
                 f32x2 AE[1] = {f32x2{1.f, 1.f}}, BE[1] = {f32x2{1.f, 1.f}};
                 float unusedA = 1.f, unusedB = 1.f;
                 const PixSrc ps = src();
+#ifdef GSR_DBG_PX
+                dbg_here = ps.x == (float)GSR_DBG_PX && ps.y == (float)GSR_DBG_PY;
+#endif
                 if (ends && k == 0) {
                     walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, live,
                          each([&](float alpha, float t_peak, float rs, float sc, float bm) {
@@ -1777,6 +1794,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
             const bool left = SAMPLE && in_range && !refined;
             if constexpr (STATS && SAMPLE) st[7] += left ? 1 : 0;
             if (SAMPLE && __ballot(left) != 0ull) {
+                if constexpr (STATS && !kClock) st_phase = 3;  // (the passes' walks counted with walk4+)
                 if constexpr (STATS) {
                     if ((tid & 63) == 0) st[5] += 1;
                 }
@@ -1869,6 +1887,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                     const float ox = __shfl(lane_fx(), owner, 64), oy = __shfl(lane_fy(), owner, 64);
                     const uint32_t ol = (uint32_t)__shfl((int)last, owner, 64);
                     float d = 0.f;
+                    if constexpr (STATS && !kClock) st_phase = 4;  // (the grouped dT walk: slots 16, 17)
                     walk(s_mask + ((tid & ~63) + owner), ol, ox, oy, gfilter(G, lane & (G - 1)), work,
                          each([&](float alpha, float t_peak, float rs, float, float) {
                              const float t_delta = (ot - t_peak) * rs;

@@ -774,7 +774,7 @@ def _audit_full_images(c, out, o, report=None):
     md_rest = np.where(tie_px, 0.0, rel)
     cand = np.argwhere(md_rest > 1e-5)
     order = np.argsort(-md_rest[cand[:, 0], cand[:, 1]]) if len(cand) else np.zeros(0, np.int64)
-    md_margin, n_md_small_ties = 0.0, 0
+    md_margin, n_md_small_ties, n_md_chain_ties = 0.0, 0, 0
     for i, k in enumerate(order):
         y, x = cand[k]
         if i >= 400:
@@ -783,11 +783,16 @@ def _audit_full_images(c, out, o, report=None):
         tg, to = ch.depth_of(int(x), int(y), md_g[y, x]), ch.depth_of(int(x), int(y), md_o[y, x])
         if FA.mdepth_flip_margin(ch, int(x), int(y), tg, to) <= 1e-4:
             n_md_small_ties += 1
+        elif FA.chain_margin(ch, int(x), int(y), int(max(nc_gpu[y, x], nc_orc[y, x])) + 1) <= 2e-4:
+            # a contributor's skip test at a tie (C3 px (285, 296): alpha 1/255 - 2e-10 in float64, in fp32
+            # 1/255 + 6e-10 — the oracle walks it, the GPU does not; its factor moves T by 6e-4 at the root)
+            n_md_chain_ties += 1
         else:
             md_margin = max(md_margin, float(md_rest[y, x]))
     if not len(cand):
         md_margin = float(md_rest.max()) if md_rest.size else 0.0
     rep["mdepth_small_ties"] = n_md_small_ties
+    rep["mdepth_small_composite_ties"] = n_md_chain_ties
     margins = {"mdepth rel (per pixel, outside ties)": (md_margin, 1e-4)}
     T_px = 1.0 - alpha.cpu().numpy()[0].astype(np.float64)
     for name, t in (("color", color), ("alpha", alpha), ("normal", normal)):

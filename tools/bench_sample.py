@@ -90,6 +90,10 @@ if os.environ.get("SAMPLE_STATS"):  # the SAMPLE raster's counters (and, in a -D
     print("walk wave-steps", s[0], "active lanes/step", round(s[1] / max(s[0], 1), 2), "composite wave-steps", s[2],
           "blending lanes/step", round(s[3] / max(s[2], 1), 2), "refine waves", s[4], "pass waves", s[5],
           "root updates", s[6], "lanes left", s[7], "dT walked exactly (loose continuation)", s[19])
+    if not s[15]:  # (no clock build) walk wave-steps and active lanes per walk index, and the grouped dT walk
+        print("per walk: " + ", ".join(f"{name} {s[8 + 2 * k]} steps x {s[9 + 2 * k] / max(s[8 + 2 * k], 1):.1f} lanes"
+                                       for k, name in enumerate(("walk1", "walk2", "walk3", "walk4+ and passes", "dT group")))
+              + f"; passes etc. {s[0] - sum(s[8 + 2 * k] for k in range(5))} steps")
     if s[15]:
         for k, name in enumerate(("composite", "masks/staging", "probe walk", "Halley walks", "passes", "-", "-")):
             print(f"clock {name}: {s[8 + k]:.4g} ({s[8 + k] / s[15]:.3f})")
