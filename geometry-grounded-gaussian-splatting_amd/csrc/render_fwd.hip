@@ -255,6 +255,9 @@ constexpr float kLooseTol = GSR_LOOSE_TOL;
 constexpr float kCurvTol = GSR_CURV_TOL;
 constexpr float kCondTol = 1e-6f;   // conditioning threshold (as the previous scheme's tolerance)
 constexpr float kTwoLn2 = 1.38629436111989061883f;
+#ifndef GSR_ILL_NEWTON
+#define GSR_ILL_NEWTON 1
+#endif
 #ifndef GSR_HNOISE
 #define GSR_HNOISE 1e-5f
 #endif
@@ -998,14 +1001,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
             bool lo_ev, hi_ev;  // lo / hi set by an evaluation of T (not the window's unevaluated ends)
             float ref_F;        // the last walk's curvature bound F (sum |H'' terms|)
         };
-#ifdef GSR_DBG_PX
+#ifdef GSR_DBG_ROOT
         bool dbg_here = false;  // (development: the walked pixel is the traced one)
 #endif
         // One walk's update of a live pixel: log2 T, its derivatives -D, E and the curvature bound F at t
         // (the products and sums of the walk), the bracket, the Halley iterate, and acceptance.
         auto root_update = [&](Refine& r, bool& live, float& t, float& lo, float& hi, float A, float B, float D, float E,
                                float F, float scale) {
-#ifdef GSR_DBG_PX
+#ifdef GSR_DBG_ROOT
             if (dbg_here)
                 printf("root_update lane %d t %.7f H %g D %g E %g F %g [%.7f %.7f]\n", (int)(threadIdx.x & 63), t,
                        __builtin_fmaf(-0.5f, __builtin_amdgcn_logf(B), __builtin_amdgcn_logf(A)) + 1.f, D, E, F, lo, hi);
@@ -1043,7 +1046,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                 const bool smooth = fabsf(r.t_ref - t) * F <= kCurvTol * D;
                 r.refined = D * tol_cond >= kHNoise && smooth;
                 // (an ill-conditioned root only where T itself is at 1/2: converged by the Newton step)
-                r.ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
+                bool ill = GSR_ILL_ACCEPT && !r.refined && newton && D * (kIllTol * scale) >= kHNoise;
+                if (GSR_ILL_NEWTON && ill && !smooth) {
+                    // A Halley step long against the curvature length crossed a splat's peak, where H''
+                    // flips sign: its iterate is not the root (W16400 case, px (14729, 10): t 5.6e-5
+                    // Newton steps before the root next to a peak, H H'' / H'^2 = 0.76, the Halley
+                    // iterate 1.8e-4 past the root).  The Newton iterate is within F (H / H')^2 / (2 |H'|)
+                    // of it; kept where that is within kIllTol, else the lane takes the reference's passes.
+                    const float sN = fast_div(H, D);
+                    r.t_ref = fminf(fmaxf(t + sN, lo), hi);
+                    ill = F * sN * sN <= 2.f * D * (kIllTol * scale);
+                }
+                r.ill = ill;
                 r.newton_done = newton;
                 live = false;
                 r.ref_t = t;
@@ -1064,7 +1078,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                 f32x2 AE[1] = {f32x2{1.f, 1.f}}, BE[1] = {f32x2{1.f, 1.f}};
                 float unusedA = 1.f, unusedB = 1.f;
                 const PixSrc ps = src();
-#ifdef GSR_DBG_PX
+#ifdef GSR_DBG_ROOT
                 dbg_here = ps.x == (float)GSR_DBG_PX && ps.y == (float)GSR_DBG_PY;
 #endif
                 if (ends && k == 0) {

@@ -5,7 +5,7 @@ set -o pipefail
 S=${1:-20}
 for lib in default ab_libs/*.so; do
   if [ "$lib" = default ]; then unset GSR_LIB; else export GSR_LIB=$(pwd)/$lib; fi
-  timeout -k 10 200 python tools/ab_option.py 4 0 $S > gpurun_out/ablib.log 2>&1 || exit 1
+  timeout -k 10 200 python tools/ab_option.py 1 0 $S > gpurun_out/ablib.log 2>&1 || exit 1
   python3 -c "
 import json
 for l in open('gpurun_out/ablib.log'):
