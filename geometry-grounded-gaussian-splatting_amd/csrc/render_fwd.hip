@@ -27,7 +27,14 @@
 // Contraction is off for this file: every fma below is written out, so each
 // template instance (plain, GSR_OPT_RENDER_STATS, the sample queries) rounds
 // identically.
+#ifndef GSR_FWD_CONTRACT
+#define GSR_FWD_CONTRACT 0  // (development: 1 = contract(fast) outside the shared footprint helpers)
+#endif
+#if GSR_FWD_CONTRACT
+#pragma clang fp contract(fast)
+#else
 #pragma clang fp contract(off)
+#endif
 
 #include <type_traits>
 
@@ -288,9 +295,10 @@ __device__ __forceinline__ void refine_step(float& A, float& B, float& D, float&
     const float x = ag * __builtin_amdgcn_rcpf(omg);
     const float xs = x * sc;
     D = __builtin_fmaf(xs, fabsf(u), D);
-    const float e = (xs * sc) * __builtin_fmaf(-kTwoLn2 * u2, 1.f + x, 1.f);
-    E += behind ? -e : e;
-    F += fabsf(e);  // bounds |H''| on either side of every splat peak (where H'' jumps)
+    const float xsc = xs * sc;
+    const float p = __builtin_fmaf(-kTwoLn2 * u2, 1.f + x, 1.f);
+    E = __builtin_fmaf(behind ? -xsc : xsc, p, E);
+    F = __builtin_fmaf(xsc, fabsf(p), F);  // bounds |H''| on either side of every splat peak (where H'' jumps)
 }
 
 // refine_step for the walk's two contributors at once, in the halves of packed registers: every product
@@ -313,9 +321,11 @@ __device__ __forceinline__ void refine_step2(f32x2& A, f32x2& B, f32x2& D, f32x2
     const f32x2 x = ag * f32x2{__builtin_amdgcn_rcpf(omg.x), __builtin_amdgcn_rcpf(omg.y)};
     const f32x2 xs = x * sc;
     D = f32x2{__builtin_fmaf(xs.x, fabsf(u.x), D.x), __builtin_fmaf(xs.y, fabsf(u.y), D.y)};
-    const f32x2 e = (xs * sc) * __builtin_elementwise_fma(f32x2{-kTwoLn2, -kTwoLn2} * u2, one + x, one);
-    E += f32x2{bx ? -e.x : e.x, by ? -e.y : e.y};
-    F = f32x2{F.x + fabsf(e.x), F.y + fabsf(e.y)};
+    // the H'' term e = xsc p, fused into its two sums (xsc >= 0: |e| = xsc |p|)
+    const f32x2 xsc = xs * sc;
+    const f32x2 p = __builtin_elementwise_fma(f32x2{-kTwoLn2, -kTwoLn2} * u2, one + x, one);
+    E = __builtin_elementwise_fma(f32x2{bx ? -xsc.x : xsc.x, by ? -xsc.y : xsc.y}, p, E);
+    F = f32x2{__builtin_fmaf(xsc.x, fabsf(p.x), F.x), __builtin_fmaf(xsc.y, fabsf(p.y), F.y)};
 }
 
 // An opaque copy of v: the compiler cannot prove it equal to v, so values

@@ -774,7 +774,9 @@ def _audit_full_images(c, out, o, report=None):
     md_rest = np.where(tie_px, 0.0, rel)
     cand = np.argwhere(md_rest > 1e-5)
     order = np.argsort(-md_rest[cand[:, 0], cand[:, 1]]) if len(cand) else np.zeros(0, np.int64)
-    md_margin, n_md_small_ties, n_md_chain_ties = 0.0, 0, 0
+    # (the pixels at or below 1e-5 are not examined: the largest of them is the floor of the margin)
+    md_margin = float(np.where(md_rest <= 1e-5, md_rest, 0.0).max()) if md_rest.size else 0.0
+    n_md_small_ties, n_md_chain_ties = 0, 0
     for i, k in enumerate(order):
         y, x = cand[k]
         if i >= 400:
