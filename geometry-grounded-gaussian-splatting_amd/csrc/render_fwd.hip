@@ -1012,7 +1012,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
             float ref_F;        // the last walk's curvature bound F (sum |H'' terms|)
         };
 #ifdef GSR_DBG_ROOT
-        bool dbg_here = false;  // (development: the walked pixel is the traced one)
+        // (development: the walked pixel is the traced one.  Build the trace with -DGSR_FWD_WAVES=5: at 6 waves
+        // per SIMD the printf call spills registers, and that build loses values in unrelated tiles — DESIGN §5)
+        bool dbg_here = false;
 #endif
         // One walk's update of a live pixel: log2 T, its derivatives -D, E and the curvature bound F at t
         // (the products and sums of the walk), the bracket, the Halley iterate, and acceptance.
@@ -1089,7 +1091,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                 float unusedA = 1.f, unusedB = 1.f;
                 const PixSrc ps = src();
 #ifdef GSR_DBG_ROOT
-                dbg_here = ps.x == (float)GSR_DBG_PX && ps.y == (float)GSR_DBG_PY;
+#ifndef GSR_DBG_ROOT_PX
+#define GSR_DBG_ROOT_PX GSR_DBG_PX
+#define GSR_DBG_ROOT_PY GSR_DBG_PY
+#endif
+                dbg_here = ps.x == (float)GSR_DBG_ROOT_PX && ps.y == (float)GSR_DBG_ROOT_PY;
 #endif
                 if (ends && k == 0) {
                     walk(ps.mask, ps.plast, ps.x, ps.y, ps.filter, live,
