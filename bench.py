@@ -342,6 +342,13 @@ def exchange_pattern(mode, P, shm, sgm, world, chunks, dev):
     return post, (2 * ring * geo.numel() + ring * gathered.numel()) * 4
 
 
+def _max_over_ranks(t):
+    """MAX over the ranks in place (gsr_dist's collective: RCCL on the device; the gloo rehearsal staged
+    through host memory, as gsr_dist does for every gloo collective on device tensors)."""
+    from gsr_dist import _all_reduce
+    _all_reduce(t, dist.ReduceOp.MAX, None)
+
+
 def time_exchange(mode, P, shm, sgm, world, chunks, dev, reps=10):
     post, bus_bytes = exchange_pattern(mode, P, shm, sgm, world, chunks, dev)
     for _ in range(2):
@@ -356,7 +363,7 @@ def time_exchange(mode, P, shm, sgm, world, chunks, dev, reps=10):
     torch.cuda.synchronize(dev)
     ms = (time.perf_counter() - t0) / reps * 1e3
     t = torch.tensor([ms], device=dev, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    _max_over_ranks(t)
     ms = float(t.item())
     return {"isolated_ms": round(ms, 4), "bus_bytes_per_rank": int(bus_bytes),
             "bus_GBps": round(bus_bytes / (ms * 1e-3) / 1e9, 2)}
@@ -726,7 +733,7 @@ def main():
     stages = _C.timing_collect()
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _max_over_ranks(t)
         elapsed = float(t.item())
     dist_info = None
     if world > 1:  # the exchange's cost: the same steps without it, and its collectives alone
@@ -743,7 +750,7 @@ def main():
         torch.cuda.synchronize(dev)
         dist.barrier()
         t = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _max_over_ranks(t)
         ms_noex = float(t.item()) / args.steps * 1e3
         state["no_exchange"] = False
         if overlap is not None:

@@ -26,6 +26,55 @@ import torch
 import torch.distributed as dist
 
 
+def _host_staged(group, *tensors) -> bool:
+    """gloo with device tensors (the one-GPU rehearsal of the N > 1 path; the product backend is RCCL):
+    the collective is staged through host memory here, by blocking copies, instead of by the backend.
+    torch's own staging of device tensors for gloo (an asynchronous copy into a pinned buffer on a side
+    stream) was observed to hand the reduction stale data — at 8 ranks, 6 of 1200 trials of the
+    exchange's pattern wrong without the rasterizer, always the first slice posted after the previous
+    trial's works were dropped, identically on every rank; 0 of 1200 staged by blocking copies
+    (tools/dbg/gloo_reuse_probe.py) — which is what the C4 test's rare wrong sum was."""
+    return any(t.is_cuda for t in tensors) and dist.get_backend(group) == "gloo"
+
+
+class _StagedWork:
+    """An async collective on host copies: wait() waits for it, then copies the result back to the device
+    tensor (stream-ordered on the caller's stream)."""
+
+    def __init__(self, work, dst: torch.Tensor, host: torch.Tensor):
+        self._work, self._dst, self._host = work, dst, host
+
+    def wait(self):
+        self._work.wait()
+        if self._dst is not None:
+            self._dst.copy_(self._host)
+            self._dst = None
+        return True
+
+
+def _all_reduce(t: torch.Tensor, op, group, async_op: bool = False):
+    if not _host_staged(group, t):
+        return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+    h = t.cpu()  # (blocking: after the work queued on the stream before it)
+    w = _StagedWork(dist.all_reduce(h, op=op, group=group, async_op=True), t, h)
+    if async_op:
+        return w
+    w.wait()
+    return None
+
+
+def _all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group, async_op: bool = False):
+    if not _host_staged(group, out, inp):
+        return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+    hi = inp.cpu()
+    ho = torch.empty(out.shape, dtype=out.dtype)
+    w = _StagedWork(dist.all_gather_into_tensor(ho, hi, group=group, async_op=True), out, ho)
+    if async_op:
+        return w
+    w.wait()
+    return None
+
+
 def _coalescing(group, tensors):
     """torch's coalescing manager (one allreduce_coalesced for several
     tensors) where the backend has it for these tensors: RCCL does; gloo
@@ -89,8 +138,7 @@ class ViewParallelGrads:
                     grads.append(p.grad)
             if cm_fn is None or len(grads) < 2:
                 for g in grads:
-                    self._work.append((None, dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
-                                                             async_op=async_op)))
+                    self._work.append((None, _all_reduce(g, dist.ReduceOp.SUM, self.group, async_op)))
             else:
                 with cm_fn(group=self.group, async_ops=async_op) as cm:  # fast path: allreduce_coalesced
                     for g in grads:
@@ -101,7 +149,7 @@ class ViewParallelGrads:
             return
         for i in range(len(self.buckets)):
             flat = self._pack(i)
-            w = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            w = _all_reduce(flat, dist.ReduceOp.SUM, self.group, async_op)
             self._work.append((i, w))
         if not async_op:
             self.finish()
@@ -249,7 +297,7 @@ class FactoredViewGrads:
         self._buf[:3 * P].view(P, 3).copy_(dc[:, 0, :])
         self._buf[3 * P:3 * P + 3].copy_(campos.reshape(3))
         self._check_contract(sh_degree, sg_degree)
-        work = dist.all_gather_into_tensor(self._gathered, self._buf, group=self.group, async_op=True)
+        work = _all_gather_into_tensor(self._gathered, self._buf, self.group, async_op=True)
         self.geometry.all_reduce()
         work.wait()
         sgo = []
@@ -403,16 +451,15 @@ class OverlappedViewGrads:
         self._campos_local[:3].copy_(campos.reshape(3))
         self._active = True
         if sh_path:
-            self._works.append(dist.all_gather_into_tensor(self._campos_all, self._campos_local, group=self.group,
-                                                           async_op=True))
+            self._works.append(_all_gather_into_tensor(self._campos_all, self._campos_local, self.group,
+                                                       async_op=True))
 
     def _post(self, b: int, e: int, rows, dc_in) -> None:
         """One range's collectives, in the order every rank posts them."""
         if not self._ar_done:
             cm_fn = _coalescing(self.group, rows)
             if cm_fn is None:
-                self._works += [dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-                                for t in rows]
+                self._works += [_all_reduce(t, dist.ReduceOp.SUM, self.group, async_op=True) for t in rows]
             else:
                 with cm_fn(group=self.group, async_ops=True) as cm:
                     for t in rows:
@@ -421,8 +468,8 @@ class OverlappedViewGrads:
             self._ar_done = True
         if self._sh:
             W = self.world
-            self._works.append(dist.all_gather_into_tensor(self._gathered[3 * W * b:3 * W * e], dc_in,
-                                                           group=self.group, async_op=True))
+            self._works.append(_all_gather_into_tensor(self._gathered[3 * W * b:3 * W * e], dc_in, self.group,
+                                                       async_op=True))
         self._ar_done = False
         self._next = e
 
@@ -520,7 +567,7 @@ class OverlappedViewGrads:
         if self._status is None or self._status.device != torch.device(dev):
             self._status = torch.zeros(1, dtype=torch.float32, device=dev)
         self._status.fill_(1.0 if failed else 0.0)
-        self._works.append(dist.all_reduce(self._status, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
+        self._works.append(_all_reduce(self._status, dist.ReduceOp.MAX, self.group, async_op=True))
 
     def finish(self, grads, means3D, sg_axis, sg_sharpness, sg_color, sh_degree: int, sg_degree: int) -> None:
         """`grads`: the backward's 11 gradients (+ dsh_rest, the split SH layout)."""
@@ -562,7 +609,7 @@ class OverlappedViewGrads:
             return
         dev = self._campos_local.device if self._campos_local is not None else "cpu"
         t = torch.tensor(sums + [-x for x in sums], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        _all_reduce(t, dist.ReduceOp.MAX, self.group)
         n = len(sums)
         hi, lo = t[:n], -t[n:]
         if not bool(torch.equal(hi, lo)):
@@ -577,6 +624,6 @@ def reduce_densification_stats(grad_norm_accum: torch.Tensor, denom: torch.Tenso
     (gaussian_model.py:818-821, train.py:236): sums for the accumulated
     screen-space gradient norms and visibility counts, max for the radii.
     Called only at densification steps (every 100 iterations), not per step."""
-    dist.all_reduce(grad_norm_accum, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(denom, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX, group=group)
+    _all_reduce(grad_norm_accum, dist.ReduceOp.SUM, group)
+    _all_reduce(denom, dist.ReduceOp.SUM, group)
+    _all_reduce(max_radii2D, dist.ReduceOp.MAX, group)

@@ -414,11 +414,11 @@ def _full_rank_worker(rank, world, port, outdir, P, sg_degree, views, forms, chu
     dkeys = ["means3D", "opacities", "scales", "rotations", "shs"]
     plain_sums = {k: _range_sums(plain[k] if k != "shs" else plain[k][:, 0], ranges).cpu().tolist() for k in dkeys}
     want = {}
-    for k in keys:  # the yardstick: sum over the views in float64
-        w = plain[k].double()
+    for k in keys:  # the yardstick: sum over the views in float64 (reduced on host copies: gloo's own staging
+        w = plain[k].double().cpu()  # of device tensors is what the round-5 wrong sum was)
         if w.numel():
             dist.all_reduce(w)
-        want[k] = w
+        want[k] = w.to(dev)
     del plain
     res = {"rank": rank, "visible": n_vis, "forms": {}}
     for form in forms:
