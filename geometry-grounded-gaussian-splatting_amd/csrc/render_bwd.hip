@@ -480,8 +480,11 @@ __global__ void __launch_bounds__(128 / NP) __attribute__((amdgpu_waves_per_eu(N
 #if GSR_TIME_BWD_PROBE == 2
             if (field_lane && red == 1234.5f && abs_red == 1.f && g == 7u) a.acc[lane] = red;
 #else
-            if (field_lane) atomicAdd(a.acc + (size_t)g * kAccFields + (lane >> 2), red);
-            if (lane == 1) atomicAdd(a.acc_abs + g, abs_red);
+            // one atomic instruction for both: as two, the |dmean2D| lane's uniform address made the
+            // compiler wrap its atomic in the atomic optimizer's scalar lane loop on every step
+            if (field_lane || lane == 1)
+                atomicAdd(lane == 1 ? a.acc_abs + g : a.acc + (size_t)g * kAccFields + (lane >> 2),
+                          lane == 1 ? abs_red : red);
 #endif
         }
     }
