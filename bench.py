@@ -77,8 +77,28 @@ def launcher_cmd(argv, nproc: int, port: int):
 
 
 def free_port() -> int:
+    """A free port for the launcher's rendezvous, outside the kernel's ephemeral range (a port picked by
+    binding to 0 is ephemeral, and outgoing connections can take it again before the launcher binds it)."""
+    import random
     import socket
 
+    lo = 32768
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        pass
+    rng = random.Random()
+    for _ in range(256):
+        p = rng.randrange(10000, max(10001, lo))
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]

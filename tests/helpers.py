@@ -116,3 +116,34 @@ def gpu_n_contrib_for_oracle(out, o, H, W):
     assert np.array_equal(okey[srt][at], want), "GPU contributor missing from the oracle's tile list"
     res[has] = opos[srt][at] + 1
     return res.astype(np.uint32)
+
+
+def free_port() -> int:
+    """A free TCP port for a process group's rendezvous, outside the kernel's ephemeral range: a port picked
+    by binding to port 0 is an ephemeral one, and the gloo connections an earlier multi-rank test left in
+    their last states take ephemeral ports too — one was taken again between the pick and the ranks' bind
+    (EADDRINUSE at the C5 8-rank test's rendezvous, round 6)."""
+    import random
+    import socket
+    lo = 32768
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        pass
+    rng = random.Random()
+    for _ in range(256):
+        p = rng.randrange(10000, max(10001, lo))
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p

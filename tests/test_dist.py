@@ -5,7 +5,6 @@ equal to a single-process sum."""
 from __future__ import annotations
 
 import os
-import socket
 import sys
 
 import torch
@@ -19,11 +18,8 @@ ROOT = os.path.dirname(HERE)
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    import helpers as Hh
+    return Hh.free_port()  # (outside the ephemeral range: see helpers.free_port)
 
 
 def _view_grads(view):

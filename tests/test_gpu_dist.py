@@ -309,13 +309,10 @@ def test_two_ranks_exchange_sums_views_on_gpu(tmp_path, sg_degree):
     give both ranks the same gradients, equal to the sum of the two views'
     plain gradients (rel. L2 <= 1e-5: the geometry rows are sums in another
     order, the colour rows are rebuilt from the gathered DC rows)."""
-    import socket
     import torch.multiprocessing as mp
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    import helpers as Hh
+    port = Hh.free_port()
     mp.start_processes(_two_rank_worker, args=(2, port, str(tmp_path), sg_degree), nprocs=2, join=True,
                        start_method="spawn")
     r0 = torch.load(tmp_path / "g0.pt", weights_only=True)
@@ -505,13 +502,10 @@ def _print_overlap_diagnosis(rs) -> None:
 
 def _run_full_ranks(tmp_path, world, P, sg_degree, views, forms, chunks=4):
     import json
-    import socket
     import torch.multiprocessing as mp
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    import helpers as Hh
+    port = Hh.free_port()
     mp.start_processes(_full_rank_worker, args=(world, port, str(tmp_path), P, sg_degree, views, forms, chunks),
                        nprocs=world, join=True, start_method="spawn")
     rs = [json.load(open(tmp_path / f"full{r}.json")) for r in range(world)]
@@ -631,13 +625,10 @@ def test_train_step_split_sh_through_overlapped_exchange(tmp_path):
     loss on the render outputs gives every raw parameter (through the fused
     getters) the sum over the two views of its plain gradient, identically on
     both ranks; and a whole TrainStep runs with the exchange installed."""
-    import socket
     import torch.multiprocessing as mp
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    import helpers as Hh
+    port = Hh.free_port()
     mp.start_processes(_train_rank_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
     r = [torch.load(tmp_path / f"t{k}.pt", weights_only=True) for k in range(2)]
     assert r[0]["finite"] and r[1]["finite"]
