@@ -236,6 +236,9 @@ constexpr int kSampleWalks = GSR_SAMPLE_WALKS;
 #define GSR_SAMPLE_DT_TOL 0.004f  // (SAMPLE) longest step, relative to the curvature length, dT/dt_m is continued over
 #endif
 constexpr float kSampleDtTol = GSR_SAMPLE_DT_TOL;
+#ifndef GSR_SAMPLE_PASS_GROUP
+#define GSR_SAMPLE_PASS_GROUP 1  // (SAMPLE) the passes and the exact dT/dt_m walk of left points in lane groups
+#endif
 #ifndef GSR_SAMPLE_NO_ENDS
 #define GSR_SAMPLE_NO_ENDS 1  // (round 5: sample_fwd 0.839-0.844 -> 0.792-0.812 ms at the sample bench; 2 more of 1.27M points to the passes)
 #endif
@@ -898,6 +901,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
         float t_ref = 0.f;
         float ref_t = 0.f, ref_D = 0.f, ref_E = 0.f;  // the last refinement walk's depth, -H', H''
         bool dt_loose = false;  // (SAMPLE) refined, but dT/dt_m continued over too long a step: walked exactly
+        float dT_pre = 0.f;  // (SAMPLE, GSR_SAMPLE_GUESS) a refined root's continued dT/dt_m
+        bool passed_grp = false;  // (SAMPLE) left to the passes, which ran in lane groups: median depth in t_ref
         // one pass of the reference's bisection (render_forward.cu:560-645) over
         // the lanes still in range and not refined; FIRST evaluates all 9
         // samples, later passes reuse the bracketing ends
@@ -1807,6 +1812,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                 // (sample_backward.cu:77-140) sat at the 1e-4 bar (drotations, P600-W96-H64-seed1) — so a
                 // root whose step is longer than kSampleDtTol of the curvature length gets the exact walk
                 dt_loose = refined && fabsf(r.t_ref - r.ref_t) * r.ref_F > kSampleDtTol * r.ref_D;
+                // (the continued dT/dt_m of the other refined roots taken here, as below: the passes' lane
+                // groups then need no continuation state; in_range and t_ref of a refined lane stand)
+                const float mb_r = in_range ? t_ref : 0.f;
+                dT_pre = refined && mb_r != 0.f
+                             ? (0.5f * 0.69314718055994530942f) * __builtin_fmaf(ref_E, mb_r - ref_t, -ref_D) : 0.f;
                 if constexpr (STATS && !kClock) st[19] += dt_loose ? 1 : 0;
                 stamp(4);
             } else {
@@ -1828,11 +1838,71 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                 if constexpr (STATS) {
                     if ((tid & 63) == 0) st[5] += 1;
                 }
-                dmin = win_lo();
-                dmax = win_hi();
-                pass(std::true_type{}, own_src, 1, true);
+                const int npass = max(a.passes, kSplitIterations);
+                if (GSR_SAMPLE_PASS_GROUP && resident) {
+                    // The wave's left points dealt to groups of 16 lanes, 4 points a round: lane q of a group
+                    // walks the contributors of index % 16 == q of its point (gfilter) and the group combines
+                    // by DPP (gprod) — a fixed group size, so a point's values do not depend on how many
+                    // other points of its wave are left (the scratch-split test holds them bit for bit);
+                    // the results go back to the owners by __shfl.  Instead of 5 passes with ~5 lanes live.
+                    // (few registers stay live across the rounds: the lanes' flags as wave masks, each left
+                    // point's median depth returned into its t_ref, which only refined lanes use)
+                    const unsigned long long bl = __ballot(left);
+                    const unsigned long long m_in = __ballot(in_range), m_ref = __ballot(refined);
+                    unsigned long long m_rin = 0ull;
+                    const int n = __popcll(bl);
+                    const int lane = tid & 63;
 #pragma unroll 1
-                for (int it = 1; it < max(a.passes, kSplitIterations); it++) pass(std::false_type{}, own_src, 1, true);
+                    for (int base = 0; base < n; base += 4) {  // (wave-uniform)
+                        // (the owner of lane's group: the e-th left lane, found again at each use)
+                        auto owner_of = [&](int ln) {
+                            const int e = base + (ln >> 4);
+                            int owner = ln;
+                            unsigned long long m = bl;
+                            for (int i = 0; i < n; i++) {  // (scalar loop: the i-th left lane of the wave)
+                                const int o = __builtin_ctzll(m);
+                                m &= m - 1ull;
+                                owner = e == i ? o : owner;
+                            }
+                            return owner;
+                        };
+                        const int e = base + (lane >> 4);
+                        const int owner = owner_of(lane);
+                        auto gsrc = [&] {
+                            const int o = owner_of(opaque_int(lane));
+                            return PixSrc{s_mask + ((tid & ~63) + o), (uint32_t)__shfl((int)last, o, 64),
+                                          __shfl(lane_fx(), o, 64), __shfl(lane_fy(), o, 64), gfilter(16, lane & 15)};
+                        };
+                        const float om = __shfl(m_init, owner, 64);
+                        dmin = fmaxf(om - a.sample_range, 0.f);  // (win_lo, win_hi of the owner)
+                        dmax = fmaxf(om + a.sample_range, 0.f);
+                        in_range = e < n;
+                        refined = false;
+                        pass(std::true_type{}, gsrc, 16, true);
+#pragma unroll 1
+                        for (int it = 1; it < npass; it++) pass(std::false_type{}, gsrc, 16, true);
+                        // the median depth as the owner path below computes it
+                        float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
+                        w_max = fminf(fmaxf(w_max, 0.f), 1.f);
+                        const float md = in_range ? __builtin_fmaf(w_max, dmax, (1.f - w_max) * dmin) : 0.f;
+                        const int rank = __popcll(bl & ((1ull << lane) - 1ull));
+                        const int from = ((rank - base) << 4) & 63;
+                        const float md_o = __shfl(md, from, 64);
+                        const bool mine = ((bl >> lane) & 1ull) && rank >= base && rank < base + 4;
+                        const bool in_o = __shfl((int)in_range, from, 64) != 0;
+                        m_rin |= __ballot(mine && in_o);
+                        if (mine) t_ref = md_o;
+                    }
+                    refined = ((m_ref >> lane) & 1ull) != 0ull;
+                    in_range = ((((bl >> lane) & 1ull) ? m_rin : m_in) >> lane) & 1ull;
+                    passed_grp = left;
+                } else {
+                    dmin = win_lo();
+                    dmax = win_hi();
+                    pass(std::true_type{}, own_src, 1, true);
+#pragma unroll 1
+                    for (int it = 1; it < npass; it++) pass(std::false_type{}, own_src, 1, true);
+                }
             }
             if constexpr (SAMPLE) stamp(5);
         } else {
@@ -1864,7 +1934,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
             float w_max = (Tp[0] - 0.5f) / (Tp[0] - Tp[kSplit]);
             w_max = fminf(fmaxf(w_max, 0.f), 1.f);  // __saturatef (NaN -> 0)
             const float w_min = 1.f - w_max;
-            mDepth = in_range ? (refined ? t_ref : __builtin_fmaf(w_max, dmax, w_min * dmin)) : 0.f;
+            mDepth = in_range ? (refined || passed_grp ? t_ref : __builtin_fmaf(w_max, dmax, w_min * dmin)) : 0.f;
 
             // The backward's median-depth pre-pass (render_backward.cu:835-880),
             // done here while the blended set is still in LDS: dT/dt_m at the
@@ -1881,7 +1951,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
             }
             float dT_dtm = 0.f;
             const bool want_dT = !SAMPLE || a.query == kQuerySample;
-            if (refined && !dt_loose) {
+            if (SAMPLE && GSR_SAMPLE_GUESS && refined && !dt_loose) {
+                dT_dtm = dT_pre;
+            } else if (refined && !dt_loose) {
                 // the reference's dT/dt_m (render_backward.cu:876) is T H' ln2 = H' ln2 / 2 at T = 1/2;
                 // continued to mDepth_b from the last walk: H'(t) = -D + E (t - ref_t) (|t - ref_t| <= a
                 // Newton step of kRefineTol max(t, 1); the next term is ~(step / sigma)^2 relative)
@@ -1894,9 +1966,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
             // blended set, combined by DPP (gsum) and sent back to the owner — instead of every lane of
             // the wave waiting while the few loose ones walk their whole sets (a quarter of the points
             // are loose at the sample bench, in almost every wave)
+            // (GSR_SAMPLE_PASS_GROUP: the points the passes decided, whose dT/dt_m is the exact walk too)
             float dT_grp = 0.f;
+            const bool grp_dT = SAMPLE && (dt_loose || (GSR_SAMPLE_PASS_GROUP && !refined));
+            bool need = false;
             if constexpr (SAMPLE) {
-                const bool need = dt_loose && resident && want_dT && inside && mDepth_b != 0.f && last != 0;
+                need = grp_dT && resident && want_dT && inside && mDepth_b != 0.f && last != 0;
                 const unsigned long long bl = __ballot(need);
                 if (bl != 0ull) {  // (wave-uniform)
                     const int lane = tid & 63;
@@ -1928,8 +2003,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SAMPL
                     dT_grp = __shfl(d, __popcll(bl & ((1ull << lane) - 1ull)) << lg, 64);
                 }
             }
-            if (SAMPLE && dt_loose) {
-                dT_dtm = dT_grp;  // (a tile past the LDS cache: 0, and md_ok tells the backward to recompute)
+            if (grp_dT) {
+                dT_dtm = need ? dT_grp : 0.f;  // (a tile past the LDS cache: 0, and md_ok tells the backward to recompute)
             } else if (!refined && resident) {
                 lane_walk(want_dT && inside && mDepth_b != 0.f && last != 0,
                           each([&](float alpha, float t_peak, float rs, float, float) {

@@ -5,7 +5,7 @@ Locks in two properties DESIGN.md relies on:
     the median-depth walks lost register values through its spills in tiles that never took the call
     (DESIGN §5 item 14), so the product keeps calls out;
   * the register budgets quoted for the raster kernels: the render instances of render_fwd and the
-    render backward spill nothing; the SAMPLE instance (held at 7 waves per SIMD) spills at most 2.
+    render backward spill nothing; the SAMPLE instance (held at 7 waves per SIMD) spills at most 16.
 The code objects are taken from the library's .hip_fatbin section (clang offload bundles) and read
 with the ROCm LLVM tools; the test skips where the library or the tools are absent.
 """
@@ -99,6 +99,8 @@ def test_raster_register_budgets(code_objects):
     # render_bwd_kernel<GEOM, 2>: no spills
     for name, f in find(r"render_bwd_kernelILb[01]ELi2E").items():
         assert f.get("vgpr_spill_count", 0) == 0, (name, f)
-    # the SAMPLE instance at 7 waves per SIMD (72 VGPRs): at most 2 spilled registers
+    # the SAMPLE instance at 7 waves per SIMD (72 VGPRs): at most 16 spilled registers (12 since the passes
+    # run in lane groups: values saved around that branch, outside the walk loops; 6 waves per SIMD without
+    # spills measured slower)
     for name, f in find(r"render_fwd_kernelILb1ELb0ELb1E").items():
-        assert f.get("vgpr_spill_count", 0) <= 2 and f.get("vgpr_count", 999) <= 72, (name, f)
+        assert f.get("vgpr_spill_count", 0) <= 16 and f.get("vgpr_count", 999) <= 72, (name, f)
