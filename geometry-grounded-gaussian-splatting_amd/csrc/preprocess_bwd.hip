@@ -206,9 +206,20 @@ __device__ __forceinline__ void wave_load_rows(const float* __restrict__ g, floa
 // A wave's n consecutive rows of nf floats each, staged in LDS in the
 // global layout, written out as whole-wave 16-B pieces: one store
 // instruction covers 1 KB of consecutive bytes instead of 64 rows.
+// (GSR_PBWD_NT: non-temporal stores — the gradient rows are read next by the optimizer step, after the
+// whole backward has streamed through the caches)
+#ifndef GSR_PBWD_NT
+#define GSR_PBWD_NT 1
+#endif
+typedef float pbwd_f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void wave_store_rows(float* __restrict__ g, const float* __restrict__ l, int nf, int lane) {
     const int n4 = nf >> 2;
-    for (int c = lane; c < n4; c += 64) reinterpret_cast<float4*>(g)[c] = reinterpret_cast<const float4*>(l)[c];
+    for (int c = lane; c < n4; c += 64) {
+        if constexpr (GSR_PBWD_NT)
+            __builtin_nontemporal_store(reinterpret_cast<const pbwd_f4*>(l)[c], reinterpret_cast<pbwd_f4*>(g) + c);
+        else
+            reinterpret_cast<float4*>(g)[c] = reinterpret_cast<const float4*>(l)[c];
+    }
     for (int c = (n4 << 2) + lane; c < nf; c += 64) g[c] = l[c];
 }
 
